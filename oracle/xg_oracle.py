@@ -1,0 +1,687 @@
+"""xg_oracle -- CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker.  The product (libxghost / libxg) never
+calls it.
+
+What it restates (every function cites the reference line it follows):
+  * aggregator placement            create_aggregator_list   mpi_test.c:1952-2006
+  * segment fingerprint             MAP_DATA / fill_buffer   mpi_test.c:23, :71-77
+  * buffer layouts                  prepare_*_data           mpi_test.c:94-133, :162-202
+  * alltoallw counts/displacements  *_alltoall_translate     mpi_test.c:233-302
+  * the per-rank MPI programs of methods 1..12                mpi_test.c:421-1950
+  * MPI point-to-point matching (non-overtaking per (src,dst,tag)) and
+    collective matching for MPI_Alltoallw, executed with byte copies.
+
+It is pinned against the real reference: tests/golden/ holds per-rank MPI
+call traces and received-segment checksums captured with oracle/pmpi_capture.c
+from the reference binary (tests/golden/make_golden.py); tests/test_oracle.py
+checks this module against every one of them.
+
+Program ops (one list per rank, in program order):
+  ('B',)                               MPI_Barrier before the timed region
+  ('s', peer, cnt, seg, blocking)      send post (Issend: blocking=False; Send / Sendrecv half: True)
+  ('r', peer, cnt, slot)               recv post (Irecv / Recv / Sendrecv half)
+  ('w', [post indices])                one completion point (Waitall / blocking call)
+  ('A', [(peer,cnt,seg)], [(peer,cnt,slot)])   MPI_Alltoallw (posts + completion)
+  ('c', seg, slot, cnt)                self memcpy (mpi_test.c:1473, :1646, :1714)
+  ('t', field, +1|-1)                  timer bracket: field in post|send|recv|total
+Post indices count 's' and 'r' ops (and the posts of an 'A') in program order.
+"""
+import numpy as np
+
+A2M_METHODS = (1, 3, 6, 7, 8, 9, 12)
+M2A_METHODS = (2, 4, 5, 10, 11)
+LABELS = {  # mpi_test.c:2186 ... :2271
+    1: "All to many", 2: "Many to all", 3: "All to many balanced", 4: "Many to all balanced",
+    5: "Many to all benchmark", 6: "All to many sync", 7: "All to many half sync",
+    8: "All to many benchmark", 9: "All to many pairwise", 10: "Many to all pairwise",
+    11: "Many to all half sync", 12: "All to many half sync 2",
+}
+
+
+def direction(method):
+    return "a2m" if method in A2M_METHODS else "m2a"
+
+
+# --------------------------------------------------------------------------- placement
+def aggregator_list(P, A, proc_node=1, agg_type=1):
+    """create_aggregator_list, mpi_test.c:1952-2006 (incl. the type-1 quirk remainder = P / A, :1957)."""
+    out = []
+    if agg_type == 1:
+        remainder, ceiling, floor = P // A, (P + A - 1) // A, P // A
+        for i in range(A):
+            out.append(ceiling * i if i < remainder else ceiling * remainder + floor * (i - remainder))
+    elif agg_type == 0:
+        out = list(range(A))
+    elif agg_type == 2:
+        remainder, ceiling, floor = P // A, (P + A - 1) // A, P // A
+        for i in range(A):
+            v = ceiling * i if i < remainder else ceiling * remainder + floor * (i - remainder)
+            out.append((v - 16 + P * 16) % P)
+    elif agg_type == 3:
+        remainder = 0
+        for i in range(A):
+            out.append(remainder)
+            remainder += proc_node
+            if remainder >= P:
+                remainder = remainder % proc_node + 1
+    else:  # the reference leaves rank_list uninitialised for other types
+        raise ValueError("aggregator type %d" % agg_type)
+    return out
+
+
+# --------------------------------------------------------------------------- bytes
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+GOLD = np.uint64(0x9E3779B97F4A7C15)
+LENK = 0xD6E8FEB86659FD93
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * M1
+    z = (z ^ (z >> np.uint64(27))) * M2
+    return z ^ (z >> np.uint64(31))
+
+
+def map_data(rank, seed, it, n):
+    """fill_buffer, mpi_test.c:71-77: byte o = (char)(rank + o + seed + iter)."""
+    return ((np.arange(n, dtype=np.int64) + (rank + seed + it)) & 0xFF).astype(np.uint8)
+
+
+def strong_data(rank, seed, it, n):
+    """Strong fingerprint (build extension, mode 1): byte o = byte (o&7) of
+    mix64(key + (o>>3) * GOLD), key = rank<<42 ^ seed<<21 ^ iter.  Makes every
+    (rank, seed, iter, offset) distinct, so a misroute the reference's weak
+    MAP_DATA cannot see (equal rank+seed) is caught."""
+    with np.errstate(over="ignore"):
+        key = np.uint64((rank << 42) ^ (seed << 21) ^ it)
+        nw = (n + 7) // 8
+        words = _mix64(key + np.arange(nw, dtype=np.uint64) * GOLD)
+    return words.view(np.uint8)[:n].copy()
+
+
+def fingerprint(mode, rank, seed, it, n):
+    return map_data(rank, seed, it, n) if mode == 0 else strong_data(rank, seed, it, n)
+
+
+def chk64(buf):
+    """xg_chk64: sum_q mix64(w_q ^ q*GOLD) + n*LENK (mod 2^64), w_q = LE u64 word q (zero padded)."""
+    buf = np.asarray(buf, dtype=np.uint8)
+    n = buf.size
+    nw = (n + 7) // 8
+    pad = np.zeros(nw * 8, dtype=np.uint8)
+    pad[:n] = buf
+    with np.errstate(over="ignore"):
+        w = pad.view("<u8")
+        h = _mix64(w ^ (np.arange(nw, dtype=np.uint64) * GOLD))
+        s = int(h.sum(dtype=np.uint64)) + n * LENK
+    return s & 0xFFFFFFFFFFFFFFFF
+
+
+# --------------------------------------------------------------------------- layouts
+def layout(method, P, A, rank_list):
+    """Per-rank (n_send_segs, n_recv_slots); prepare_all_to_many_data :162-202 /
+    prepare_many_to_all_data :94-133 (span = 1, so every segment is d bytes)."""
+    aggs = set(rank_list)
+    if direction(method) == "a2m":
+        return {r: (A, P if r in aggs else 0) for r in range(P)}
+    return {r: (P if r in aggs else 0, A) for r in range(P)}
+
+
+def seg_seed(method, rank, seg):
+    """Seed of send segment `seg` of `rank`: a2m seg index = aggregator index (:195-199);
+    m2a seg index = destination rank (:106-110)."""
+    return seg
+
+
+def expected_recv(method, P, A, d, rank_list, it, mode=0):
+    """Closed form of every receive slot: a2m aggregator index a, slot s <- MAP(s, seed=a);
+    m2a rank r, slot i <- MAP(rank_list[i], seed=r) (check_buffer call sites :139, :215)."""
+    out = {}
+    if direction(method) == "a2m":
+        for a, g in enumerate(rank_list):
+            out[g] = np.concatenate([fingerprint(mode, s, a, it, d) for s in range(P)]) if P else None
+    else:
+        for r in range(P):
+            out[r] = np.concatenate([fingerprint(mode, g, r, it, d) for g in rank_list])
+    return out
+
+
+# --------------------------------------------------------------------------- programs
+class _Prog:
+    def __init__(self):
+        self.ops = []
+        self.nposts = 0
+
+    def s(self, peer, cnt, seg, blocking=False):
+        self.ops.append(("s", peer, cnt, seg, blocking))
+        self.nposts += 1
+        return self.nposts - 1
+
+    def r(self, peer, cnt, slot):
+        self.ops.append(("r", peer, cnt, slot))
+        self.nposts += 1
+        return self.nposts - 1
+
+    def w(self, idxs):
+        self.ops.append(("w", list(idxs)))
+
+    def send(self, peer, cnt, seg):          # blocking MPI_Send
+        self.w([self.s(peer, cnt, seg, True)])
+
+    def recv(self, peer, cnt, slot):         # blocking MPI_Recv
+        self.w([self.r(peer, cnt, slot)])
+
+    def sendrecv(self, dst, scnt, seg, src, rcnt, slot):   # MPI_Sendrecv
+        a = self.s(dst, scnt, seg, True)
+        b = self.r(src, rcnt, slot)
+        self.w([a, b])
+
+    def t(self, field, sign):
+        self.ops.append(("t", field, sign))
+
+    def alltoallw(self, sends, recvs):
+        self.ops.append(("A", list(sends), list(recvs)))
+        self.nposts += len(sends) + len(recvs)
+
+
+def _window_start(idx, k, ceiling, floor, remainder):
+    # mpi_test.c:1463-1467 / :1478-1482 (even block split by aggregator index)
+    return k + idx * ceiling if idx < remainder else k + remainder * ceiling + (idx - remainder) * floor
+
+
+def _in_window(rank, temp, cs, P):
+    # the window test of mpi_test.c:1483-1499 (identical at :1617-1633), including its edge cases
+    if (temp >= P and temp + cs >= P) or (temp < P and temp + cs < P):
+        return temp % P <= rank < (temp + cs) % P
+    return rank >= temp or rank < (temp + cs) % P
+
+
+def programs(method, P, A, d, c, rank_list, ntimes):
+    """Per-rank op lists of method `method` exactly as the reference issues them."""
+    aggidx = {g: i for i, g in enumerate(rank_list)}
+    progs = []
+    for rank in range(P):
+        isagg = rank in aggidx
+        # prepare_*: myindex is the LAST matching index (:111-115, :183-187)
+        myindex = max(i for i, g in enumerate(rank_list) if g == rank) if isagg else 0
+        p = _Prog()
+        p.ops.append(("B",))
+        p.t("total", +1)
+        _METHODS[method](p, rank, isagg, myindex, P, A, d, c, rank_list, ntimes)
+        p.t("total", -1)
+        progs.append(p.ops)
+    return progs
+
+
+def _m1(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):          # all_to_many :1748-1824
+    for _ in range(ntimes):
+        if c >= P:
+            p.t("post", +1)
+            idx = []
+            if isagg:
+                idx += [p.r(i, d, i) for i in range(P)]
+            idx += [p.s(rl[i], d, i) for i in range(A)]
+            p.t("post", -1)
+            if idx:
+                p.t("recv", +1); p.w(idx); p.t("recv", -1)
+        else:
+            p.t("post", +1)
+            sends = [p.s(rl[i], d, i) for i in range(A)]
+            p.t("post", -1)
+            steps = (P + c - 1) // c
+            for k in range(steps):
+                idx = []
+                if isagg:
+                    p.t("post", +1)
+                    idx = [p.r(i, d, i) for i in range(k, P, steps)]
+                    p.t("post", -1)
+                if idx:
+                    p.t("recv", +1); p.w(idx); p.t("recv", -1)
+            if sends:
+                p.t("send", +1); p.w(sends); p.t("send", -1)
+
+
+def _m2(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):          # many_to_all :1871-1950
+    for _ in range(ntimes):
+        if c >= P:
+            p.t("post", +1)
+            idx = [p.r(rl[i], d, i) for i in range(A)]
+            if isagg:
+                idx += [p.s(i, d, i) for i in range(P)]
+            p.t("post", -1)
+            if idx:
+                p.t("recv", +1); p.w(idx); p.t("recv", -1)
+        else:
+            p.t("post", +1)
+            recvs = [p.r(rl[i], d, i) for i in range(A)]
+            p.t("post", -1)
+            steps = (P + c - 1) // c
+            for k in range(steps):
+                idx = []
+                if isagg:
+                    p.t("post", +1)
+                    idx = [p.s(i, d, i) for i in range(k, P, steps)]
+                    p.t("post", -1)
+                if idx:
+                    p.t("send", +1); p.w(idx); p.t("send", -1)
+            if recvs:
+                p.t("recv", +1); p.w(recvs); p.t("recv", -1)
+
+
+def _split(P, A):
+    return (P + A - 1) // A, P // A, P % A
+
+
+def _send_start(rank, ceiling, floor, remainder):                    # :1449-1453 / :1599-1603
+    if rank >= remainder * ceiling:
+        return remainder + (rank - remainder * ceiling) // floor
+    return rank // ceiling
+
+
+def _m3(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):          # all_to_many_balanced :1422-1517
+    if c > P:
+        c = P
+    bblock = c
+    ceiling, floor, remainder = _split(P, A)
+    send_start = _send_start(rank, ceiling, floor, remainder)
+    for _ in range(ntimes):
+        cs = bblock
+        k = 0
+        while k < P:
+            if P - k < cs:
+                cs = P - k
+            idx = []
+            if isagg:
+                for i in range(cs):
+                    temp = _window_start(myindex, k + i, ceiling, floor, remainder) % P
+                    if temp != rank:
+                        p.t("post", +1); idx.append(p.r(temp, d, temp)); p.t("post", -1)
+                    else:
+                        p.ops.append(("c", myindex, temp, d))
+            for _x in range(A):
+                temp = _window_start(send_start, k, ceiling, floor, remainder)
+                if _in_window(rank, temp, cs, P):
+                    if rl[send_start] != rank:
+                        idx.append(p.s(rl[send_start], d, send_start))
+                else:
+                    break
+                send_start = (send_start - 1 + A) % A
+            if idx:
+                fields = ("recv",) if isagg else ("recv", "send")
+                for f in fields:
+                    p.t(f, +1)
+                p.w(idx)
+                for f in fields:
+                    p.t(f, -1)
+            k += cs
+
+
+def _m4(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):          # many_to_all_balanced :1576-1663
+    cs = P if c > P else c          # NOT reset between repetitions (:1604-1608)
+    ceiling, floor, remainder = _split(P, A)
+    send_start = _send_start(rank, ceiling, floor, remainder)
+    for _ in range(ntimes):
+        k = 0
+        while k < P:
+            if P - k < cs:
+                cs = P - k
+            idx = []
+            p.t("post", +1)
+            for _x in range(A):
+                temp = _window_start(send_start, k, ceiling, floor, remainder)
+                if _in_window(rank, temp, cs, P):
+                    if rl[send_start] != rank:
+                        idx.append(p.r(rl[send_start], d, send_start))
+                else:
+                    break
+                send_start = (send_start - 1 + A) % A
+            if isagg:
+                for i in range(cs):
+                    temp = _window_start(myindex, k + i, ceiling, floor, remainder) % P
+                    if temp != rank:
+                        idx.append(p.s(temp, d, temp))
+                    else:
+                        p.ops.append(("c", temp, myindex, d))
+            p.t("post", -1)
+            if idx:
+                p.t("recv", +1); p.w(idx); p.t("recv", -1)
+            k += cs
+
+
+def _a2m_translate(rank, isagg, P, A, d, rl):                       # :233-262
+    sc, sd = [0] * P, [0] * P
+    for i in range(A):
+        sd[rl[i]] = i * d
+        sc[rl[i]] = d
+    rc, rd = ([d] * P, [i * d for i in range(P)]) if isagg else ([0] * P, [0] * P)
+    return sc, sd, rc, rd
+
+
+def _m2a_translate(rank, isagg, P, A, d, rl):                       # :273-302
+    rc, rd = [0] * P, [0] * P
+    rd[rl[0]] = 0
+    rc[rl[0]] = d
+    for i in range(1, A):
+        rd[rl[i]] = rd[rl[i - 1]] + d
+        rc[rl[i]] = d
+    sc, sd = ([d] * P, [i * d for i in range(P)]) if isagg else ([0] * P, [0] * P)
+    return sc, sd, rc, rd
+
+
+def _alltoallw(translate):
+    def run(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):       # :599-654 / :885-940
+        sc, sd, rc, rd = translate(rank, isagg, P, A, d, rl)
+        sends = [(q, sc[q], sd[q] // d if d else 0) for q in range(P) if sc[q] > 0]
+        recvs = [(q, rc[q], rd[q] // d if d else 0) for q in range(P) if rc[q] > 0]
+        for _ in range(ntimes):
+            p.alltoallw(sends, recvs)
+    return run
+
+
+def _m6(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):          # all_to_many_sync :1665-1746
+    cs = A if c > A else c
+    for _ in range(ntimes):
+        k = 0
+        while k < A:
+            if A - k < cs:
+                cs = A - k
+            p.t("recv", +1)
+            if isagg:
+                for i in range(cs):
+                    temp = (rank + k + i) % A
+                    temp2 = (myindex - k - i + A) % A
+                    if rl[temp] != rank and temp2 != rank:
+                        p.sendrecv(rl[temp], d, temp, temp2, d, temp2)
+                    elif rl[temp] == rank:
+                        p.ops.append(("c", temp, rank, d))
+                        if temp2 != rank:
+                            p.recv(temp2, d, temp2)
+                    elif temp2 == rank:
+                        p.send(rl[temp], d, temp)
+                    x = temp2 + A
+                    while x < P:
+                        if rank != x:
+                            p.recv(x, d, x)
+                        x += A
+            else:
+                for i in range(cs):
+                    temp = (rank + k + i) % A
+                    p.send(rl[temp], d, temp)
+            p.t("recv", -1)
+            k += cs
+
+
+def _m7(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):          # all_to_many_half_sync :1055-1114
+    cs = A if c > A else c
+    for _ in range(ntimes):
+        k = 0
+        while k < A:
+            if A - k < cs:
+                cs = A - k
+            idx = []
+            if isagg:
+                for i in range(cs):
+                    x = (myindex - k - i + A) % A
+                    while x < P:
+                        idx.append(p.r(x, d, x))
+                        x += A
+            for i in range(cs):
+                temp = (rank + k + i) % A
+                p.send(rl[temp], d, temp)
+            p.t("recv", +1)
+            if idx:
+                p.w(idx)
+            p.t("recv", -1)
+            k += cs
+
+
+def _m11(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):         # many_to_all_half_sync :942-997
+    cs = P if c > P else c
+    stride = (P + A - 1) // A
+    for _ in range(ntimes):
+        k = 0
+        while k < P:
+            if P - k < cs:
+                cs = P - k
+            idx = []
+            p.t("post", +1)
+            if isagg:
+                for i in range(cs):
+                    temp = (stride * myindex + k + i) % P
+                    idx.append(p.s(temp, d, temp))
+            p.t("post", -1)
+            p.t("recv", +1)
+            for x in range(cs):
+                for i in range(A):
+                    if rank == (k + i * stride + x) % P:
+                        p.recv(rl[i], d, i)
+            if idx:
+                p.w(idx)
+            p.t("recv", -1)
+            k += cs
+
+
+def _m12(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):         # all_to_many_half_sync2 :999-1053
+    cs = A if c > A else c
+    for _ in range(ntimes):
+        k = 0
+        while k < A:
+            if A - k < cs:
+                cs = A - k
+            idx = []
+            for i in range(cs):
+                temp = (rank + k + i) % A
+                idx.append(p.s(rl[temp], d, temp))
+            if isagg:
+                for i in range(cs):
+                    x = (myindex - k - i + A) % A
+                    while x < P:
+                        p.recv(x, d, x)
+                        x += A
+            p.t("recv", +1)
+            if idx:
+                p.w(idx)
+            p.t("recv", -1)
+            k += cs
+
+
+def _pairwise(translate):
+    def run(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):       # :421-508 / :510-597
+        sc, sd, rc, rd = translate(rank, isagg, P, A, d, rl)
+        i = 1
+        while i < P:
+            i *= 2
+        pof2 = i == P
+        for _ in range(ntimes):
+            for i in range(P):
+                if pof2:
+                    src = dst = rank ^ i
+                else:
+                    src, dst = (rank - i + P) % P, (rank + i) % P
+                p.sendrecv(dst, sc[dst], sd[dst] // d if sc[dst] else -1,
+                           src, rc[src], rd[src] // d if rc[src] else -1)
+    return run
+
+
+_METHODS = {
+    1: _m1, 2: _m2, 3: _m3, 4: _m4, 5: _alltoallw(_m2a_translate), 6: _m6, 7: _m7,
+    8: _alltoallw(_a2m_translate), 9: _pairwise(_a2m_translate), 10: _pairwise(_m2a_translate),
+    11: _m11, 12: _m12,
+}
+
+
+# --------------------------------------------------------------------------- traces
+def _idx_list(idxs):
+    idxs = sorted(idxs)
+    out, i = [], 0
+    while i < len(idxs):
+        j = i
+        while j + 1 < len(idxs) and idxs[j + 1] == idxs[j] + 1:
+            j += 1
+        out.append(str(idxs[i]) if i == j else "%d-%d" % (idxs[i], idxs[j]))
+        i = j + 1
+    return ",".join(out)
+
+
+def trace_tokens(ops, ntimes_split=False):
+    """Canonical token string, identical to the PMPI capture format (tests/golden/make_golden.py)."""
+    toks = []
+    for op in ops:
+        k = op[0]
+        if k == "B":
+            toks.append("B")
+        elif k == "s":
+            toks.append("s%d:%d" % (op[1], op[2]))
+        elif k == "r":
+            toks.append("r%d:%d" % (op[1], op[2]))
+        elif k == "w":
+            toks.append("w" + _idx_list(op[1]))
+        elif k == "A":
+            toks.append("A")
+    return " ".join(toks)
+
+
+# --------------------------------------------------------------------------- execution
+def match(progs):
+    """MPI matching.  Returns the message list [(src, seg, dst, slot, cnt, s_post, r_post)]
+    where s_post / r_post are the post indices at the sender / receiver.
+    Point-to-point: FIFO per (src, dst, tag=src+dst) (MPI non-overtaking).
+    Alltoallw: the k-th call of every rank forms one collective."""
+    from collections import defaultdict, deque
+    sends = defaultdict(deque)
+    recvs = defaultdict(deque)
+    coll_s = defaultdict(dict)   # k -> {(src,dst): (cnt, seg, post)}
+    coll_r = defaultdict(dict)
+    for r, ops in enumerate(progs):
+        post, ncoll = 0, 0
+        for op in ops:
+            if op[0] == "s":
+                sends[(r, op[1])].append((op[3], op[2], post)); post += 1
+            elif op[0] == "r":
+                recvs[(op[1], r)].append((op[3], op[2], post)); post += 1
+            elif op[0] == "A":
+                for q, cnt, seg in op[1]:
+                    coll_s[ncoll][(r, q)] = (cnt, seg, post); post += 1
+                for q, cnt, slot in op[2]:
+                    coll_r[ncoll][(q, r)] = (cnt, slot, post); post += 1
+                ncoll += 1
+    msgs = []
+    for key in sorted(set(sends) | set(recvs)):
+        s, rq = sends[key], recvs[key]
+        if len(s) != len(rq):
+            raise RuntimeError("unmatched point-to-point traffic on %s: %d sends, %d recvs" % (key, len(s), len(rq)))
+        for (seg, scnt, sp), (slot, rcnt, rp) in zip(s, rq):
+            if scnt > rcnt:
+                raise RuntimeError("message truncated on %s" % (key,))
+            msgs.append((key[0], seg, key[1], slot, scnt, sp, rp))
+    for k in coll_s:
+        if set(coll_s[k]) != set(coll_r[k]):
+            raise RuntimeError("alltoallw count mismatch")
+        for (src, dst), (cnt, seg, sp) in coll_s[k].items():
+            rcnt, slot, rp = coll_r[k][(src, dst)]
+            msgs.append((src, seg, dst, slot, cnt, sp, rp))
+    return msgs
+
+
+def execute(method, P, A, d, rank_list, progs, it, mode=0):
+    """Run the matched programs with byte copies; returns {rank: recv buffer (uint8)}."""
+    lay = layout(method, P, A, rank_list)
+    send = {r: np.concatenate([fingerprint(mode, r, seg_seed(method, r, s), it, d) for s in range(n)])
+            if n else np.zeros(0, np.uint8) for r, (n, _) in lay.items()}
+    recv = {r: np.full(m * d, 0xA5, np.uint8) for r, (_, m) in lay.items()}
+    for src, seg, dst, slot, cnt, _sp, _rp in match(progs):
+        if cnt:
+            recv[dst][slot * d: slot * d + cnt] = send[src][seg * d: seg * d + cnt]
+    for r, ops in enumerate(progs):
+        for op in ops:
+            if op[0] == "c":
+                _, seg, slot, cnt = op
+                recv[r][slot * d: slot * d + cnt] = send[r][seg * d: seg * d + cnt]
+    return recv
+
+
+MPICH_EAGER_LIMIT = 65424   # measured on the image's MPICH 3.3.2 ch3:nemesis
+
+
+def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT):
+    """Earliest-step schedule of the matched messages: a message moves in step
+    1 + max(step of every message completed by an earlier completion point of
+    EITHER endpoint before it was posted).  Issend is synchronous; a blocking
+    MPI_Send / MPI_Sendrecv send of <= eager_limit bytes completes locally (MPI
+    eager protocol), so it does not hold its sender's completion point.
+    Returns (step per message, n_steps).  Raises on a cycle (the reference
+    deadlocks there as well, e.g. m6 at P32 A14 d64KiB c3)."""
+    if msgs is None:
+        msgs = match(progs)
+    P = len(progs)
+    eager = set()
+    for r, ops in enumerate(progs):
+        post = 0
+        for op in ops:
+            if op[0] == "s":
+                if op[4] and op[2] <= eager_limit:
+                    eager.add((r, post))
+                post += 1
+            elif op[0] == "r":
+                post += 1
+            elif op[0] == "A":
+                post += len(op[1]) + len(op[2])
+    by_post = {}
+    for mi, (src, _seg, dst, _slot, _cnt, sp, rp) in enumerate(msgs):
+        by_post[(src, sp)] = mi
+        by_post[(dst, rp)] = mi
+    post_epoch = {}            # (rank, post) -> epoch of that rank when posted
+    step = [None] * len(msgs)
+    pc = [0] * P
+    epoch = [-1] * P
+    npost = [0] * P
+    done = [False] * P
+    progress = True
+    while progress:
+        progress = False
+        for r in range(P):
+            ops = progs[r]
+            while pc[r] < len(ops):
+                op = ops[pc[r]]
+                k = op[0]
+                if k in ("s", "r"):
+                    post_epoch[(r, npost[r])] = epoch[r]
+                    npost[r] += 1
+                elif k == "A":
+                    n = len(op[1]) + len(op[2])
+                    if (r, "A", pc[r]) not in post_epoch:      # post once, then wait
+                        post_epoch[(r, "A", pc[r])] = npost[r]
+                        for _ in range(n):
+                            post_epoch[(r, npost[r])] = epoch[r]
+                            npost[r] += 1
+                    first = post_epoch[(r, "A", pc[r])]
+                    # the collective completes all of its own posts
+                    if not _try_wait(r, range(first, first + n), by_post, msgs, post_epoch, step, epoch):
+                        break
+                elif k == "w":
+                    if not _try_wait(r, [q for q in op[1] if (r, q) not in eager],
+                                     by_post, msgs, post_epoch, step, epoch):
+                        break
+                pc[r] += 1
+                progress = True
+            if pc[r] == len(ops):
+                done[r] = True
+    if not all(done):
+        raise RuntimeError("deadlock: ranks %s blocked" % [r for r in range(P) if not done[r]])
+    nsteps = max([s for s in step if s is not None], default=-1) + 1
+    return step, nsteps
+
+
+def _try_wait(r, posts, by_post, msgs, post_epoch, step, epoch):
+    mids = [by_post[(r, q)] for q in posts]
+    for mi in mids:
+        if step[mi] is None:
+            src, _seg, dst, _slot, _cnt, sp, rp = msgs[mi]
+            if (src, sp) not in post_epoch or (dst, rp) not in post_epoch:
+                return False
+            step[mi] = max(post_epoch[(src, sp)], post_epoch[(dst, rp)]) + 1
+    if mids:
+        epoch[r] = max(epoch[r], max(step[mi] for mi in mids))
+    return True
