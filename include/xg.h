@@ -1,0 +1,107 @@
+/*
+ * xg.h -- device half of the MI355X aggregator-exchange framework (C-ABI).
+ *
+ * One process per GPU.  Everything the reference does with malloc'd host
+ * buffers and MPI point-to-point calls happens here on HBM with hand-written
+ * CDNA4 kernels (gfx950) and grouped RCCL send/recv over xGMI.  No torch
+ * types, no HIP types in the signatures: plain pointers, sizes, int status
+ * (0 = ok; otherwise an XG_E* code, with a file:line message on stderr --
+ * the reference's unused ERR macro, mpi_test.c:15-22, made real).
+ *
+ * Interface replaced (reference file:line)               -> entry point
+ *   MPI_Init / Comm_rank / Comm_size  mpi_test.c:2127-2129 -> xg_get_unique_id, xg_init
+ *   MPI_Finalize                      mpi_test.c:2345      -> xg_finalize
+ *   MPI_Barrier before each timed loop (e.g. :1762)        -> xg_barrier
+ *   MPI_Reduce(5 doubles, MAX, root 0) (e.g. :2184)        -> xg_allreduce_max
+ *   malloc in prepare_*_data  :94-133, :162-202            -> xg_regions_alloc
+ *   fill_buffer / MAP_DATA    :71-77, :23                  -> xg_fill
+ *   check_buffer              :83-92 (call sites :139,:215)-> xg_verify
+ *   free in clean_*           :135-231                     -> xg_regions_free
+ *   the timed Irecv/Issend/Send/Recv/Sendrecv/Waitall/
+ *   Alltoallw loop of each method (:421-1950)              -> xg_plan_load + xg_plan_run
+ *                                                            (xg_plan_enqueue for back-to-back runs)
+ *   MPI_Wtime post / waitall brackets                      -> step_post / step_done of xg_plan_run
+ */
+#ifndef XG_H
+#define XG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "xg_sched.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XG_OK 0
+#define XG_EHIP 1
+#define XG_ERCCL 2
+#define XG_EARG 3
+#define XG_ENOMEM 4
+
+#define XG_UNIQUE_ID_BYTES 128
+
+typedef struct xg_ctx xg_ctx;
+typedef struct xg_regions xg_regions;
+typedef struct xg_plan xg_plan;
+
+/* xg_segrun / xg_slot and their builders live in xg_sched.h (host layout). */
+/* ------------------------------------------------------------------ context */
+int xg_get_unique_id(void *uid /* XG_UNIQUE_ID_BYTES */);
+/* rank/nranks: this process in the job (one per GPU).  device: HIP ordinal.
+ * uid: from rank 0's xg_get_unique_id (ignored when nranks == 1). */
+int xg_init(xg_ctx **out, int rank, int nranks, int device, const void *uid);
+int xg_finalize(xg_ctx *ctx);
+int xg_rank(const xg_ctx *ctx);
+int xg_nranks(const xg_ctx *ctx);
+int xg_barrier(xg_ctx *ctx);
+int xg_allreduce_max(xg_ctx *ctx, double *vals, int n);       /* in place, MAX over all GPUs */
+int xg_sync(xg_ctx *ctx);
+/* device name, CU count, HBM bytes (any pointer may be NULL) */
+int xg_device_info(xg_ctx *ctx, char *name, size_t namelen, int *cus, size_t *hbm_bytes);
+double xg_now(void);                                           /* host seconds (monotonic) */
+
+/* ------------------------------------------------------------------ HBM regions */
+/* region_bytes: XG_BUF_SEND, XG_BUF_RECV, XG_BUF_STAGE_SEND, XG_BUF_STAGE_RECV
+ * (xg_devplan.region_bytes).  The RECV region is poisoned (0xA5). */
+int xg_regions_alloc(xg_ctx *ctx, const int64_t region_bytes[4], xg_regions **out);
+int xg_regions_free(xg_regions *r);
+int xg_regions_poison(xg_regions *r);
+/* Device pointer of a region (for tests that read buffers back). */
+void *xg_regions_ptr(xg_regions *r, int buf);
+int xg_regions_read(xg_regions *r, int buf, int64_t off, void *host, int64_t len);
+
+int xg_fill(xg_regions *r, const xg_segrun *runs, int nruns, int64_t d, int iter, int mode);
+/* Per slot: chk[i] = xg_chk64 of the slot bytes, bad[i] = number of bytes that
+ * differ from the expected fingerprint, first_bad[i] = first differing offset
+ * (or -1).  Any output pointer may be NULL. */
+int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_t d, int iter, int mode,
+              uint64_t *chk, int64_t *bad, int64_t *first_bad);
+
+/* ------------------------------------------------------------------ plans */
+int xg_plan_load(xg_ctx *ctx, xg_regions *r, const xg_devplan *dp, xg_plan **out);
+int xg_plan_free(xg_plan *p);
+int xg_plan_nsteps(const xg_plan *p);
+/* Timed run (caller barriers first): enqueues every step with a completion
+ * event, waits, and returns per step the device completion time (seconds
+ * since the run started) and the host enqueue time; *wall = host seconds from
+ * start to the final synchronisation. */
+int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall);
+/* Enqueue all steps once without events or synchronisation (bench loops). */
+int xg_plan_enqueue(xg_plan *p);
+/* Kernel timing session: while active, every copy_kernel launch of any plan
+ * on this context is bracketed by HIP events on the stream it runs on.
+ * xg_ktime_end waits for the stream and returns the summed kernel time (ms),
+ * the number of launches and their algorithmic HBM bytes (read + write). */
+int xg_ktime_begin(xg_ctx *ctx, int max_launches);
+int xg_ktime_end(xg_ctx *ctx, double *total_ms, int *launches, int64_t *bytes);
+
+/* Tuning: chunk bytes per copy workgroup (default 65536), copy kernel
+ * variant (0 = default).  Applied to plans loaded afterwards. */
+int xg_set_copy_params(xg_ctx *ctx, int64_t chunk_bytes, int variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

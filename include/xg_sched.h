@@ -1,0 +1,183 @@
+/*
+ * xg_sched.h -- host-side (plain C, no HIP headers) half of the MI355X
+ * aggregator-exchange framework.
+ *
+ * The reference (QiaoK/MPI-Asynchronous-Communication-Test, mpi_test.c) runs
+ * one MPI process per rank; each method issues Irecv/Issend/Send/Recv/
+ * Sendrecv/Waitall/Alltoallw calls.  Here every logical rank's program is
+ * restated literally (same loops, same quirks), matched with MPI semantics,
+ * and compiled into a list of device-wide STEPS: step s holds every segment
+ * that can move once everything of steps < s is delivered (earliest-step
+ * schedule; MPI eager protocol for small blocking sends).  Each GPU then
+ * executes its share of each step as one gather/scatter kernel + one grouped
+ * RCCL exchange (xg.h).
+ *
+ * Interfaces replaced (reference file:line):
+ *   xg_aggregator_list  <- create_aggregator_list        mpi_test.c:1952-2006
+ *   xg_sched_build      <- the body of each method       mpi_test.c:421-1950
+ *                          (+ *_alltoall_translate :233-302)
+ *   xg_sched_rank_timer <- the MPI_Wtime brackets filling Timer   :25-31
+ *   xg_summarize_results<- summarize_results             mpi_test.c:2068-2118
+ */
+#ifndef XG_SCHED_H
+#define XG_SCHED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Timer of the reference, field order preserved (mpi_test.c:25-31): MPI_Reduce
+ * reduces it as 5 doubles. */
+typedef struct {
+    double post_request_time;
+    double send_wait_all_time;
+    double recv_wait_all_time;
+    double barrier_time;
+    double total_time;
+} xg_timer;
+
+enum { XG_A2M = 0, XG_M2A = 1 };
+
+/* One matched message (one d-byte segment; zero-length for the pairwise
+ * methods' non-participating pairs).  sseg: index of the segment in the
+ * sender's send buffer; dslot: index of the slot in the receiver's receive
+ * buffer.  step: the device-wide step it moves in.  Self memcpy's of
+ * m3/m4/m6 (mpi_test.c:1473, :1646, :1714) are messages with src == dst and
+ * XG_MSG_COPY. */
+typedef struct {
+    int32_t src, sseg, dst, dslot;
+    int64_t len;
+    int32_t step;
+    int32_t flags;
+} xg_msg;
+
+#define XG_MSG_COPY 1
+#define XG_MSG_COLL 2   /* part of an MPI_Alltoallw */
+
+#define XG_MPICH_EAGER_LIMIT 65424   /* see DESIGN.md "blocking-send semantics" */
+
+typedef struct xg_sched xg_sched;
+
+/* create_aggregator_list (mpi_test.c:1952-2006).  Returns 0, or -1 for an
+ * aggregator type the reference does not define. */
+int xg_aggregator_list(int procs, int cb_nodes, int proc_node, int type, int *rank_list);
+
+/* Label printed by summarize_results for a method (mpi_test.c:2186-2271), NULL if out of scope. */
+const char *xg_method_label(int method);
+/* XG_A2M or XG_M2A, -1 if method not in 1..12. */
+int xg_method_direction(int method);
+
+/* Build the schedule of one method run (all `ntimes` repetitions).
+ * eager_limit: blocking sends of <= eager_limit bytes complete locally
+ * (XG_MPICH_EAGER_LIMIT reproduces the reference built on the image's MPICH).
+ * Returns NULL and writes a message into err on failure, e.g. when the
+ * programs deadlock under MPI semantics (the reference hangs there too). */
+xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size, int comm_size,
+                         const int *rank_list, int ntimes, int64_t eager_limit,
+                         char *err, size_t errlen);
+void xg_sched_free(xg_sched *s);
+
+int xg_sched_nmsg(const xg_sched *s);
+const xg_msg *xg_sched_msgs(const xg_sched *s);
+int xg_sched_nsteps(const xg_sched *s);
+int xg_sched_direction(const xg_sched *s);
+int xg_sched_procs(const xg_sched *s);
+
+/* Canonical MPI call trace of one logical rank (same token format as the
+ * PMPI capture in tests/golden/); returns the length written (truncated to
+ * buflen-1) or the needed length if buf is NULL. */
+size_t xg_sched_trace(const xg_sched *s, int rank, char *buf, size_t buflen);
+
+/* Per-rank timer from device step timestamps:
+ *   step_done[s]  seconds from the timed-region start until step s completed
+ *                 on the GPU that hosts `rank`;
+ *   step_post[s]  host seconds spent enqueuing step s on that GPU (may be NULL).
+ * Each reference timer bracket (MPI_Wtime pairs) becomes an interval of the
+ * rank's logical clock, which advances at completion points to the step
+ * completion time of the awaited messages. */
+int xg_sched_rank_timer(const xg_sched *s, int rank, const double *step_done,
+                        const double *step_post, xg_timer *out);
+
+/* ---------------------------------------------------------------- device plan
+ * Block mapping of logical ranks onto G GPUs: gpu(r) = r / ceil(P/G).
+ * Buffers of GPU g (byte offsets inside four regions):
+ *   XG_BUF_SEND  send segments of its ranks (a2m: each local rank A segs;
+ *                m2a: each local aggregator rank P segs), rank-major
+ *   XG_BUF_RECV  receive slots (a2m: each local aggregator rank P slots;
+ *                m2a: each local rank A slots), rank-major
+ *   XG_BUF_STAGE_SEND / XG_BUF_STAGE_RECV  packed per-peer staging
+ */
+enum { XG_BUF_SEND = 0, XG_BUF_RECV = 1, XG_BUF_STAGE_SEND = 2, XG_BUF_STAGE_RECV = 3 };
+
+typedef struct {
+    int64_t src_off, dst_off, len;
+    int32_t src_buf, dst_buf;
+} xg_copy;
+
+typedef struct {
+    int64_t off, len;
+    int32_t peer, buf;
+    int32_t is_send;
+    int32_t pad;
+} xg_p2p;
+
+typedef struct {
+    int32_t pre_begin, pre_count;     /* local copies + packs   (before the exchange) */
+    int32_t p2p_begin, p2p_count;     /* grouped RCCL send/recv                       */
+    int32_t post_begin, post_count;   /* unpacks                (after the exchange)  */
+} xg_stepplan;
+
+typedef struct {
+    int32_t gpu, ngpus, nsteps, pad;
+    int64_t region_bytes[4];          /* send, recv, stage_send, stage_recv           */
+    int32_t ncopy, np2p;
+    xg_copy *copies;
+    xg_p2p *p2p;
+    xg_stepplan *steps;
+    int64_t local_bytes, remote_send_bytes, remote_recv_bytes;   /* per whole plan  */
+} xg_devplan;
+
+/* Ranks hosted by GPU g: [*lo, *hi). */
+void xg_block_range(int procs, int ngpus, int g, int *lo, int *hi);
+int xg_gpu_of(int procs, int ngpus, int rank);
+
+/* Region sizes and per-rank region offsets (-1 if the rank has no such buffer
+ * on that GPU). */
+int64_t xg_send_offset(const xg_sched *s, int ngpus, int rank);
+int64_t xg_recv_offset(const xg_sched *s, int ngpus, int rank);
+int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf);
+
+/* Build GPU g's share of every step.  pack_max_seg: per (step, peer), pack the
+ * segments into one staging buffer when there are >= 2 and their mean length
+ * is < pack_max_seg (0 = never pack); otherwise one RCCL op per segment. */
+xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg);
+void xg_devplan_free(xg_devplan *p);
+
+/* fill: `nsegs` consecutive d-byte segments at `off` in the SEND region,
+ * segment i = fingerprint(rank, seed0 + i, iter) (prepare_*_data loops). */
+typedef struct { int32_t rank, seed0; int64_t off; int32_t nsegs, pad; } xg_segrun;
+/* verify: one d-byte receive slot at `off` in the RECV region that must hold
+ * fingerprint(src, seed, iter); dst is the receiving logical rank. */
+typedef struct { int32_t src, seed, dst, pad; int64_t off; } xg_slot;
+
+enum { XG_FP_REFERENCE = 0, XG_FP_STRONG = 1 };   /* fingerprint modes */
+
+/* Fill/verify descriptors of GPU g (host side, from the schedule's layout).
+ * Return the count; out may be NULL to query it. */
+int xg_fill_runs(const xg_sched *s, int ngpus, int g, xg_segrun *out);
+int xg_verify_slots(const xg_sched *s, int ngpus, int g, xg_slot *out);
+
+/* ---------------------------------------------------------------- report
+ * summarize_results (mpi_test.c:2068-2118): 8 "| ..." lines on stdout and one
+ * appended row (header on first write) in `filename`. */
+int xg_summarize_results(int procs, int cb_nodes, int data_size, int comm_size, int ntimes,
+                         int type, const char *filename, const char *prefix,
+                         xg_timer timer1, xg_timer max_timer1);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

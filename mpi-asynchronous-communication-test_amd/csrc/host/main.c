@@ -1,0 +1,306 @@
+/*
+ * main.c -- drop-in for the reference's ./test (mpi_test.c:2120-2347).
+ *
+ * Same getopt surface "hp:c:m:d:a:i:k:t:r:b:" (:2130), same defaults (:2121),
+ * same header (:2171-2177), same per-method report and results.csv
+ * (summarize_results, :2068-2118), same experiment loop (:2181-2343).
+ *
+ * Differences, by design:
+ *  - One process per GPU; P logical ranks are block-mapped onto the GPUs.
+ *    P defaults to the number of processes (as `mpiexec -n P`); host more
+ *    logical ranks per GPU with --procs N or XG_PROCS=N.
+ *  - Launch: single process, or any launcher that sets RANK/WORLD_SIZE
+ *    (torchrun --no-python) or PMI_RANK/PMI_SIZE (mpiexec).  The RCCL unique
+ *    id is handed over through a file in $XG_RDZV_DIR (default /tmp).
+ *  - -m 0 runs methods 1..12; 13..20 are outside this build's scope and are
+ *    reported as skipped on stderr.
+ *  - Extra, opt-in: --verify (or XG_VERIFY=1) checks every received byte on
+ *    the GPU and prints one extra "| <label> verify ..." line per method;
+ *    --fingerprint strong switches to the collision-free fingerprint.
+ */
+#include <errno.h>
+#include <getopt.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "xg.h"
+#include "xg_sched.h"
+
+static void usage(const char *argv0)   /* mpi_test.c:41-69 */
+{
+    const char *help =
+        "Usage: %s [OPTION]... [FILE]...\n"
+        "       [-h] Print help\n"
+        "       [-a] number of aggregators (in the context of ROMIO)\n"
+        "       [-p] number of processes per node (does not really matter)\n"
+        "       [-d] data size\n"
+        "       [-c] maximum communication size\n"
+        "       [-i] number of experiments (MPI barrier between experiments)\n"
+        "       [-k] number of iteration (run methods many times, there is no sync between individual runs)\n"
+        "       [-m] method\n"
+        "           0: All experiments\n"
+        "           1: All to many without ordering (all-to-many)\n"
+        "           2: Many to all without ordering (many-to-all)\n"
+        "           3: All to many with ordering (all-to-many)\n"
+        "           4: Many to all with ordering (many-to-all)\n"
+        "           5: Many to all with alltoallw (many-to-all)\n"
+        "           6: All to many sync (all-to-many sync)\n"
+        "           7: All to many half sync (all-to-many half sync)\n"
+        "           8: All to many with alltoallw (all-to-many benchmark)\n"
+        "           9: All to many pairwise (all-to-many pairwise)\n"
+        "           10: Many to all pairwise (many-to-all pairwise)\n"
+        "           11: Many to all half sync (many-to-all half sync)\n"
+        "           12: Many to all half sync2 (many-to-all half sync2)\n";
+    fprintf(stderr, help, argv0);
+}
+
+static int env_int(const char *a, const char *b, int dflt)
+{
+    const char *v = getenv(a);
+    if (!v && b) v = getenv(b);
+    return v ? atoi(v) : dflt;
+}
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+/* RCCL unique-id hand-over through a file (single node). */
+static int rendezvous(int rank, int nranks, unsigned char uid[XG_UNIQUE_ID_BYTES], char *path, size_t pathlen)
+{
+    const char *dir = getenv("XG_RDZV_DIR");
+    const char *key = getenv("XG_RDZV_KEY");
+    char kbuf[128];
+    double t_start = now_s();
+    if (!dir) dir = "/tmp";
+    if (!key) {
+        const char *port = getenv("MASTER_PORT"), *run = getenv("TORCHELASTIC_RUN_ID");
+        if (port) snprintf(kbuf, sizeof kbuf, "p%s_%s", port, run ? run : "");
+        else snprintf(kbuf, sizeof kbuf, "pp%ld", (long)getppid());
+        key = kbuf;
+    }
+    snprintf(path, pathlen, "%s/xg_rdzv_%s.bin", dir, key);
+    if (rank == 0) {
+        char tmp[4200];
+        FILE *f;
+        if (xg_get_unique_id(uid)) return -1;
+        snprintf(tmp, sizeof tmp, "%s.%ld", path, (long)getpid());
+        f = fopen(tmp, "wb");
+        if (!f || fwrite(uid, 1, XG_UNIQUE_ID_BYTES, f) != XG_UNIQUE_ID_BYTES) { perror(tmp); return -1; }
+        fclose(f);
+        if (rename(tmp, path)) { perror(path); return -1; }
+        return 0;
+    }
+    for (;;) {
+        struct stat st;
+        if (stat(path, &st) == 0 && st.st_mtime >= (time_t)t_start - 30) {
+            FILE *f = fopen(path, "rb");
+            if (f) {
+                size_t n = fread(uid, 1, XG_UNIQUE_ID_BYTES, f);
+                fclose(f);
+                if (n == XG_UNIQUE_ID_BYTES) return 0;
+            }
+        }
+        if (now_s() - t_start > 120) {
+            fprintf(stderr, "rank %d/%d: no RCCL id at %s after 120 s\n", rank, nranks, path);
+            return -1;
+        }
+        { struct timespec ts = {0, 2000000}; nanosleep(&ts, NULL); }
+    }
+}
+
+#define DIE(...) do { fprintf(stderr, __VA_ARGS__); fputc('\n', stderr); exit(1); } while (0)
+#define XGCALL(x) do { int rc_ = (x); if (rc_) DIE("xg call failed (%d): %s", rc_, #x); } while (0)
+
+typedef struct {
+    int P, A, d, c, ntimes, type, proc_node;
+    int verify, fp_mode;
+    int64_t eager, pack_max;
+    int *rank_list;
+} opts_t;
+
+static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
+{
+    const int g = xg_rank(ctx), G = xg_nranks(ctx);
+    const char *label = xg_method_label(method);
+    char err[512];
+    xg_sched *s = xg_sched_build(method, o->P, o->A, o->d, o->c, o->rank_list, o->ntimes, o->eager, err, sizeof err);
+    xg_devplan *dp;
+    xg_regions *reg;
+    xg_plan *plan;
+    xg_segrun *runs;
+    int nruns, nsteps, lo, hi, r;
+    double *done, *post, wall;
+    xg_timer t0 = {0, 0, 0, 0, 0}, tmax = {0, 0, 0, 0, 0};
+    double red[5];
+
+    if (!s) {
+        if (g == 0) fprintf(stderr, "| %s: %s\n", label, err);
+        return;
+    }
+    dp = xg_devplan_build(s, G, g, o->pack_max);
+    XGCALL(xg_regions_alloc(ctx, dp->region_bytes, &reg));
+    /* prepare_*_data: allocate + fill (untimed) */
+    nruns = xg_fill_runs(s, G, g, NULL);
+    runs = (xg_segrun *)malloc(sizeof(xg_segrun) * (nruns + 1));
+    xg_fill_runs(s, G, g, runs);
+    XGCALL(xg_fill(reg, runs, nruns, o->d, iter, o->fp_mode));
+    free(runs);
+    XGCALL(xg_plan_load(ctx, reg, dp, &plan));
+    nsteps = xg_sched_nsteps(s);
+    done = (double *)calloc(nsteps + 1, sizeof(double));
+    post = (double *)calloc(nsteps + 1, sizeof(double));
+    /* MPI_Barrier; total_start = MPI_Wtime(); ... timed loop ... */
+    XGCALL(xg_barrier(ctx));
+    XGCALL(xg_plan_run(plan, done, post, &wall));
+    /* per logical rank timers, then MPI_Reduce(MAX) (:2184) */
+    xg_block_range(o->P, G, g, &lo, &hi);
+    for (r = lo; r < hi; ++r) {
+        xg_timer t;
+        xg_sched_rank_timer(s, r, done, post, &t);
+        if (r == 0) t0 = t;
+        if (t.post_request_time > tmax.post_request_time) tmax.post_request_time = t.post_request_time;
+        if (t.send_wait_all_time > tmax.send_wait_all_time) tmax.send_wait_all_time = t.send_wait_all_time;
+        if (t.recv_wait_all_time > tmax.recv_wait_all_time) tmax.recv_wait_all_time = t.recv_wait_all_time;
+        if (t.total_time > tmax.total_time) tmax.total_time = t.total_time;
+    }
+    red[0] = tmax.post_request_time; red[1] = tmax.send_wait_all_time; red[2] = tmax.recv_wait_all_time;
+    red[3] = 0; red[4] = tmax.total_time;
+    XGCALL(xg_allreduce_max(ctx, red, 5));
+    tmax.post_request_time = red[0]; tmax.send_wait_all_time = red[1]; tmax.recv_wait_all_time = red[2];
+    tmax.barrier_time = 0; tmax.total_time = red[4];
+    if (g == 0)
+        xg_summarize_results(o->P, o->A, o->d, o->c, o->ntimes, o->type, "results.csv", label, t0, tmax);
+    if (o->verify) {
+        int ns = xg_verify_slots(s, G, g, NULL), i;
+        xg_slot *sl = (xg_slot *)malloc(sizeof(xg_slot) * (ns + 1));
+        int64_t *bad = (int64_t *)calloc(ns + 1, sizeof(int64_t)), *first = (int64_t *)calloc(ns + 1, sizeof(int64_t));
+        uint64_t *chk = (uint64_t *)calloc(ns + 1, sizeof(uint64_t)), cc = 0;
+        double v[2] = {0, 0};
+        xg_verify_slots(s, G, g, sl);
+        XGCALL(xg_verify(reg, sl, ns, o->d, iter, o->fp_mode, chk, bad, first));
+        for (i = 0; i < ns; ++i) {
+            if (bad[i]) {
+                if (v[0] == 0)
+                    fprintf(stderr, "rank %d, message is wrong from rank %d (first bad byte %lld)\n", sl[i].dst,
+                            sl[i].src, (long long)first[i]);
+                v[0] += 1;
+            }
+            cc += chk[i];
+        }
+        v[1] = (double)(cc >> 11);
+        XGCALL(xg_allreduce_max(ctx, v, 1));
+        if (g == 0) {
+            const double bytes = (double)o->P * o->A * o->d * o->ntimes;
+            printf("| %s verify = %s (%d slots on gpu 0, bad slots max over gpus = %.0f), aggregate = %.3f GB/s\n",
+                   label, v[0] == 0 ? "OK" : "FAILED", ns, v[0], tmax.total_time > 0 ? bytes / tmax.total_time / 1e9 : 0.0);
+        }
+        free(sl); free(bad); free(first); free(chk);
+    }
+    free(done); free(post);
+    XGCALL(xg_plan_free(plan));
+    XGCALL(xg_regions_free(reg));
+    xg_devplan_free(dp);
+    xg_sched_free(s);
+}
+
+int main(int argc, char **argv)
+{
+    /* defaults of mpi_test.c:2121 */
+    int cb_nodes = 1, method = 0, data_size = 0, proc_node = 1, i, comm_size = 200000000, iter = 1, ntimes = 1;
+    int aggregator_type = 1, barrier_type = 0, procs = 0, verify = 0, fp_mode = XG_FP_REFERENCE;
+    int64_t eager = XG_MPICH_EAGER_LIMIT, pack_max = 1 << 20;
+    char prefix[200];
+    int rank, nranks, device, ngpu_dev;
+    unsigned char uid[XG_UNIQUE_ID_BYTES];
+    char rdzv_path[4096] = {0};
+    xg_ctx *ctx;
+    opts_t o;
+    static struct option longopts[] = {
+        {"procs", required_argument, 0, 1000},
+        {"verify", no_argument, 0, 1001},
+        {"fingerprint", required_argument, 0, 1002},
+        {"eager-limit", required_argument, 0, 1003},
+        {"pack-max-seg", required_argument, 0, 1004},
+        {0, 0, 0, 0}};
+    prefix[0] = '\0';
+
+    rank = env_int("RANK", "PMI_RANK", 0);
+    nranks = env_int("WORLD_SIZE", "PMI_SIZE", 1);
+    device = env_int("LOCAL_RANK", "MPI_LOCALRANKID", rank);
+    procs = env_int("XG_PROCS", NULL, 0);
+    verify = env_int("XG_VERIFY", NULL, 0);
+    if (getenv("XG_FINGERPRINT") && !strcmp(getenv("XG_FINGERPRINT"), "strong")) fp_mode = XG_FP_STRONG;
+    if (getenv("XG_EAGER_LIMIT")) eager = atoll(getenv("XG_EAGER_LIMIT"));
+    if (getenv("XG_PACK_MAX_SEG")) pack_max = atoll(getenv("XG_PACK_MAX_SEG"));
+
+    while ((i = getopt_long(argc, argv, "hp:c:m:d:a:i:k:t:r:b:", longopts, NULL)) != EOF) {
+        switch (i) {
+        case 'm': method = atoi(optarg); break;
+        case 'a': cb_nodes = atoi(optarg); break;
+        case 'd': data_size = atoi(optarg); break;
+        case 'c': comm_size = atoi(optarg); break;
+        case 'i': iter = atoi(optarg); break;
+        case 'p': proc_node = atoi(optarg); break;
+        case 'k': ntimes = atoi(optarg); break;
+        case 't': aggregator_type = atoi(optarg); break;
+        case 'r': strncpy(prefix, optarg, sizeof prefix - 1); prefix[sizeof prefix - 1] = 0; break;
+        case 'b': barrier_type = atoi(optarg); break;
+        case 1000: procs = atoi(optarg); break;
+        case 1001: verify = 1; break;
+        case 1002: fp_mode = !strcmp(optarg, "strong") ? XG_FP_STRONG : XG_FP_REFERENCE; break;
+        case 1003: eager = atoll(optarg); break;
+        case 1004: pack_max = atoll(optarg); break;
+        default:
+            if (rank == 0) usage(argv[0]);
+            return 0;
+        }
+    }
+    (void)barrier_type;   /* -b only affects method 13 (out of scope) */
+    if (procs <= 0) procs = nranks;
+    if (nranks > procs) DIE("more GPU processes (%d) than logical ranks (%d)", nranks, procs);
+    if (cb_nodes < 1 || cb_nodes > procs) DIE("-a %d: need 1 <= aggregators <= ranks (%d)", cb_nodes, procs);
+    if (data_size < 0) DIE("-d must be >= 0");
+
+    if (nranks > 1 && rendezvous(rank, nranks, uid, rdzv_path, sizeof rdzv_path)) DIE("rendezvous failed");
+    ngpu_dev = device;
+    XGCALL(xg_init(&ctx, rank, nranks, ngpu_dev, uid));
+    XGCALL(xg_barrier(ctx));
+    if (rank == 0 && rdzv_path[0]) unlink(rdzv_path);
+
+    o.P = procs; o.A = cb_nodes; o.d = data_size; o.c = comm_size; o.ntimes = ntimes; o.type = aggregator_type;
+    o.proc_node = proc_node; o.verify = verify; o.fp_mode = fp_mode; o.eager = eager; o.pack_max = pack_max;
+    o.rank_list = (int *)malloc(sizeof(int) * cb_nodes);
+    if (xg_aggregator_list(procs, cb_nodes, proc_node, aggregator_type, o.rank_list))
+        DIE("-t %d: aggregator type not defined by the reference", aggregator_type);
+
+    if (rank == 0) {   /* :2170-2179 */
+        printf("total number of processes = %d, cb_nodes = %d, proc_node = %d, data size = %d, comm_size = %d, "
+               "ntimes=%d\n", procs, cb_nodes, proc_node, data_size, comm_size, ntimes);
+        printf("aggregators = ");
+        for (i = 0; i < cb_nodes; ++i) printf("%d, ", o.rank_list[i]);
+        printf("\n");
+        if (method > 12) fprintf(stderr, "method %d is outside this build's scope (1..12)\n", method);
+        if (method == 0) fprintf(stderr, "-m 0: running methods 1..12 (13..20 are outside this build's scope)\n");
+    }
+    for (i = 0; i < iter; ++i) {   /* :2181-2343 */
+        int m;
+        for (m = 1; m <= 12; ++m)
+            if (method == 0 || method == m) run_method(ctx, &o, m, i);
+        if (rank == 0) {
+            printf("| --------------------------------------\n");
+            fflush(stdout);
+        }
+    }
+    free(o.rank_list);
+    XGCALL(xg_finalize(ctx));
+    return 0;
+}

@@ -1,0 +1,1174 @@
+/*
+ * sched.c -- per-rank program restatement of methods 1..12, MPI matching, and
+ * the step compiler that turns the reference's per-process MPI schedules into
+ * device-wide steps.  Plain C99, no HIP.  See include/xg_sched.h.
+ *
+ * Each method builder below follows the reference function line by line
+ * (cited per function); the only translation is that an MPI call becomes an
+ * op appended to the logical rank's program:
+ *   Irecv/Issend  -> OP_RECV/OP_SEND post      Waitall -> OP_WAIT
+ *   Send/Recv     -> post + OP_WAIT             Sendrecv -> 2 posts + OP_WAIT
+ *   Alltoallw     -> OP_A2AW + collective posts + OP_WAIT
+ *   memcpy (self) -> OP_COPY                    MPI_Wtime brackets -> OP_TMARK
+ */
+#include "xg_sched.h"
+
+#include <limits.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+enum { OP_BARRIER, OP_SEND, OP_RECV, OP_WAIT, OP_A2AW, OP_COPY, OP_TMARK };
+enum { F_POST = 0, F_SEND = 1, F_RECV = 2, F_TOTAL = 3 };
+
+typedef struct {
+    int8_t kind, blocking, field, sign;
+    int32_t coll;           /* -1: point-to-point; k: the rank's k-th Alltoallw */
+    int32_t peer;
+    int32_t idx;            /* send: segment; recv: slot; copy: segment      */
+    int32_t idx2;           /* copy: slot                                     */
+    int32_t post;           /* send/recv: post index; copy: message index      */
+    int32_t wbeg, wcnt;     /* wait: range in the rank's pool                 */
+    int64_t cnt;
+} op_t;
+
+typedef struct {
+    op_t *ops;
+    int nops, cap;
+    int32_t *pool;
+    int npool, poolcap;
+    int nposts, ncoll;
+} prog_t;
+
+struct xg_sched {
+    int method, P, A, ntimes, dir, c;
+    int64_t d, eager;
+    int *rank_list;
+    int *isagg, *agg_prefix;     /* agg_prefix[r] = number of aggregator ranks < r */
+    prog_t *progs;
+    xg_msg *msgs;
+    int nmsg, msgcap;
+    int32_t *msg_spost, *msg_rpost;
+    int32_t **post_msg;          /* [rank][post] -> message */
+    uint8_t **post_eager;        /* [rank][post] -> blocking send <= eager limit   */
+    int nsteps;
+};
+
+/* ------------------------------------------------------------------ helpers */
+static void *xmalloc(size_t n)
+{
+    void *p = malloc(n ? n : 1);
+    if (!p) { fprintf(stderr, "xg_sched: out of host memory (%zu bytes)\n", n); abort(); }
+    return p;
+}
+
+static op_t *push(prog_t *p)
+{
+    if (p->nops == p->cap) {
+        p->cap = p->cap ? 2 * p->cap : 64;
+        p->ops = (op_t *)realloc(p->ops, sizeof(op_t) * p->cap);
+        if (!p->ops) abort();
+    }
+    op_t *o = &p->ops[p->nops++];
+    memset(o, 0, sizeof *o);
+    o->coll = -1;
+    return o;
+}
+
+static int post_send(prog_t *p, int peer, int64_t cnt, int seg, int blocking)
+{
+    op_t *o = push(p);
+    o->kind = OP_SEND; o->peer = peer; o->cnt = cnt; o->idx = seg; o->blocking = (int8_t)blocking;
+    o->post = p->nposts++;
+    return o->post;
+}
+
+static int post_recv(prog_t *p, int peer, int64_t cnt, int slot)
+{
+    op_t *o = push(p);
+    o->kind = OP_RECV; o->peer = peer; o->cnt = cnt; o->idx = slot;
+    o->post = p->nposts++;
+    return o->post;
+}
+
+static void wait_list(prog_t *p, const int *idx, int n)
+{
+    op_t *o;
+    if (p->npool + n > p->poolcap) {
+        while (p->npool + n > p->poolcap) p->poolcap = p->poolcap ? 2 * p->poolcap : 256;
+        p->pool = (int32_t *)realloc(p->pool, sizeof(int32_t) * p->poolcap);
+        if (!p->pool) abort();
+    }
+    o = push(p);
+    o->kind = OP_WAIT; o->wbeg = p->npool; o->wcnt = n;
+    memcpy(p->pool + p->npool, idx, sizeof(int) * n);
+    p->npool += n;
+}
+
+static void wait1(prog_t *p, int a) { wait_list(p, &a, 1); }
+
+static void send_blocking(prog_t *p, int peer, int64_t cnt, int seg) { wait1(p, post_send(p, peer, cnt, seg, 1)); }
+static void recv_blocking(prog_t *p, int peer, int64_t cnt, int slot) { wait1(p, post_recv(p, peer, cnt, slot)); }
+
+static void sendrecv(prog_t *p, int dst, int64_t scnt, int seg, int src, int64_t rcnt, int slot)
+{
+    int ab[2];
+    ab[0] = post_send(p, dst, scnt, seg, 1);
+    ab[1] = post_recv(p, src, rcnt, slot);
+    wait_list(p, ab, 2);
+}
+
+static void tmark(prog_t *p, int field, int sign)
+{
+    op_t *o = push(p);
+    o->kind = OP_TMARK; o->field = (int8_t)field; o->sign = (int8_t)sign;
+}
+
+static void tstart(prog_t *p, int f) { tmark(p, f, +1); }
+static void tstop(prog_t *p, int f) { tmark(p, f, -1); }
+
+static void copy_op(prog_t *p, int seg, int slot, int64_t cnt)
+{
+    op_t *o = push(p);
+    o->kind = OP_COPY; o->idx = seg; o->idx2 = slot; o->cnt = cnt; o->post = -1;
+}
+
+/* growable int list for request indices */
+typedef struct { int *v; int n, cap; } ilist;
+static void il_push(ilist *l, int x)
+{
+    if (l->n == l->cap) { l->cap = l->cap ? 2 * l->cap : 64; l->v = (int *)realloc(l->v, sizeof(int) * l->cap); if (!l->v) abort(); }
+    l->v[l->n++] = x;
+}
+
+typedef struct {
+    prog_t *p;
+    int rank, isagg, myindex, P, A, c, ntimes;
+    int64_t d;
+    const int *rl;
+} ctx_t;
+
+/* ------------------------------------------------------------------ methods */
+
+/* all_to_many, mpi_test.c:1748-1824 */
+static void m1_all_to_many(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int m, i, k, P = x->P, A = x->A;
+    ilist l = {0};
+    for (m = 0; m < x->ntimes; ++m) {
+        if (x->c >= P) {                                    /* :1765-1784 */
+            l.n = 0;
+            tstart(p, F_POST);
+            if (x->isagg)
+                for (i = 0; i < P; ++i) il_push(&l, post_recv(p, i, x->d, i));
+            for (i = 0; i < A; ++i) il_push(&l, post_send(p, x->rl[i], x->d, i, 0));
+            tstop(p, F_POST);
+            if (l.n) { tstart(p, F_RECV); wait_list(p, l.v, l.n); tstop(p, F_RECV); }
+        } else {                                            /* :1785-1817 */
+            int steps = (P + x->c - 1) / x->c;
+            ilist sends = {0};
+            tstart(p, F_POST);
+            for (i = 0; i < A; ++i) il_push(&sends, post_send(p, x->rl[i], x->d, i, 0));
+            tstop(p, F_POST);
+            for (k = 0; k < steps; ++k) {
+                l.n = 0;
+                if (x->isagg) {
+                    tstart(p, F_POST);
+                    for (i = k; i < P; i += steps) il_push(&l, post_recv(p, i, x->d, i));
+                    tstop(p, F_POST);
+                }
+                if (l.n) { tstart(p, F_RECV); wait_list(p, l.v, l.n); tstop(p, F_RECV); }
+            }
+            if (sends.n) { tstart(p, F_SEND); wait_list(p, sends.v, sends.n); tstop(p, F_SEND); }
+            free(sends.v);
+        }
+    }
+    free(l.v);
+}
+
+/* many_to_all, mpi_test.c:1871-1950 */
+static void m2_many_to_all(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int m, i, k, P = x->P, A = x->A;
+    ilist l = {0};
+    for (m = 0; m < x->ntimes; ++m) {
+        if (x->c >= P) {                                    /* :1889-1906 */
+            l.n = 0;
+            tstart(p, F_POST);
+            for (i = 0; i < A; ++i) il_push(&l, post_recv(p, x->rl[i], x->d, i));
+            if (x->isagg)
+                for (i = 0; i < P; ++i) il_push(&l, post_send(p, i, x->d, i, 0));
+            tstop(p, F_POST);
+            if (l.n) { tstart(p, F_RECV); wait_list(p, l.v, l.n); tstop(p, F_RECV); }
+        } else {                                            /* :1907-1943 */
+            int steps = (P + x->c - 1) / x->c;
+            ilist recvs = {0};
+            tstart(p, F_POST);
+            for (i = 0; i < A; ++i) il_push(&recvs, post_recv(p, x->rl[i], x->d, i));
+            tstop(p, F_POST);
+            for (k = 0; k < steps; ++k) {
+                l.n = 0;
+                if (x->isagg) {
+                    tstart(p, F_POST);
+                    for (i = k; i < P; i += steps) il_push(&l, post_send(p, i, x->d, i, 0));
+                    tstop(p, F_POST);
+                }
+                if (l.n) { tstart(p, F_SEND); wait_list(p, l.v, l.n); tstop(p, F_SEND); }
+            }
+            if (recvs.n) { tstart(p, F_RECV); wait_list(p, recvs.v, recvs.n); tstop(p, F_RECV); }
+            free(recvs.v);
+        }
+    }
+    free(l.v);
+}
+
+/* window start of aggregator index idx in round k (mpi_test.c:1463-1467, :1478-1482) */
+static long win_start(int idx, long k, int ceiling, int floor_, int remainder)
+{
+    return idx < remainder ? k + (long)idx * ceiling
+                           : k + (long)remainder * ceiling + (long)(idx - remainder) * floor_;
+}
+
+/* window membership test, mpi_test.c:1483-1499 (= :1617-1633), edge cases included */
+static int in_window(int rank, long temp, int cs, int P)
+{
+    if ((temp >= P && temp + cs >= P) || (temp < P && temp + cs < P))
+        return rank >= temp % P && rank < (temp + cs) % P;
+    return rank >= temp || rank < (temp + cs) % P;
+}
+
+static int send_start0(int rank, int ceiling, int floor_, int remainder)   /* :1449-1453 */
+{
+    if (rank >= remainder * ceiling) return remainder + (rank - remainder * ceiling) / floor_;
+    return rank / ceiling;
+}
+
+/* all_to_many_balanced, mpi_test.c:1422-1517 */
+static void m3_balanced(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, A = x->A, c = x->c, m, i, cs, k, xx;
+    int ceiling = (P + A - 1) / A, floor_ = P / A, remainder = P % A;
+    int bblock, send_start;
+    ilist l = {0};
+    if (c > P) c = P;
+    bblock = c;
+    send_start = send_start0(x->rank, ceiling, floor_, remainder);
+    for (m = 0; m < x->ntimes; ++m) {
+        cs = bblock;                                         /* :1455 reset */
+        for (k = 0; k < P; k += cs) {
+            if (P - k < cs) cs = P - k;
+            l.n = 0;
+            if (x->isagg) {
+                for (i = 0; i < cs; ++i) {
+                    int temp = (int)(win_start(x->myindex, (long)k + i, ceiling, floor_, remainder) % P);
+                    if (temp != x->rank) {
+                        tstart(p, F_POST);
+                        il_push(&l, post_recv(p, temp, x->d, temp));
+                        tstop(p, F_POST);
+                    } else {
+                        copy_op(p, x->myindex, temp, x->d);          /* :1473 */
+                    }
+                }
+            }
+            for (xx = 0; xx < A; ++xx) {
+                long temp = win_start(send_start, k, ceiling, floor_, remainder);
+                if (!in_window(x->rank, temp, cs, P)) break;
+                if (x->rl[send_start] != x->rank)
+                    il_push(&l, post_send(p, x->rl[send_start], x->d, send_start, 0));
+                send_start = (send_start - 1 + A) % A;
+            }
+            if (l.n) {
+                tstart(p, F_RECV);
+                if (!x->isagg) tstart(p, F_SEND);
+                wait_list(p, l.v, l.n);
+                tstop(p, F_RECV);
+                if (!x->isagg) tstop(p, F_SEND);
+            }
+        }
+    }
+    free(l.v);
+}
+
+/* many_to_all_balanced, mpi_test.c:1576-1663 (comm_size NOT reset between repetitions) */
+static void m4_balanced(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, A = x->A, m, i, k, xx;
+    int ceiling = (P + A - 1) / A, floor_ = P / A, remainder = P % A;
+    int cs = x->c > P ? P : x->c;
+    int send_start = send_start0(x->rank, ceiling, floor_, remainder);
+    ilist l = {0};
+    for (m = 0; m < x->ntimes; ++m) {
+        for (k = 0; k < P; k += cs) {
+            if (P - k < cs) cs = P - k;
+            l.n = 0;
+            tstart(p, F_POST);
+            for (xx = 0; xx < A; ++xx) {
+                long temp = win_start(send_start, k, ceiling, floor_, remainder);
+                if (!in_window(x->rank, temp, cs, P)) break;
+                if (x->rl[send_start] != x->rank)
+                    il_push(&l, post_recv(p, x->rl[send_start], x->d, send_start));
+                send_start = (send_start - 1 + A) % A;
+            }
+            if (x->isagg) {
+                for (i = 0; i < cs; ++i) {
+                    int temp = (int)(win_start(x->myindex, (long)k + i, ceiling, floor_, remainder) % P);
+                    if (temp != x->rank)
+                        il_push(&l, post_send(p, temp, x->d, temp, 0));
+                    else
+                        copy_op(p, temp, x->myindex, x->d);          /* :1646 */
+                }
+            }
+            tstop(p, F_POST);
+            if (l.n) { tstart(p, F_RECV); wait_list(p, l.v, l.n); tstop(p, F_RECV); }
+        }
+    }
+    free(l.v);
+}
+
+/* *_alltoall_translate, mpi_test.c:233-262 (a2m) and :273-302 (m2a) */
+static void translate(ctx_t *x, int dir, int64_t *sc, int64_t *sd, int64_t *rc, int64_t *rd)
+{
+    int i, P = x->P, A = x->A;
+    int64_t d = x->d;
+    memset(sc, 0, sizeof(int64_t) * P); memset(sd, 0, sizeof(int64_t) * P);
+    memset(rc, 0, sizeof(int64_t) * P); memset(rd, 0, sizeof(int64_t) * P);
+    if (dir == XG_A2M) {
+        for (i = 0; i < A; ++i) { sd[x->rl[i]] = (int64_t)i * d; sc[x->rl[i]] = d; }
+        if (x->isagg)
+            for (i = 0; i < P; ++i) { rc[i] = d; rd[i] = (int64_t)i * d; }
+    } else {
+        rd[x->rl[0]] = 0; rc[x->rl[0]] = d;
+        for (i = 1; i < A; ++i) { rd[x->rl[i]] = rd[x->rl[i - 1]] + d; rc[x->rl[i]] = d; }
+        if (x->isagg)
+            for (i = 0; i < P; ++i) { sc[i] = d; sd[i] = (int64_t)i * d; }
+    }
+}
+
+/* many_to_all_benchmark :599-654 / all_to_many_benchmark :885-940 (MPI_Alltoallw) */
+static void m_alltoallw(ctx_t *x, int dir)
+{
+    prog_t *p = x->p;
+    int P = x->P, m, q;
+    int64_t *sc = xmalloc(sizeof(int64_t) * 4 * P), *sd = sc + P, *rc = sc + 2 * P, *rd = sc + 3 * P;
+    ilist l = {0};
+    translate(x, dir, sc, sd, rc, rd);
+    for (m = 0; m < x->ntimes; ++m) {
+        op_t *a;
+        int coll = p->ncoll++;
+        a = push(p); a->kind = OP_A2AW; a->coll = coll;
+        l.n = 0;
+        for (q = 0; q < P; ++q)
+            if (sc[q] > 0) { int id = post_send(p, q, sc[q], (int)(sd[q] / x->d), 0); p->ops[p->nops - 1].coll = coll; il_push(&l, id); }
+        for (q = 0; q < P; ++q)
+            if (rc[q] > 0) { int id = post_recv(p, q, rc[q], (int)(rd[q] / x->d)); p->ops[p->nops - 1].coll = coll; il_push(&l, id); }
+        wait_list(p, l.v, l.n);
+        p->ops[p->nops - 1].coll = coll;
+    }
+    free(l.v);
+    free(sc);
+}
+
+/* all_to_many_sync, mpi_test.c:1665-1746 */
+static void m6_sync(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, A = x->A, m, i, k, xx;
+    int cs = x->c > A ? A : x->c;
+    for (m = 0; m < x->ntimes; ++m) {
+        for (k = 0; k < A; k += cs) {
+            if (A - k < cs) cs = A - k;
+            tstart(p, F_RECV);
+            if (x->isagg) {
+                for (i = 0; i < cs; ++i) {
+                    int temp = (x->rank + k + i) % A;
+                    int temp2 = (x->myindex - k - i + A) % A;
+                    if (x->rl[temp] != x->rank && temp2 != x->rank) {
+                        sendrecv(p, x->rl[temp], x->d, temp, temp2, x->d, temp2);
+                    } else if (x->rl[temp] == x->rank) {
+                        copy_op(p, temp, x->rank, x->d);             /* :1714 */
+                        if (temp2 != x->rank) recv_blocking(p, temp2, x->d, temp2);
+                    } else if (temp2 == x->rank) {
+                        send_blocking(p, x->rl[temp], x->d, temp);
+                    }
+                    for (xx = temp2 + A; xx < P; xx += A)
+                        if (x->rank != xx) recv_blocking(p, xx, x->d, xx);
+                }
+            } else {
+                for (i = 0; i < cs; ++i) {
+                    int temp = (x->rank + k + i) % A;
+                    send_blocking(p, x->rl[temp], x->d, temp);
+                }
+            }
+            tstop(p, F_RECV);
+        }
+    }
+}
+
+/* all_to_many_half_sync, mpi_test.c:1055-1114 */
+static void m7_half_sync(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, A = x->A, m, i, k, xx;
+    int cs = x->c > A ? A : x->c;
+    ilist l = {0};
+    for (m = 0; m < x->ntimes; ++m) {
+        for (k = 0; k < A; k += cs) {
+            if (A - k < cs) cs = A - k;
+            l.n = 0;
+            if (x->isagg)
+                for (i = 0; i < cs; ++i)
+                    for (xx = (x->myindex - k - i + A) % A; xx < P; xx += A)
+                        il_push(&l, post_recv(p, xx, x->d, xx));
+            for (i = 0; i < cs; ++i) {
+                int temp = (x->rank + k + i) % A;
+                send_blocking(p, x->rl[temp], x->d, temp);
+            }
+            tstart(p, F_RECV);
+            if (l.n) wait_list(p, l.v, l.n);
+            tstop(p, F_RECV);
+        }
+    }
+    free(l.v);
+}
+
+/* many_to_all_half_sync, mpi_test.c:942-997 */
+static void m11_half_sync(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, A = x->A, m, i, k, xx;
+    int cs = x->c > P ? P : x->c;
+    int stride = (P + A - 1) / A;
+    ilist l = {0};
+    for (m = 0; m < x->ntimes; ++m) {
+        for (k = 0; k < P; k += cs) {
+            if (P - k < cs) cs = P - k;
+            l.n = 0;
+            tstart(p, F_POST);
+            if (x->isagg)
+                for (i = 0; i < cs; ++i) {
+                    int temp = (int)(((long)stride * x->myindex + k + i) % P);
+                    il_push(&l, post_send(p, temp, x->d, temp, 0));
+                }
+            tstop(p, F_POST);
+            tstart(p, F_RECV);
+            for (xx = 0; xx < cs; ++xx)
+                for (i = 0; i < A; ++i)
+                    if (x->rank == (int)(((long)k + (long)i * stride + xx) % P))
+                        recv_blocking(p, x->rl[i], x->d, i);
+            if (l.n) wait_list(p, l.v, l.n);
+            tstop(p, F_RECV);
+        }
+    }
+    free(l.v);
+}
+
+/* all_to_many_half_sync2, mpi_test.c:999-1053 */
+static void m12_half_sync2(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, A = x->A, m, i, k, xx;
+    int cs = x->c > A ? A : x->c;
+    ilist l = {0};
+    for (m = 0; m < x->ntimes; ++m) {
+        for (k = 0; k < A; k += cs) {
+            if (A - k < cs) cs = A - k;
+            l.n = 0;
+            for (i = 0; i < cs; ++i) {
+                int temp = (x->rank + k + i) % A;
+                il_push(&l, post_send(p, x->rl[temp], x->d, temp, 0));
+            }
+            if (x->isagg)
+                for (i = 0; i < cs; ++i)
+                    for (xx = (x->myindex - k - i + A) % A; xx < P; xx += A)
+                        recv_blocking(p, xx, x->d, xx);
+            tstart(p, F_RECV);
+            if (l.n) wait_list(p, l.v, l.n);
+            tstop(p, F_RECV);
+        }
+    }
+    free(l.v);
+}
+
+/* many_to_all_pairwise :421-508 / all_to_many_pairwise :510-597 */
+static void m_pairwise(ctx_t *x, int dir)
+{
+    prog_t *p = x->p;
+    int P = x->P, m, i, pof2, src, dst;
+    int64_t *sc = xmalloc(sizeof(int64_t) * 4 * P), *sd = sc + P, *rc = sc + 2 * P, *rd = sc + 3 * P;
+    translate(x, dir, sc, sd, rc, rd);
+    i = 1;
+    while (i < P) i *= 2;
+    pof2 = i == P;
+    for (m = 0; m < x->ntimes; ++m) {
+        for (i = 0; i < P; ++i) {
+            if (pof2) src = dst = x->rank ^ i;
+            else { src = (x->rank - i + P) % P; dst = (x->rank + i) % P; }
+            sendrecv(p, dst, sc[dst], sc[dst] ? (int)(sd[dst] / x->d) : -1,
+                     src, rc[src], rc[src] ? (int)(rd[src] / x->d) : -1);
+        }
+    }
+    free(sc);
+}
+
+/* ------------------------------------------------------------------ public: placement / labels */
+int xg_aggregator_list(int procs, int cb_nodes, int proc_node, int type, int *rl)
+{
+    int i, remainder, ceiling, floor_;
+    if (type == 1 || type == 2) {                 /* :1956-1990, quirk: remainder = procs / cb_nodes */
+        remainder = procs / cb_nodes;
+        ceiling = (procs + cb_nodes - 1) / cb_nodes;
+        floor_ = procs / cb_nodes;
+        for (i = 0; i < cb_nodes; ++i) {
+            int v = i < remainder ? ceiling * i : ceiling * remainder + floor_ * (i - remainder);
+            rl[i] = type == 1 ? v : (v - 16 + procs * 16) % procs;
+        }
+    } else if (type == 0) {                       /* :1970-1976 */
+        for (i = 0; i < cb_nodes; ++i) rl[i] = i;
+    } else if (type == 3) {                       /* :1991-2002 */
+        remainder = 0;
+        for (i = 0; i < cb_nodes; ++i) {
+            rl[i] = remainder;
+            remainder += proc_node;
+            if (remainder >= procs) remainder = remainder % proc_node + 1;
+        }
+    } else {
+        return -1;
+    }
+    return 0;
+}
+
+const char *xg_method_label(int method)
+{
+    static const char *labels[] = {
+        NULL, "All to many", "Many to all", "All to many balanced", "Many to all balanced",
+        "Many to all benchmark", "All to many sync", "All to many half sync", "All to many benchmark",
+        "All to many pairwise", "Many to all pairwise", "Many to all half sync", "All to many half sync 2",
+    };
+    return method >= 1 && method <= 12 ? labels[method] : NULL;
+}
+
+int xg_method_direction(int method)
+{
+    switch (method) {
+    case 1: case 3: case 6: case 7: case 8: case 9: case 12: return XG_A2M;
+    case 2: case 4: case 5: case 10: case 11: return XG_M2A;
+    default: return -1;
+    }
+}
+
+/* ------------------------------------------------------------------ matching */
+typedef struct {
+    int32_t coll, a, b, rank, post, idx;
+    int64_t cnt;
+} pst_t;
+
+static int pst_cmp(const void *x_, const void *y_)
+{
+    const pst_t *x = (const pst_t *)x_, *y = (const pst_t *)y_;
+    if (x->coll != y->coll) return x->coll < y->coll ? -1 : 1;
+    if (x->a != y->a) return x->a < y->a ? -1 : 1;
+    if (x->b != y->b) return x->b < y->b ? -1 : 1;
+    return x->post < y->post ? -1 : x->post > y->post;
+}
+
+static xg_msg *new_msg(xg_sched *s)
+{
+    if (s->nmsg == s->msgcap) {
+        s->msgcap = s->msgcap ? 2 * s->msgcap : 1024;
+        s->msgs = (xg_msg *)realloc(s->msgs, sizeof(xg_msg) * s->msgcap);
+        s->msg_spost = (int32_t *)realloc(s->msg_spost, sizeof(int32_t) * s->msgcap);
+        s->msg_rpost = (int32_t *)realloc(s->msg_rpost, sizeof(int32_t) * s->msgcap);
+        if (!s->msgs || !s->msg_spost || !s->msg_rpost) abort();
+    }
+    memset(&s->msgs[s->nmsg], 0, sizeof(xg_msg));
+    s->msg_spost[s->nmsg] = s->msg_rpost[s->nmsg] = -1;
+    return &s->msgs[s->nmsg++];
+}
+
+static int do_match(xg_sched *s, char *err, size_t errlen)
+{
+    int r, i, ns = 0, nr = 0, j;
+    size_t tot_s = 0, tot_r = 0;
+    pst_t *S, *R;
+    for (r = 0; r < s->P; ++r)
+        for (i = 0; i < s->progs[r].nops; ++i) {
+            tot_s += s->progs[r].ops[i].kind == OP_SEND;
+            tot_r += s->progs[r].ops[i].kind == OP_RECV;
+        }
+    S = (pst_t *)xmalloc(sizeof(pst_t) * tot_s);
+    R = (pst_t *)xmalloc(sizeof(pst_t) * tot_r);
+    for (r = 0; r < s->P; ++r) {
+        const prog_t *p = &s->progs[r];
+        for (i = 0; i < p->nops; ++i) {
+            const op_t *o = &p->ops[i];
+            if (o->kind == OP_SEND) {
+                pst_t t = { o->coll, r, o->peer, r, o->post, o->idx, o->cnt };
+                S[ns++] = t;
+            } else if (o->kind == OP_RECV) {
+                pst_t t = { o->coll, o->peer, r, r, o->post, o->idx, o->cnt };
+                R[nr++] = t;
+            }
+        }
+    }
+    qsort(S, ns, sizeof(pst_t), pst_cmp);
+    qsort(R, nr, sizeof(pst_t), pst_cmp);
+    for (i = 0, j = 0; i < ns || j < nr; ++i, ++j) {
+        xg_msg *m;
+        if (i >= ns || j >= nr || S[i].coll != R[j].coll || S[i].a != R[j].a || S[i].b != R[j].b) {
+            const pst_t *u = i < ns ? &S[i] : &R[j];
+            snprintf(err, errlen, "unmatched point-to-point traffic %d -> %d (the reference would hang)", u->a, u->b);
+            free(S); free(R);
+            return -1;
+        }
+        if (S[i].cnt > R[j].cnt) {
+            snprintf(err, errlen, "message truncated %d -> %d", S[i].a, S[i].b);
+            free(S); free(R);
+            return -1;
+        }
+        m = new_msg(s);
+        m->src = S[i].a; m->sseg = S[i].idx; m->dst = S[i].b; m->dslot = R[j].idx;
+        m->len = S[i].cnt; m->step = -1;
+        m->flags = S[i].coll >= 0 ? XG_MSG_COLL : 0;
+        s->msg_spost[s->nmsg - 1] = S[i].post;
+        s->msg_rpost[s->nmsg - 1] = R[j].post;
+        s->post_msg[S[i].rank][S[i].post] = s->nmsg - 1;
+        s->post_msg[R[j].rank][R[j].post] = s->nmsg - 1;
+    }
+    free(S); free(R);
+    /* self copies become messages too (their step is set by the step compiler) */
+    for (r = 0; r < s->P; ++r) {
+        prog_t *p = &s->progs[r];
+        for (i = 0; i < p->nops; ++i)
+            if (p->ops[i].kind == OP_COPY) {
+                xg_msg *m = new_msg(s);
+                m->src = m->dst = r; m->sseg = p->ops[i].idx; m->dslot = p->ops[i].idx2;
+                m->len = p->ops[i].cnt; m->step = -1; m->flags = XG_MSG_COPY;
+                p->ops[i].post = s->nmsg - 1;
+            }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ step compiler */
+static int compile_steps(xg_sched *s, char *err, size_t errlen)
+{
+    int P = s->P, r, progress = 1, maxstep = -1;
+    int *pc = (int *)xmalloc(sizeof(int) * P), *epoch = (int *)xmalloc(sizeof(int) * P);
+    int32_t **pe = (int32_t **)xmalloc(sizeof(int32_t *) * P);     /* post epoch */
+    for (r = 0; r < P; ++r) {
+        int q;
+        pc[r] = 0; epoch[r] = -1;
+        pe[r] = (int32_t *)xmalloc(sizeof(int32_t) * (s->progs[r].nposts + 1));
+        for (q = 0; q < s->progs[r].nposts; ++q) pe[r][q] = INT_MIN;
+    }
+    while (progress) {
+        progress = 0;
+        for (r = 0; r < P; ++r) {
+            prog_t *p = &s->progs[r];
+            while (pc[r] < p->nops) {
+                op_t *o = &p->ops[pc[r]];
+                if (o->kind == OP_SEND || o->kind == OP_RECV) {
+                    pe[r][o->post] = epoch[r];
+                } else if (o->kind == OP_COPY) {
+                    s->msgs[o->post].step = epoch[r] + 1;
+                    if (epoch[r] + 1 > maxstep) maxstep = epoch[r] + 1;
+                } else if (o->kind == OP_WAIT) {
+                    int q, blocked = 0, e = epoch[r];
+                    for (q = 0; q < o->wcnt; ++q) {
+                        int post = p->pool[o->wbeg + q], mi;
+                        xg_msg *m;
+                        if (s->post_eager[r][post]) continue;       /* eager send: completes locally */
+                        mi = s->post_msg[r][post];
+                        m = &s->msgs[mi];
+                        if (m->step < 0) {
+                            int a = pe[m->src][s->msg_spost[mi]], b = pe[m->dst][s->msg_rpost[mi]];
+                            if (a == INT_MIN || b == INT_MIN) { blocked = 1; break; }
+                            m->step = (a > b ? a : b) + 1;
+                            if (m->step > maxstep) maxstep = m->step;
+                        }
+                        if (m->step > e) e = m->step;
+                    }
+                    if (blocked) break;
+                    epoch[r] = e;
+                }
+                pc[r]++;
+                progress = 1;
+            }
+        }
+    }
+    for (r = 0; r < P; ++r)
+        if (pc[r] < s->progs[r].nops) {
+            snprintf(err, errlen,
+                     "method %d deadlocks under MPI semantics at P=%d A=%d d=%lld c=%d (rank %d blocked; "
+                     "the reference hangs here too)", s->method, s->P, s->A, (long long)s->d, s->c, r);
+            break;
+        }
+    {
+        int bad = r < P, i;
+        for (i = 0; !bad && i < s->nmsg; ++i)
+            if (s->msgs[i].step < 0) {      /* a message nobody waits for: runs after its posts */
+                int a = pe[s->msgs[i].src][s->msg_spost[i]], b = pe[s->msgs[i].dst][s->msg_rpost[i]];
+                s->msgs[i].step = (a > b ? a : b) + 1;
+                if (s->msgs[i].step > maxstep) maxstep = s->msgs[i].step;
+            }
+        for (r = 0; r < P; ++r) free(pe[r]);
+        free(pe); free(pc); free(epoch);
+        s->nsteps = maxstep + 1;
+        return bad ? -1 : 0;
+    }
+}
+
+/* ------------------------------------------------------------------ build */
+void xg_sched_free(xg_sched *s)
+{
+    int r;
+    if (!s) return;
+    if (s->progs)
+        for (r = 0; r < s->P; ++r) { free(s->progs[r].ops); free(s->progs[r].pool); }
+    if (s->post_msg)
+        for (r = 0; r < s->P; ++r) { free(s->post_msg[r]); free(s->post_eager[r]); }
+    free(s->post_msg); free(s->post_eager);
+    free(s->progs); free(s->msgs); free(s->msg_spost); free(s->msg_rpost);
+    free(s->rank_list); free(s->isagg); free(s->agg_prefix);
+    free(s);
+}
+
+xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size, int comm_size,
+                         const int *rank_list, int ntimes, int64_t eager_limit, char *err, size_t errlen)
+{
+    xg_sched *s;
+    int r, i;
+    char dummy[8];
+    if (!err) { err = dummy; errlen = sizeof dummy; }
+    err[0] = 0;
+    if (method < 1 || method > 12) { snprintf(err, errlen, "method %d is out of scope (1..12)", method); return NULL; }
+    if (procs < 1 || cb_nodes < 1 || cb_nodes > procs || data_size < 0 || ntimes < 0) {
+        snprintf(err, errlen, "bad sizes P=%d A=%d d=%lld k=%d", procs, cb_nodes, (long long)data_size, ntimes);
+        return NULL;
+    }
+    if (comm_size < 1) { snprintf(err, errlen, "comm_size must be >= 1 (the reference divides by it)"); return NULL; }
+    for (i = 0; i < cb_nodes; ++i)
+        if (rank_list[i] < 0 || rank_list[i] >= procs) { snprintf(err, errlen, "aggregator %d out of range", rank_list[i]); return NULL; }
+    s = (xg_sched *)calloc(1, sizeof *s);
+    s->method = method; s->P = procs; s->A = cb_nodes; s->d = data_size; s->c = comm_size;
+    s->ntimes = ntimes; s->eager = eager_limit; s->dir = xg_method_direction(method);
+    s->rank_list = (int *)xmalloc(sizeof(int) * cb_nodes);
+    memcpy(s->rank_list, rank_list, sizeof(int) * cb_nodes);
+    s->isagg = (int *)calloc(procs, sizeof(int));
+    s->agg_prefix = (int *)xmalloc(sizeof(int) * (procs + 1));
+    for (i = 0; i < cb_nodes; ++i) s->isagg[rank_list[i]] = 1;
+    s->agg_prefix[0] = 0;
+    for (r = 0; r < procs; ++r) s->agg_prefix[r + 1] = s->agg_prefix[r] + s->isagg[r];
+    s->progs = (prog_t *)calloc(procs, sizeof(prog_t));
+    for (r = 0; r < procs; ++r) {
+        ctx_t x;
+        prog_t *p = &s->progs[r];
+        x.p = p; x.rank = r; x.isagg = s->isagg[r]; x.myindex = 0;
+        x.P = procs; x.A = cb_nodes; x.c = comm_size; x.ntimes = ntimes; x.d = data_size; x.rl = rank_list;
+        for (i = 0; i < cb_nodes; ++i)            /* last match, :111-115 / :183-187 */
+            if (rank_list[i] == r) x.myindex = i;
+        push(p)->kind = OP_BARRIER;
+        tstart(p, F_TOTAL);
+        switch (method) {
+        case 1: m1_all_to_many(&x); break;
+        case 2: m2_many_to_all(&x); break;
+        case 3: m3_balanced(&x); break;
+        case 4: m4_balanced(&x); break;
+        case 5: m_alltoallw(&x, XG_M2A); break;
+        case 6: m6_sync(&x); break;
+        case 7: m7_half_sync(&x); break;
+        case 8: m_alltoallw(&x, XG_A2M); break;
+        case 9: m_pairwise(&x, XG_A2M); break;
+        case 10: m_pairwise(&x, XG_M2A); break;
+        case 11: m11_half_sync(&x); break;
+        case 12: m12_half_sync2(&x); break;
+        }
+        tstop(p, F_TOTAL);
+    }
+    s->post_msg = (int32_t **)calloc(procs, sizeof(int32_t *));
+    s->post_eager = (uint8_t **)calloc(procs, sizeof(uint8_t *));
+    for (r = 0; r < procs; ++r) {
+        prog_t *p = &s->progs[r];
+        s->post_msg[r] = (int32_t *)xmalloc(sizeof(int32_t) * (p->nposts + 1));
+        s->post_eager[r] = (uint8_t *)calloc(p->nposts + 1, 1);
+        for (i = 0; i < p->nops; ++i)
+            if (p->ops[i].kind == OP_SEND && p->ops[i].blocking && p->ops[i].cnt <= eager_limit)
+                s->post_eager[r][p->ops[i].post] = 1;
+    }
+    if (do_match(s, err, errlen) || compile_steps(s, err, errlen)) {
+        xg_sched_free(s);
+        return NULL;
+    }
+    return s;
+}
+
+int xg_sched_nmsg(const xg_sched *s) { return s->nmsg; }
+const xg_msg *xg_sched_msgs(const xg_sched *s) { return s->msgs; }
+int xg_sched_nsteps(const xg_sched *s) { return s->nsteps; }
+int xg_sched_direction(const xg_sched *s) { return s->dir; }
+int xg_sched_procs(const xg_sched *s) { return s->P; }
+
+/* ------------------------------------------------------------------ traces */
+typedef struct { char *buf; size_t len, cap; } sbuf;
+static void sb_put(sbuf *b, const char *str)
+{
+    size_t n = strlen(str);
+    if (b->buf && b->len + n < b->cap) memcpy(b->buf + b->len, str, n + 1);
+    else if (b->buf && b->len < b->cap) { memcpy(b->buf + b->len, str, b->cap - 1 - b->len); b->buf[b->cap - 1] = 0; }
+    b->len += n;
+}
+
+static int icmp(const void *a, const void *b) { return *(const int *)a - *(const int *)b; }
+
+size_t xg_sched_trace(const xg_sched *s, int rank, char *buf, size_t buflen)
+{
+    sbuf b = { buf, 0, buflen };
+    const prog_t *p = &s->progs[rank];
+    int i, first = 1;
+    char tok[64];
+    if (buf && buflen) buf[0] = 0;
+    for (i = 0; i < p->nops; ++i) {
+        const op_t *o = &p->ops[i];
+        tok[0] = 0;
+        if (o->kind == OP_BARRIER) strcpy(tok, "B");
+        else if (o->kind == OP_A2AW) strcpy(tok, "A");
+        else if (o->coll >= 0) continue;
+        else if (o->kind == OP_SEND) snprintf(tok, sizeof tok, "s%d:%lld", o->peer, (long long)o->cnt);
+        else if (o->kind == OP_RECV) snprintf(tok, sizeof tok, "r%d:%lld", o->peer, (long long)o->cnt);
+        else if (o->kind == OP_WAIT) {
+            int *v = (int *)xmalloc(sizeof(int) * (o->wcnt + 1)), a = 0;
+            memcpy(v, p->pool + o->wbeg, sizeof(int) * o->wcnt);
+            qsort(v, o->wcnt, sizeof(int), icmp);
+            if (!first) sb_put(&b, " ");
+            first = 0;
+            sb_put(&b, "w");
+            while (a < o->wcnt) {
+                int e = a;
+                while (e + 1 < o->wcnt && v[e + 1] == v[e] + 1) ++e;
+                if (a) sb_put(&b, ",");
+                if (e == a) snprintf(tok, sizeof tok, "%d", v[a]);
+                else snprintf(tok, sizeof tok, "%d-%d", v[a], v[e]);
+                sb_put(&b, tok);
+                a = e + 1;
+            }
+            free(v);
+            continue;
+        } else continue;
+        if (!first) sb_put(&b, " ");
+        first = 0;
+        sb_put(&b, tok);
+    }
+    return b.len;
+}
+
+/* ------------------------------------------------------------------ timers */
+int xg_sched_rank_timer(const xg_sched *s, int rank, const double *step_done,
+                        const double *step_post, xg_timer *out)
+{
+    const prog_t *p = &s->progs[rank];
+    double clock = 0, open[4] = {0, 0, 0, 0}, acc[4] = {0, 0, 0, 0}, postacc = 0;
+    int depth[4] = {0, 0, 0, 0};
+    int i, interval = 0;
+    int *stamp = (int *)calloc(s->nsteps + 1, sizeof(int));
+    for (i = 0; i < p->nops; ++i) {
+        const op_t *o = &p->ops[i];
+        if (o->kind == OP_TMARK) {
+            if (o->sign > 0) {
+                if (depth[o->field]++ == 0) {
+                    open[o->field] = clock;
+                    if (o->field == F_POST) { postacc = 0; ++interval; }
+                }
+            } else if (--depth[o->field] == 0) {
+                acc[o->field] += clock - open[o->field];
+                if (o->field == F_POST) acc[F_POST] += postacc;
+            }
+        } else if ((o->kind == OP_SEND || o->kind == OP_RECV) && depth[F_POST] && step_post) {
+            int st = s->msgs[s->post_msg[rank][o->post]].step;
+            if (st >= 0 && stamp[st] != interval) { stamp[st] = interval; postacc += step_post[st]; }
+        } else if (o->kind == OP_WAIT) {
+            int q;
+            for (q = 0; q < o->wcnt; ++q) {
+                int post = p->pool[o->wbeg + q];
+                int st;
+                if (s->post_eager[rank][post]) continue;
+                st = s->msgs[s->post_msg[rank][post]].step;
+                if (st >= 0 && step_done[st] > clock) clock = step_done[st];
+            }
+        }
+    }
+    free(stamp);
+    out->post_request_time = acc[F_POST];
+    out->send_wait_all_time = acc[F_SEND];
+    out->recv_wait_all_time = acc[F_RECV];
+    out->barrier_time = 0;
+    out->total_time = acc[F_TOTAL];
+    return 0;
+}
+
+/* ------------------------------------------------------------------ block mapping / layout */
+void xg_block_range(int procs, int ngpus, int g, int *lo, int *hi)
+{
+    int rpg = (procs + ngpus - 1) / ngpus;
+    *lo = g * rpg < procs ? g * rpg : procs;
+    *hi = *lo + rpg < procs ? *lo + rpg : procs;
+}
+
+int xg_gpu_of(int procs, int ngpus, int rank)
+{
+    int rpg = (procs + ngpus - 1) / ngpus;
+    return rank / rpg;
+}
+
+static int nsend_segs(const xg_sched *s, int r)
+{
+    return s->dir == XG_A2M ? s->A : (s->isagg[r] ? s->P : 0);
+}
+
+static int nrecv_slots(const xg_sched *s, int r)
+{
+    return s->dir == XG_A2M ? (s->isagg[r] ? s->P : 0) : s->A;
+}
+
+static int64_t rank_offset(const xg_sched *s, int ngpus, int rank, int recv)
+{
+    int lo, hi, g = xg_gpu_of(s->P, ngpus, rank);
+    int per_rank = recv ? nrecv_slots(s, rank) : nsend_segs(s, rank);
+    xg_block_range(s->P, ngpus, g, &lo, &hi);
+    if (!per_rank) return -1;
+    /* ranks with a buffer of this kind on the GPU are laid out rank-major */
+    if ((s->dir == XG_A2M) == (recv != 0))
+        return (int64_t)(s->agg_prefix[rank] - s->agg_prefix[lo]) * s->P * s->d;   /* aggregator buffers */
+    return (int64_t)(rank - lo) * s->A * s->d;                                      /* every-rank buffers */
+}
+
+int64_t xg_send_offset(const xg_sched *s, int ngpus, int rank) { return rank_offset(s, ngpus, rank, 0); }
+int64_t xg_recv_offset(const xg_sched *s, int ngpus, int rank) { return rank_offset(s, ngpus, rank, 1); }
+
+int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf)
+{
+    int lo, hi, naggs;
+    xg_block_range(s->P, ngpus, g, &lo, &hi);
+    naggs = s->agg_prefix[hi] - s->agg_prefix[lo];
+    if (buf == XG_BUF_SEND)
+        return s->dir == XG_A2M ? (int64_t)(hi - lo) * s->A * s->d : (int64_t)naggs * s->P * s->d;
+    if (buf == XG_BUF_RECV)
+        return s->dir == XG_A2M ? (int64_t)naggs * s->P * s->d : (int64_t)(hi - lo) * s->A * s->d;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ device plan */
+typedef struct { xg_copy *v; int n, cap; } cvec;
+typedef struct { xg_p2p *v; int n, cap; } pvec;
+static xg_copy *cpush(cvec *c)
+{
+    if (c->n == c->cap) { c->cap = c->cap ? 2 * c->cap : 256; c->v = (xg_copy *)realloc(c->v, sizeof(xg_copy) * c->cap); if (!c->v) abort(); }
+    memset(&c->v[c->n], 0, sizeof(xg_copy));
+    return &c->v[c->n++];
+}
+static xg_p2p *ppush(pvec *c)
+{
+    if (c->n == c->cap) { c->cap = c->cap ? 2 * c->cap : 256; c->v = (xg_p2p *)realloc(c->v, sizeof(xg_p2p) * c->cap); if (!c->v) abort(); }
+    memset(&c->v[c->n], 0, sizeof(xg_p2p));
+    return &c->v[c->n++];
+}
+
+void xg_devplan_free(xg_devplan *p)
+{
+    if (!p) return;
+    free(p->copies); free(p->p2p); free(p->steps); free(p);
+}
+
+/* same decision on both ends of a (step, src gpu, dst gpu) transfer list */
+static int use_pack(int n, int64_t total, int64_t pack_max_seg)
+{
+    return pack_max_seg > 0 && n >= 2 && total / n < pack_max_seg;
+}
+
+xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg)
+{
+    xg_devplan *dp = (xg_devplan *)calloc(1, sizeof *dp);
+    int nst = s->nsteps, i, st, G = ngpus;
+    int *cnt = (int *)calloc(nst + 1, sizeof(int)), *order = (int *)xmalloc(sizeof(int) * (s->nmsg + 1));
+    cvec pre = {0}, post = {0};
+    pvec pp = {0};
+    int64_t stage_s_max = 0, stage_r_max = 0;
+    int *bucket_n = (int *)calloc((size_t)G * 2, sizeof(int));
+    int64_t *bucket_b = (int64_t *)calloc((size_t)G * 2, sizeof(int64_t));
+    dp->gpu = g; dp->ngpus = G; dp->nsteps = nst;
+    dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan));
+    /* counting sort of messages by step, stable in message order */
+    for (i = 0; i < s->nmsg; ++i) cnt[s->msgs[i].step + 1]++;
+    for (st = 0; st < nst; ++st) cnt[st + 1] += cnt[st];
+    {
+        int *pos = (int *)xmalloc(sizeof(int) * (nst + 1));
+        memcpy(pos, cnt, sizeof(int) * (nst + 1));
+        for (i = 0; i < s->nmsg; ++i) order[pos[s->msgs[i].step]++] = i;
+        free(pos);
+    }
+    dp->region_bytes[XG_BUF_SEND] = xg_region_bytes(s, G, g, XG_BUF_SEND);
+    dp->region_bytes[XG_BUF_RECV] = xg_region_bytes(s, G, g, XG_BUF_RECV);
+    for (st = 0; st < nst; ++st) {
+        int b = cnt[st], e = cnt[st + 1], k, p;
+        int64_t sbase = 0, rbase = 0;
+        xg_stepplan *sp = &dp->steps[st];
+        /* per-peer volume (out: [p], in: [G+p]) for the pack decision */
+        memset(bucket_n, 0, sizeof(int) * 2 * G);
+        memset(bucket_b, 0, sizeof(int64_t) * 2 * G);
+        sp->pre_begin = pre.n;
+        for (k = b; k < e; ++k) {
+            const xg_msg *m = &s->msgs[order[k]];
+            int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
+            if (m->len <= 0) continue;
+            if (gs == g && gd == g) {
+                xg_copy *c = cpush(&pre);
+                c->src_buf = XG_BUF_SEND; c->src_off = xg_send_offset(s, G, m->src) + (int64_t)m->sseg * s->d;
+                c->dst_buf = XG_BUF_RECV; c->dst_off = xg_recv_offset(s, G, m->dst) + (int64_t)m->dslot * s->d;
+                c->len = m->len;
+                dp->local_bytes += m->len;
+            } else if (gs == g) {
+                bucket_n[gd]++; bucket_b[gd] += m->len;
+            } else if (gd == g) {
+                bucket_n[G + gs]++; bucket_b[G + gs] += m->len;
+            }
+        }
+        /* packs (into staging) join the pre-exchange copy launch */
+        for (p = 0; p < G; ++p) {
+            int64_t off = 0;
+            if (p == g || !bucket_n[p] || !use_pack(bucket_n[p], bucket_b[p], pack_max_seg)) continue;
+            for (k = b; k < e; ++k) {
+                const xg_msg *m = &s->msgs[order[k]];
+                if (m->len <= 0 || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
+                {
+                    xg_copy *c = cpush(&pre);
+                    c->src_buf = XG_BUF_SEND; c->src_off = xg_send_offset(s, G, m->src) + (int64_t)m->sseg * s->d;
+                    c->dst_buf = XG_BUF_STAGE_SEND; c->dst_off = sbase + off;
+                    c->len = m->len;
+                    off += m->len;
+                }
+            }
+            sbase += off;
+        }
+        sp->pre_count = pre.n - sp->pre_begin;
+        /* the grouped exchange: per peer, sends then receives, message order */
+        sp->p2p_begin = pp.n;
+        sp->post_begin = post.n;
+        {
+            int64_t soff = 0;
+            for (p = 0; p < G; ++p) {
+                int pk;
+                if (p == g) continue;
+                if (bucket_n[p]) {
+                    pk = use_pack(bucket_n[p], bucket_b[p], pack_max_seg);
+                    if (pk) {
+                        xg_p2p *o = ppush(&pp);
+                        o->peer = p; o->is_send = 1; o->buf = XG_BUF_STAGE_SEND; o->off = soff; o->len = bucket_b[p];
+                        soff += bucket_b[p];
+                    } else {
+                        for (k = b; k < e; ++k) {
+                            const xg_msg *m = &s->msgs[order[k]];
+                            if (m->len <= 0 || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
+                            {
+                                xg_p2p *o = ppush(&pp);
+                                o->peer = p; o->is_send = 1; o->buf = XG_BUF_SEND;
+                                o->off = xg_send_offset(s, G, m->src) + (int64_t)m->sseg * s->d; o->len = m->len;
+                            }
+                        }
+                    }
+                    dp->remote_send_bytes += bucket_b[p];
+                }
+                if (bucket_n[G + p]) {
+                    pk = use_pack(bucket_n[G + p], bucket_b[G + p], pack_max_seg);
+                    if (pk) {
+                        xg_p2p *o = ppush(&pp);
+                        int64_t off = 0;
+                        o->peer = p; o->is_send = 0; o->buf = XG_BUF_STAGE_RECV; o->off = rbase; o->len = bucket_b[G + p];
+                        for (k = b; k < e; ++k) {
+                            const xg_msg *m = &s->msgs[order[k]];
+                            if (m->len <= 0 || xg_gpu_of(s->P, G, m->src) != p || xg_gpu_of(s->P, G, m->dst) != g) continue;
+                            {
+                                xg_copy *c = cpush(&post);
+                                c->src_buf = XG_BUF_STAGE_RECV; c->src_off = rbase + off;
+                                c->dst_buf = XG_BUF_RECV; c->dst_off = xg_recv_offset(s, G, m->dst) + (int64_t)m->dslot * s->d;
+                                c->len = m->len;
+                                off += m->len;
+                            }
+                        }
+                        rbase += bucket_b[G + p];
+                    } else {
+                        for (k = b; k < e; ++k) {
+                            const xg_msg *m = &s->msgs[order[k]];
+                            if (m->len <= 0 || xg_gpu_of(s->P, G, m->src) != p || xg_gpu_of(s->P, G, m->dst) != g) continue;
+                            {
+                                xg_p2p *o = ppush(&pp);
+                                o->peer = p; o->is_send = 0; o->buf = XG_BUF_RECV;
+                                o->off = xg_recv_offset(s, G, m->dst) + (int64_t)m->dslot * s->d; o->len = m->len;
+                            }
+                        }
+                    }
+                    dp->remote_recv_bytes += bucket_b[G + p];
+                }
+            }
+            if (soff != sbase) { fprintf(stderr, "xg_devplan_build: staging mismatch\n"); abort(); }
+        }
+        sp->p2p_count = pp.n - sp->p2p_begin;
+        sp->post_count = post.n - sp->post_begin;
+        if (sbase > stage_s_max) stage_s_max = sbase;
+        if (rbase > stage_r_max) stage_r_max = rbase;
+    }
+    /* post copies are stored after the pre copies in one array */
+    dp->ncopy = pre.n + post.n;
+    dp->copies = (xg_copy *)xmalloc(sizeof(xg_copy) * (dp->ncopy + 1));
+    memcpy(dp->copies, pre.v, sizeof(xg_copy) * pre.n);
+    if (post.n) memcpy(dp->copies + pre.n, post.v, sizeof(xg_copy) * post.n);
+    for (st = 0; st < nst; ++st) dp->steps[st].post_begin += pre.n;
+    dp->np2p = pp.n;
+    dp->p2p = pp.v ? pp.v : (xg_p2p *)xmalloc(sizeof(xg_p2p));
+    dp->region_bytes[XG_BUF_STAGE_SEND] = stage_s_max;
+    dp->region_bytes[XG_BUF_STAGE_RECV] = stage_r_max;
+    free(pre.v); free(post.v); free(cnt); free(order); free(bucket_n); free(bucket_b);
+    return dp;
+}
+
+/* ------------------------------------------------------------------ fill / verify descriptors */
+int xg_fill_runs(const xg_sched *s, int ngpus, int g, xg_segrun *out)
+{
+    int lo, hi, r, n = 0;
+    xg_block_range(s->P, ngpus, g, &lo, &hi);
+    for (r = lo; r < hi; ++r) {
+        int ns = nsend_segs(s, r);
+        if (!ns) continue;
+        if (out) {   /* prepare_*_data: segment i of rank r carries seed i (:106-110, :195-199) */
+            out[n].rank = r; out[n].seed0 = 0; out[n].nsegs = ns; out[n].pad = 0;
+            out[n].off = xg_send_offset(s, ngpus, r);
+        }
+        n++;
+    }
+    return n;
+}
+
+int xg_verify_slots(const xg_sched *s, int ngpus, int g, xg_slot *out)
+{
+    int lo, hi, r, i, n = 0;
+    xg_block_range(s->P, ngpus, g, &lo, &hi);
+    for (r = lo; r < hi; ++r) {
+        int nslots = nrecv_slots(s, r), myindex = 0;
+        int64_t base;
+        if (!nslots) continue;
+        base = xg_recv_offset(s, ngpus, r);
+        for (i = 0; i < s->A; ++i)
+            if (s->rank_list[i] == r) myindex = i;
+        for (i = 0; i < nslots; ++i, ++n) {
+            if (!out) continue;
+            /* check_buffer call sites: a2m (src=i, seed=myindex) :215; m2a (src=rank_list[i], seed=rank) :139 */
+            out[n].src = s->dir == XG_A2M ? i : s->rank_list[i];
+            out[n].seed = s->dir == XG_A2M ? myindex : r;
+            out[n].dst = r; out[n].pad = 0;
+            out[n].off = base + (int64_t)i * s->d;
+        }
+    }
+    return n;
+}

@@ -1,0 +1,237 @@
+// kernels.h -- CDNA4 (gfx950) kernels of the aggregator exchange.
+//
+// All of this path is byte movement, HBM-bound; nothing is GEMM-shaped, so no
+// MFMA.  The rules that matter (MI355X_MICROARCH.md, cdna_hip_programming.md):
+// 16-B per lane accesses (global_load/store_dwordx4), several loads in flight
+// per lane before the first store, 256-thread workgroups (4 wave64s) and
+// >> 256 workgroups per launch.  No workgroup reads another's output inside a
+// launch, so no inter-workgroup hand-off protocol is needed.
+//
+//  fill_kernel   fill_buffer / MAP_DATA (mpi_test.c:71-77, :23): byte o of a
+//                segment of `rank` with seed `seed` = (rank + o + seed + iter)
+//                mod 256, produced 16 bytes per lane with SWAR byte adds.
+//  copy_kernel   the exchange itself: one workgroup per <= chunk-byte piece of
+//                a segment transfer (local gather/scatter, pack into and unpack
+//                out of RCCL staging).  Replaces the shared-memory copies MPI
+//                does inside Irecv/Issend/Alltoallw.
+//  verify_kernel check_buffer (mpi_test.c:83-92) + xg_chk64 per receive slot.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace xgk {
+
+constexpr int kThreads = 256;
+
+struct DCopy {          // one workgroup's piece of a transfer (absolute device pointers)
+    const uint8_t *src;
+    uint8_t *dst;
+    int64_t len;
+};
+
+struct DSeg {           // one segment to fingerprint
+    int64_t off;
+    int32_t rank, seed;
+};
+
+struct DSlot {          // one receive slot to verify
+    int64_t off;
+    int32_t src, seed;
+};
+
+constexpr uint64_t kGold = 0x9E3779B97F4A7C15ull;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// byte-wise add of two packed u32 (no carry between bytes)
+__device__ __forceinline__ uint32_t add_bytes(uint32_t x, uint32_t y)
+{
+    return ((x & 0x7f7f7f7fu) + (y & 0x7f7f7f7fu)) ^ ((x ^ y) & 0x80808080u);
+}
+
+// 16 reference-fingerprint bytes whose first byte is b (mod 256)
+__device__ __forceinline__ uint4 ramp16(uint32_t b)
+{
+    const uint32_t rep = (b & 0xffu) * 0x01010101u;
+    uint4 v;
+    v.x = add_bytes(rep, 0x03020100u);
+    v.y = add_bytes(rep, 0x07060504u);
+    v.z = add_bytes(rep, 0x0b0a0908u);
+    v.w = add_bytes(rep, 0x0f0e0d0cu);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t strong_key(int rank, int seed, int iter)
+{
+    return ((uint64_t)(uint32_t)rank << 42) ^ ((uint64_t)(uint32_t)seed << 21) ^ (uint64_t)(uint32_t)iter;
+}
+
+// expected 8 bytes of word q of a segment (mode 0: reference ramp; 1: strong)
+__device__ __forceinline__ uint64_t expect_word(int mode, uint32_t b0, uint64_t key, int64_t q)
+{
+    if (mode == 0) {
+        const uint32_t rep = ((b0 + (uint32_t)(q * 8)) & 0xffu) * 0x01010101u;
+        return (uint64_t)add_bytes(rep, 0x03020100u) | ((uint64_t)add_bytes(rep, 0x07060504u) << 32);
+    }
+    return mix64(key + (uint64_t)q * kGold);
+}
+
+// ---------------------------------------------------------------- fill
+__global__ __launch_bounds__(kThreads) void fill_kernel(uint8_t *__restrict__ base, const DSeg *__restrict__ segs,
+                                                        int chunks_per_seg, int64_t d, int64_t chunk, int iter,
+                                                        int mode)
+{
+    const int64_t b = blockIdx.x;
+    const DSeg sg = segs[b / chunks_per_seg];
+    const int64_t c0 = (b % chunks_per_seg) * chunk;
+    const int64_t c1 = c0 + chunk < d ? c0 + chunk : d;
+    uint8_t *p = base + sg.off;
+    const uint32_t b0 = (uint32_t)(sg.rank + sg.seed + iter);
+    const uint64_t key = strong_key(sg.rank, sg.seed, iter);
+    if ((((uintptr_t)p | (uint64_t)d) & 15) == 0) {
+        for (int64_t o = c0 + (int64_t)threadIdx.x * 16; o < c1; o += kThreads * 16) {
+            uint4 v;
+            if (mode == 0) {
+                v = ramp16(b0 + (uint32_t)o);
+            } else {
+                const uint64_t w0 = mix64(key + (uint64_t)(o >> 3) * kGold);
+                const uint64_t w1 = mix64(key + (uint64_t)((o >> 3) + 1) * kGold);
+                v.x = (uint32_t)w0; v.y = (uint32_t)(w0 >> 32); v.z = (uint32_t)w1; v.w = (uint32_t)(w1 >> 32);
+            }
+            *reinterpret_cast<uint4 *>(p + o) = v;
+        }
+    } else {
+        for (int64_t o = c0 + threadIdx.x; o < c1; o += kThreads) {
+            p[o] = mode == 0 ? (uint8_t)(b0 + (uint32_t)o)
+                             : (uint8_t)(mix64(key + (uint64_t)(o >> 3) * kGold) >> (8 * (o & 7)));
+        }
+    }
+}
+
+// ---------------------------------------------------------------- copy
+template <bool NT>
+__device__ __forceinline__ void st16(uint4 *p, uint4 v)
+{
+    if constexpr (NT) {
+        __builtin_nontemporal_store(v.x, &p->x);
+        __builtin_nontemporal_store(v.y, &p->y);
+        __builtin_nontemporal_store(v.z, &p->z);
+        __builtin_nontemporal_store(v.w, &p->w);
+    } else {
+        *p = v;
+    }
+}
+
+// One workgroup per DCopy piece.  U independent 16-B loads per lane are in
+// flight before the first store (4 KiB per wave-group step, U*4 KiB per block
+// iteration).
+template <int U, bool NT>
+__global__ __launch_bounds__(kThreads) void copy_kernel(const DCopy *__restrict__ pieces)
+{
+    const DCopy c = pieces[blockIdx.x];
+    const uint8_t *s = c.src;
+    uint8_t *t = c.dst;
+    const int64_t n = c.len;
+    if ((((uintptr_t)s | (uintptr_t)t | (uint64_t)n) & 15) == 0) {
+        const uint4 *__restrict__ s4 = reinterpret_cast<const uint4 *>(s);
+        uint4 *__restrict__ t4 = reinterpret_cast<uint4 *>(t);
+        const int64_t n4 = n >> 4;
+        int64_t i = threadIdx.x;
+        for (; i + (int64_t)(U - 1) * kThreads < n4; i += (int64_t)U * kThreads) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = s4[i + u * kThreads];
+#pragma unroll
+            for (int u = 0; u < U; ++u) st16<NT>(t4 + i + u * kThreads, v[u]);
+        }
+        for (; i < n4; i += kThreads) st16<NT>(t4 + i, s4[i]);
+    } else if ((((uintptr_t)s ^ (uintptr_t)t) & 3) == 0) {
+        // same 4-byte phase: byte head, dword body, byte tail
+        int64_t head = (4 - ((uintptr_t)s & 3)) & 3;
+        if (head > n) head = n;
+        if ((int64_t)threadIdx.x < head) t[threadIdx.x] = s[threadIdx.x];
+        const int64_t nw = (n - head) >> 2;
+        const uint32_t *s1 = reinterpret_cast<const uint32_t *>(s + head);
+        uint32_t *t1 = reinterpret_cast<uint32_t *>(t + head);
+        for (int64_t i = threadIdx.x; i < nw; i += kThreads) t1[i] = s1[i];
+        for (int64_t i = head + nw * 4 + threadIdx.x; i < n; i += kThreads) t[i] = s[i];
+    } else {
+        for (int64_t i = threadIdx.x; i < n; i += kThreads) t[i] = s[i];
+    }
+}
+
+// ---------------------------------------------------------------- verify
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_min(uint64_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = __shfl_xor(v, o, 64);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+// grid: slots x chunks; each lane hashes 8-byte words.  chk excludes the
+// length term (added on the host); first_bad = UINT64_MAX when clean.
+__global__ __launch_bounds__(kThreads) void verify_kernel(const uint8_t *__restrict__ base,
+                                                          const DSlot *__restrict__ slots, int chunks_per_slot,
+                                                          int64_t d, int64_t chunk, int iter, int mode,
+                                                          unsigned long long *chk, unsigned long long *bad,
+                                                          unsigned long long *first_bad)
+{
+    const int64_t b = blockIdx.x;
+    const int si = (int)(b / chunks_per_slot);
+    const DSlot sl = slots[si];
+    const int64_t c0 = (b % chunks_per_slot) * chunk;           // chunk is a multiple of 8
+    const int64_t c1 = c0 + chunk < d ? c0 + chunk : d;
+    const uint8_t *p = base + sl.off;
+    const uint32_t b0 = (uint32_t)(sl.src + sl.seed + iter);
+    const uint64_t key = strong_key(sl.src, sl.seed, iter);
+    const bool aligned = (((uintptr_t)p) & 7) == 0;
+    uint64_t sum = 0, nbad = 0, first = ~0ull;
+    for (int64_t o = c0 + (int64_t)threadIdx.x * 8; o < c1; o += kThreads * 8) {
+        const int64_t q = o >> 3;
+        const int nb = c1 - o >= 8 ? 8 : (int)(c1 - o);
+        uint64_t w = 0;
+        if (aligned && nb == 8) {
+            w = *reinterpret_cast<const uint64_t *>(p + o);
+        } else {
+            for (int j = 0; j < nb; ++j) w |= (uint64_t)p[o + j] << (8 * j);
+        }
+        uint64_t e = expect_word(mode, b0, key, q);
+        if (nb < 8) e &= (1ull << (8 * nb)) - 1;
+        sum += mix64(w ^ ((uint64_t)q * kGold));
+        uint64_t x = w ^ e;
+        if (x) {
+            for (int j = 0; j < nb; ++j)
+                if ((x >> (8 * j)) & 0xff) {
+                    ++nbad;
+                    if ((uint64_t)(o + j) < first) first = (uint64_t)(o + j);
+                }
+        }
+    }
+    sum = wave_sum(sum);
+    nbad = wave_sum(nbad);
+    first = wave_min(first);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&chk[si], (unsigned long long)sum);
+        if (nbad) {
+            atomicAdd(&bad[si], (unsigned long long)nbad);
+            atomicMin(&first_bad[si], (unsigned long long)first);
+        }
+    }
+}
+
+}  // namespace xgk

@@ -1,0 +1,514 @@
+// xg_runtime.hip -- device half of the C-ABI (include/xg.h): HBM regions,
+// kernel launches, grouped RCCL exchange, step timing.  gfx950 only.
+//
+// Execution of one step on GPU g (xg_devplan, built by libxghost):
+//   1. one copy_kernel launch over every local gather/scatter piece and every
+//      pack into the per-peer staging region                (pre copies)
+//   2. one ncclGroupStart .. ncclSend/ncclRecv .. ncclGroupEnd with the <= 7
+//      peer GPUs this step talks to (xGMI)                  (p2p)
+//   3. one copy_kernel launch unpacking staging into the receive slots (post)
+//   4. hipEventRecord(step event)     -- the reference's Waitall boundary
+// All on one HIP stream per context, so step s+1 starts after step s; the
+// cross-GPU order comes from RCCL send/recv matching.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <vector>
+
+#include "kernels.h"
+#include "xg.h"
+
+#define HIPCHK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                    \
+            fprintf(stderr, "xg: HIP error %s at %s:%d: %s\n", hipGetErrorString(e_), __FILE__,   \
+                    __LINE__, #x);                                                                 \
+            return XG_EHIP;                                                                        \
+        }                                                                                          \
+    } while (0)
+
+#define NCCLCHK(x)                                                                                 \
+    do {                                                                                           \
+        ncclResult_t r_ = (x);                                                                     \
+        if (r_ != ncclSuccess) {                                                                   \
+            fprintf(stderr, "xg: RCCL error %s at %s:%d: %s\n", ncclGetErrorString(r_), __FILE__, \
+                    __LINE__, #x);                                                                 \
+            return XG_ERCCL;                                                                       \
+        }                                                                                          \
+    } while (0)
+
+struct xg_ctx {
+    int rank, nranks, device;
+    hipStream_t stream;
+    ncclComm_t comm;
+    double *d_red;          // device scratch for barrier / MAX reductions
+    int64_t chunk;          // bytes per copy workgroup
+    int variant;            // copy kernel variant
+    // kernel timing session (xg_ktime_begin/end)
+    bool kt_on;
+    int nk;
+    std::vector<hipEvent_t> kev;   // start/end pairs per copy launch
+    std::vector<int64_t> kbytes;   // algorithmic bytes (read + write) per launch
+};
+
+struct xg_regions {
+    xg_ctx *ctx;
+    uint8_t *ptr[4];
+    int64_t bytes[4];
+};
+
+struct StepR {
+    int pre_b, pre_n, post_b, post_n, p2p_b, p2p_n;
+    int64_t pre_bytes, post_bytes;   // bytes copied by each launch (read once + written once)
+};
+
+struct xg_plan {
+    xg_ctx *ctx;
+    xg_regions *reg;
+    int nsteps;
+    xgk::DCopy *d_pieces;
+    int npieces;
+    std::vector<StepR> steps;
+    std::vector<xg_p2p> p2p;
+    std::vector<hipEvent_t> ev;
+    hipEvent_t ev0;
+    int variant;
+};
+
+extern "C" double xg_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+// ------------------------------------------------------------------ context
+extern "C" int xg_get_unique_id(void *uid)
+{
+    ncclUniqueId id;
+    static_assert(sizeof(ncclUniqueId) == XG_UNIQUE_ID_BYTES, "unique id size");
+    NCCLCHK(ncclGetUniqueId(&id));
+    memcpy(uid, &id, sizeof id);
+    return XG_OK;
+}
+
+extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const void *uid)
+{
+    int ndev = 0;
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks) return XG_EARG;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) {
+        fprintf(stderr, "xg: device %d not present (%d visible)\n", device, ndev);
+        return XG_EARG;
+    }
+    HIPCHK(hipSetDevice(device));
+    xg_ctx *c = new xg_ctx();
+    c->rank = rank; c->nranks = nranks; c->device = device; c->comm = nullptr;
+    c->chunk = 65536; c->variant = 0; c->kt_on = false; c->nk = 0;
+    const char *env = getenv("XG_COPY_CHUNK");
+    if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
+    env = getenv("XG_COPY_VARIANT");
+    if (env) c->variant = atoi(env);
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&c->d_red, 64 * sizeof(double)));
+    if (nranks > 1) {
+        ncclUniqueId id;
+        if (!uid) return XG_EARG;
+        memcpy(&id, uid, sizeof id);
+        NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
+    }
+    *out = c;
+    return XG_OK;
+}
+
+extern "C" int xg_finalize(xg_ctx *c)
+{
+    if (!c) return XG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->comm) NCCLCHK(ncclCommDestroy(c->comm));
+    for (auto &e : c->kev) HIPCHK(hipEventDestroy(e));
+    HIPCHK(hipFree(c->d_red));
+    HIPCHK(hipStreamDestroy(c->stream));
+    delete c;
+    return XG_OK;
+}
+
+extern "C" int xg_rank(const xg_ctx *c) { return c->rank; }
+extern "C" int xg_nranks(const xg_ctx *c) { return c->nranks; }
+
+extern "C" int xg_sync(xg_ctx *c)
+{
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return XG_OK;
+}
+
+extern "C" int xg_allreduce_max(xg_ctx *c, double *vals, int n)
+{
+    if (n < 0 || n > 64) return XG_EARG;
+    if (c->nranks == 1 || n == 0) return XG_OK;
+    HIPCHK(hipMemcpyAsync(c->d_red, vals, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(ncclAllReduce(c->d_red, c->d_red, n, ncclFloat64, ncclMax, c->comm, c->stream));
+    HIPCHK(hipMemcpyAsync(vals, c->d_red, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return XG_OK;
+}
+
+extern "C" int xg_barrier(xg_ctx *c)
+{
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->nranks > 1) {
+        NCCLCHK(ncclAllReduce(c->d_red, c->d_red, 1, ncclFloat64, ncclMax, c->comm, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return XG_OK;
+}
+
+extern "C" int xg_device_info(xg_ctx *c, char *name, size_t namelen, int *cus, size_t *hbm)
+{
+    hipDeviceProp_t p;
+    HIPCHK(hipGetDeviceProperties(&p, c->device));
+    if (name && namelen) { strncpy(name, p.gcnArchName, namelen - 1); name[namelen - 1] = 0; }
+    if (cus) *cus = p.multiProcessorCount;
+    if (hbm) *hbm = p.totalGlobalMem;
+    return XG_OK;
+}
+
+extern "C" int xg_set_copy_params(xg_ctx *c, int64_t chunk, int variant)
+{
+    if (chunk >= 4096) c->chunk = chunk & ~(int64_t)15;
+    c->variant = variant;
+    return XG_OK;
+}
+
+// ------------------------------------------------------------------ regions
+extern "C" int xg_regions_alloc(xg_ctx *c, const int64_t bytes[4], xg_regions **out)
+{
+    HIPCHK(hipSetDevice(c->device));
+    xg_regions *r = new xg_regions();
+    r->ctx = c;
+    for (int i = 0; i < 4; ++i) {
+        r->bytes[i] = bytes[i];
+        r->ptr[i] = nullptr;
+        if (bytes[i] > 0) {
+            hipError_t e = hipMalloc(&r->ptr[i], (size_t)bytes[i]);
+            if (e != hipSuccess) {
+                fprintf(stderr, "xg: hipMalloc(%lld) for region %d failed: %s\n", (long long)bytes[i], i,
+                        hipGetErrorString(e));
+                for (int j = 0; j < i; ++j) (void)hipFree(r->ptr[j]);
+                delete r;
+                return XG_ENOMEM;
+            }
+        }
+    }
+    *out = r;
+    return xg_regions_poison(r);
+}
+
+extern "C" int xg_regions_poison(xg_regions *r)
+{
+    if (r->bytes[XG_BUF_RECV] > 0)
+        HIPCHK(hipMemsetAsync(r->ptr[XG_BUF_RECV], 0xA5, (size_t)r->bytes[XG_BUF_RECV], r->ctx->stream));
+    HIPCHK(hipStreamSynchronize(r->ctx->stream));
+    return XG_OK;
+}
+
+extern "C" int xg_regions_free(xg_regions *r)
+{
+    if (!r) return XG_OK;
+    HIPCHK(hipStreamSynchronize(r->ctx->stream));
+    for (int i = 0; i < 4; ++i)
+        if (r->ptr[i]) HIPCHK(hipFree(r->ptr[i]));
+    delete r;
+    return XG_OK;
+}
+
+extern "C" void *xg_regions_ptr(xg_regions *r, int buf) { return buf >= 0 && buf < 4 ? r->ptr[buf] : nullptr; }
+
+extern "C" int xg_regions_read(xg_regions *r, int buf, int64_t off, void *host, int64_t len)
+{
+    if (buf < 0 || buf > 3 || off < 0 || len < 0 || off + len > r->bytes[buf]) return XG_EARG;
+    HIPCHK(hipMemcpyAsync(host, r->ptr[buf] + off, (size_t)len, hipMemcpyDeviceToHost, r->ctx->stream));
+    HIPCHK(hipStreamSynchronize(r->ctx->stream));
+    return XG_OK;
+}
+
+// ------------------------------------------------------------------ fill / verify
+extern "C" int xg_fill(xg_regions *r, const xg_segrun *runs, int nruns, int64_t d, int iter, int mode)
+{
+    xg_ctx *c = r->ctx;
+    std::vector<xgk::DSeg> segs;
+    for (int i = 0; i < nruns; ++i)
+        for (int k = 0; k < runs[i].nsegs; ++k) {
+            xgk::DSeg s;
+            s.off = runs[i].off + (int64_t)k * d;
+            s.rank = runs[i].rank;
+            s.seed = runs[i].seed0 + k;
+            if (s.off < 0 || s.off + d > r->bytes[XG_BUF_SEND]) {
+                fprintf(stderr, "xg_fill: segment outside the send region\n");
+                return XG_EARG;
+            }
+            segs.push_back(s);
+        }
+    if (segs.empty() || d == 0) return XG_OK;
+    const int64_t chunk = 65536;
+    const int64_t cps = (d + chunk - 1) / chunk;
+    if ((int64_t)segs.size() * cps > 0x7fffffff) return XG_EARG;
+    xgk::DSeg *dsegs;
+    HIPCHK(hipMalloc(&dsegs, sizeof(xgk::DSeg) * segs.size()));
+    HIPCHK(hipMemcpyAsync(dsegs, segs.data(), sizeof(xgk::DSeg) * segs.size(), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(xgk::fill_kernel, dim3((unsigned)(segs.size() * cps)), dim3(xgk::kThreads), 0, c->stream,
+                       r->ptr[XG_BUF_SEND], dsegs, (int)cps, d, chunk, iter, mode);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipFree(dsegs));
+    return XG_OK;
+}
+
+extern "C" int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_t d, int iter, int mode,
+                         uint64_t *chk, int64_t *bad, int64_t *first_bad)
+{
+    xg_ctx *c = r->ctx;
+    if (nslots <= 0) return XG_OK;
+    std::vector<xgk::DSlot> sl(nslots);
+    for (int i = 0; i < nslots; ++i) {
+        sl[i].off = slots[i].off; sl[i].src = slots[i].src; sl[i].seed = slots[i].seed;
+        if (sl[i].off < 0 || sl[i].off + d > r->bytes[XG_BUF_RECV]) return XG_EARG;
+    }
+    const int64_t chunk = 65536;
+    const int64_t cps = d > 0 ? (d + chunk - 1) / chunk : 1;
+    xgk::DSlot *dsl;
+    unsigned long long *dout;
+    HIPCHK(hipMalloc(&dsl, sizeof(xgk::DSlot) * nslots));
+    HIPCHK(hipMalloc(&dout, sizeof(unsigned long long) * 3 * nslots));
+    HIPCHK(hipMemcpyAsync(dsl, sl.data(), sizeof(xgk::DSlot) * nslots, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(dout, 0, sizeof(unsigned long long) * 2 * nslots, c->stream));
+    HIPCHK(hipMemsetAsync(dout + 2 * nslots, 0xff, sizeof(unsigned long long) * nslots, c->stream));
+    if (d > 0) {
+        hipLaunchKernelGGL(xgk::verify_kernel, dim3((unsigned)(nslots * cps)), dim3(xgk::kThreads), 0, c->stream,
+                           r->ptr[XG_BUF_RECV], dsl, (int)cps, d, chunk, iter, mode, dout, dout + nslots,
+                           dout + 2 * nslots);
+        HIPCHK(hipGetLastError());
+    }
+    std::vector<unsigned long long> h(3 * (size_t)nslots);
+    HIPCHK(hipMemcpyAsync(h.data(), dout, sizeof(unsigned long long) * 3 * nslots, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipFree(dsl));
+    HIPCHK(hipFree(dout));
+    const uint64_t lenk = 0xD6E8FEB86659FD93ull * (uint64_t)d;
+    for (int i = 0; i < nslots; ++i) {
+        if (chk) chk[i] = h[i] + lenk;
+        if (bad) bad[i] = (int64_t)h[nslots + i];
+        if (first_bad) first_bad[i] = h[2 * nslots + i] == ~0ull ? -1 : (int64_t)h[2 * nslots + i];
+    }
+    return XG_OK;
+}
+
+// ------------------------------------------------------------------ plans
+extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_plan **out)
+{
+    if (!c || !r || !dp || !out) return XG_EARG;
+    if (dp->ngpus != c->nranks || dp->gpu != c->rank) {
+        fprintf(stderr, "xg_plan_load: plan for gpu %d/%d loaded on rank %d/%d\n", dp->gpu, dp->ngpus, c->rank,
+                c->nranks);
+        return XG_EARG;
+    }
+    for (int i = 0; i < 4; ++i)
+        if (dp->region_bytes[i] > r->bytes[i]) {
+            fprintf(stderr, "xg_plan_load: region %d too small (%lld < %lld)\n", i, (long long)r->bytes[i],
+                    (long long)dp->region_bytes[i]);
+            return XG_EARG;
+        }
+    HIPCHK(hipSetDevice(c->device));
+    xg_plan *p = new xg_plan();
+    p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant;
+    const int64_t chunk = c->chunk;
+    std::vector<xgk::DCopy> pieces;
+    auto add = [&](const xg_copy &cp) -> bool {
+        if (cp.len <= 0) return true;
+        if (cp.src_off < 0 || cp.dst_off < 0 || cp.src_off + cp.len > r->bytes[cp.src_buf] ||
+            cp.dst_off + cp.len > r->bytes[cp.dst_buf])
+            return false;
+        for (int64_t o = 0; o < cp.len; o += chunk) {
+            xgk::DCopy d;
+            d.src = r->ptr[cp.src_buf] + cp.src_off + o;
+            d.dst = r->ptr[cp.dst_buf] + cp.dst_off + o;
+            d.len = cp.len - o < chunk ? cp.len - o : chunk;
+            pieces.push_back(d);
+        }
+        return true;
+    };
+    p->steps.resize(dp->nsteps);
+    for (int s = 0; s < dp->nsteps; ++s) {
+        const xg_stepplan &sp = dp->steps[s];
+        StepR &st = p->steps[s];
+        st.pre_b = (int)pieces.size();
+        for (int i = 0; i < sp.pre_count; ++i)
+            if (!add(dp->copies[sp.pre_begin + i])) goto bad;
+        st.pre_n = (int)pieces.size() - st.pre_b;
+        st.pre_bytes = 0;
+        for (int i = st.pre_b; i < st.pre_b + st.pre_n; ++i) st.pre_bytes += pieces[i].len;
+        st.post_b = (int)pieces.size();
+        for (int i = 0; i < sp.post_count; ++i)
+            if (!add(dp->copies[sp.post_begin + i])) goto bad;
+        st.post_n = (int)pieces.size() - st.post_b;
+        st.post_bytes = 0;
+        for (int i = st.post_b; i < st.post_b + st.post_n; ++i) st.post_bytes += pieces[i].len;
+        st.p2p_b = (int)p->p2p.size();
+        for (int i = 0; i < sp.p2p_count; ++i) {
+            const xg_p2p &o = dp->p2p[sp.p2p_begin + i];
+            if (o.peer < 0 || o.peer >= c->nranks || o.peer == c->rank || o.off < 0 ||
+                o.off + o.len > r->bytes[o.buf])
+                goto bad;
+            p->p2p.push_back(o);
+        }
+        st.p2p_n = (int)p->p2p.size() - st.p2p_b;
+    }
+    p->npieces = (int)pieces.size();
+    p->d_pieces = nullptr;
+    if (p->npieces) {
+        HIPCHK(hipMalloc(&p->d_pieces, sizeof(xgk::DCopy) * pieces.size()));
+        HIPCHK(hipMemcpy(p->d_pieces, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
+    }
+    p->ev.resize(dp->nsteps);
+    for (auto &e : p->ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipEventCreate(&p->ev0));
+    *out = p;
+    return XG_OK;
+bad:
+    fprintf(stderr, "xg_plan_load: copy or p2p descriptor outside its region\n");
+    delete p;
+    return XG_EARG;
+}
+
+extern "C" int xg_plan_free(xg_plan *p)
+{
+    if (!p) return XG_OK;
+    HIPCHK(hipStreamSynchronize(p->ctx->stream));
+    if (p->d_pieces) HIPCHK(hipFree(p->d_pieces));
+    for (auto &e : p->ev) HIPCHK(hipEventDestroy(e));
+    HIPCHK(hipEventDestroy(p->ev0));
+    delete p;
+    return XG_OK;
+}
+
+extern "C" int xg_plan_nsteps(const xg_plan *p) { return p->nsteps; }
+
+static int launch_copy(xg_plan *p, int b, int n)
+{
+    hipStream_t st = p->ctx->stream;
+    const xgk::DCopy *pc = p->d_pieces + b;
+    switch (p->variant) {
+    case 1: hipLaunchKernelGGL((xgk::copy_kernel<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 2: hipLaunchKernelGGL((xgk::copy_kernel<8, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 3: hipLaunchKernelGGL((xgk::copy_kernel<8, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 4: hipLaunchKernelGGL((xgk::copy_kernel<2, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    default: hipLaunchKernelGGL((xgk::copy_kernel<4, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    }
+    HIPCHK(hipGetLastError());
+    return XG_OK;
+}
+
+static int enqueue_step(xg_plan *p, int s)
+{
+    xg_ctx *c = p->ctx;
+    const StepR &st = p->steps[s];
+    int rc;
+    auto timed = [&](int b, int n, int64_t bytes) -> int {
+        const bool kt = c->kt_on && 2 * (size_t)c->nk + 1 < c->kev.size();
+        if (kt) HIPCHK(hipEventRecord(c->kev[2 * c->nk], c->stream));
+        if ((rc = launch_copy(p, b, n))) return rc;
+        if (kt) {
+            HIPCHK(hipEventRecord(c->kev[2 * c->nk + 1], c->stream));
+            c->kbytes[c->nk] = 2 * bytes;      // algorithmic HBM bytes: read + write
+            c->nk++;
+        }
+        return XG_OK;
+    };
+    if (st.pre_n && (rc = timed(st.pre_b, st.pre_n, st.pre_bytes))) return rc;
+    if (st.p2p_n) {
+        NCCLCHK(ncclGroupStart());
+        for (int i = 0; i < st.p2p_n; ++i) {
+            const xg_p2p &o = p->p2p[st.p2p_b + i];
+            uint8_t *ptr = p->reg->ptr[o.buf] + o.off;
+            if (o.is_send)
+                NCCLCHK(ncclSend(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream));
+            else
+                NCCLCHK(ncclRecv(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream));
+        }
+        NCCLCHK(ncclGroupEnd());
+    }
+    if (st.post_n && (rc = timed(st.post_b, st.post_n, st.post_bytes))) return rc;
+    return XG_OK;
+}
+
+extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
+{
+    xg_ctx *c = p->ctx;
+    int rc;
+    HIPCHK(hipSetDevice(c->device));
+    const double t0 = xg_now();
+    HIPCHK(hipEventRecord(p->ev0, c->stream));
+    for (int s = 0; s < p->nsteps; ++s) {
+        const double tp = xg_now();
+        if ((rc = enqueue_step(p, s))) return rc;
+        HIPCHK(hipEventRecord(p->ev[s], c->stream));
+        if (step_post) step_post[s] = xg_now() - tp;
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (wall) *wall = xg_now() - t0;
+    if (step_done)
+        for (int s = 0; s < p->nsteps; ++s) {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[s]));
+            step_done[s] = ms * 1e-3;
+        }
+    return XG_OK;
+}
+
+extern "C" int xg_plan_enqueue(xg_plan *p)
+{
+    int rc;
+    for (int s = 0; s < p->nsteps; ++s)
+        if ((rc = enqueue_step(p, s))) return rc;
+    return XG_OK;
+}
+
+extern "C" int xg_ktime_begin(xg_ctx *c, int max_launches)
+{
+    if (max_launches < 1) return XG_EARG;
+    HIPCHK(hipSetDevice(c->device));
+    while (c->kev.size() < 2 * (size_t)max_launches) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        c->kev.push_back(e);
+    }
+    c->kbytes.resize(max_launches);
+    c->nk = 0;
+    c->kt_on = true;
+    return XG_OK;
+}
+
+extern "C" int xg_ktime_end(xg_ctx *c, double *total_ms, int *launches, int64_t *bytes)
+{
+    double tot = 0;
+    int64_t b = 0;
+    c->kt_on = false;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int k = 0; k < c->nk; ++k) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, c->kev[2 * k], c->kev[2 * k + 1]));
+        tot += ms;
+        b += c->kbytes[k];
+    }
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = c->nk;
+    if (bytes) *bytes = b;
+    return XG_OK;
+}

@@ -1,0 +1,383 @@
+"""ctypes binding of the framework's C-ABI (include/xg_sched.h, include/xg.h).
+
+Python is only the harness here (bench.py, tests): every byte of the exchange
+is moved by lib/libxg.so (HIP kernels + RCCL) and every schedule comes from
+lib/libxghost.so.  There is no fallback: if a library is missing, loading
+fails with an error that says how to build it.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(HERE, "lib")
+
+
+class XGError(RuntimeError):
+    pass
+
+
+class Timer(C.Structure):
+    """Timer of the reference (mpi_test.c:25-31)."""
+    _fields_ = [("post_request_time", C.c_double), ("send_wait_all_time", C.c_double),
+                ("recv_wait_all_time", C.c_double), ("barrier_time", C.c_double),
+                ("total_time", C.c_double)]
+
+    def as_tuple(self):
+        return (self.post_request_time, self.send_wait_all_time, self.recv_wait_all_time,
+                self.barrier_time, self.total_time)
+
+
+class Msg(C.Structure):
+    _fields_ = [("src", C.c_int32), ("sseg", C.c_int32), ("dst", C.c_int32), ("dslot", C.c_int32),
+                ("len", C.c_int64), ("step", C.c_int32), ("flags", C.c_int32)]
+
+
+class Copy(C.Structure):
+    _fields_ = [("src_off", C.c_int64), ("dst_off", C.c_int64), ("len", C.c_int64),
+                ("src_buf", C.c_int32), ("dst_buf", C.c_int32)]
+
+
+class P2P(C.Structure):
+    _fields_ = [("off", C.c_int64), ("len", C.c_int64), ("peer", C.c_int32), ("buf", C.c_int32),
+                ("is_send", C.c_int32), ("pad", C.c_int32)]
+
+
+class StepPlan(C.Structure):
+    _fields_ = [("pre_begin", C.c_int32), ("pre_count", C.c_int32), ("p2p_begin", C.c_int32),
+                ("p2p_count", C.c_int32), ("post_begin", C.c_int32), ("post_count", C.c_int32)]
+
+
+class DevPlan(C.Structure):
+    _fields_ = [("gpu", C.c_int32), ("ngpus", C.c_int32), ("nsteps", C.c_int32), ("pad", C.c_int32),
+                ("region_bytes", C.c_int64 * 4), ("ncopy", C.c_int32), ("np2p", C.c_int32),
+                ("copies", C.POINTER(Copy)), ("p2p", C.POINTER(P2P)), ("steps", C.POINTER(StepPlan)),
+                ("local_bytes", C.c_int64), ("remote_send_bytes", C.c_int64),
+                ("remote_recv_bytes", C.c_int64)]
+
+
+A2M, M2A = 0, 1
+BUF_SEND, BUF_RECV, BUF_STAGE_SEND, BUF_STAGE_RECV = 0, 1, 2, 3
+MPICH_EAGER_LIMIT = 65424
+
+
+def _load(name):
+    path = os.path.join(LIBDIR, name)
+    if not os.path.exists(path):
+        raise XGError("%s not built: run `make -C %s` (or __graft_entry__.build())" % (path, HERE))
+    return C.CDLL(path, mode=C.RTLD_GLOBAL)
+
+
+_host = None
+_dev = None
+
+
+def host():
+    global _host
+    if _host is None:
+        h = _load("libxghost.so")
+        h.xg_aggregator_list.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
+        h.xg_method_label.restype = C.c_char_p
+        h.xg_method_label.argtypes = [C.c_int]
+        h.xg_method_direction.argtypes = [C.c_int]
+        h.xg_sched_build.restype = C.c_void_p
+        h.xg_sched_build.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_int),
+                                     C.c_int, C.c_int64, C.c_char_p, C.c_size_t]
+        h.xg_sched_free.argtypes = [C.c_void_p]
+        for fn in ("xg_sched_nmsg", "xg_sched_nsteps", "xg_sched_direction", "xg_sched_procs"):
+            getattr(h, fn).argtypes = [C.c_void_p]
+        h.xg_sched_msgs.restype = C.POINTER(Msg)
+        h.xg_sched_msgs.argtypes = [C.c_void_p]
+        h.xg_sched_trace.restype = C.c_size_t
+        h.xg_sched_trace.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_size_t]
+        h.xg_sched_rank_timer.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double),
+                                          C.POINTER(C.c_double), C.POINTER(Timer)]
+        h.xg_block_range.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        h.xg_gpu_of.argtypes = [C.c_int, C.c_int, C.c_int]
+        for fn in ("xg_send_offset", "xg_recv_offset"):
+            getattr(h, fn).restype = C.c_int64
+            getattr(h, fn).argtypes = [C.c_void_p, C.c_int, C.c_int]
+        h.xg_region_bytes.restype = C.c_int64
+        h.xg_region_bytes.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+        h.xg_devplan_build.restype = C.POINTER(DevPlan)
+        h.xg_devplan_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64]
+        h.xg_devplan_free.argtypes = [C.POINTER(DevPlan)]
+        _host = h
+    return _host
+
+
+def aggregator_list(procs, cb_nodes, proc_node=1, agg_type=1):
+    rl = (C.c_int * cb_nodes)()
+    if host().xg_aggregator_list(procs, cb_nodes, proc_node, agg_type, rl) != 0:
+        raise XGError("aggregator type %d is not defined by the reference" % agg_type)
+    return list(rl)
+
+
+def method_label(method):
+    lab = host().xg_method_label(method)
+    return lab.decode() if lab else None
+
+
+class Schedule:
+    """One method run (all -k repetitions), compiled to device-wide steps."""
+
+    def __init__(self, method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes=1,
+                 eager_limit=MPICH_EAGER_LIMIT):
+        h = host()
+        self.method, self.P, self.A, self.d, self.c = method, procs, cb_nodes, data_size, comm_size
+        self.rank_list = list(rank_list)
+        self.ntimes = ntimes
+        err = C.create_string_buffer(512)
+        rl = (C.c_int * cb_nodes)(*rank_list)
+        self._h = h.xg_sched_build(method, procs, cb_nodes, data_size, comm_size, rl, ntimes,
+                                   eager_limit, err, 512)
+        if not self._h:
+            raise XGError(err.value.decode())
+        self.nsteps = h.xg_sched_nsteps(self._h)
+        self.direction = h.xg_sched_direction(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _host is not None:
+            _host.xg_sched_free(self._h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def messages(self):
+        n = host().xg_sched_nmsg(self._h)
+        ptr = host().xg_sched_msgs(self._h)
+        return [(m.src, m.sseg, m.dst, m.dslot, m.len, m.step, m.flags) for m in ptr[:n]]
+
+    def trace(self, rank):
+        n = host().xg_sched_trace(self._h, rank, None, 0)
+        buf = C.create_string_buffer(n + 1)
+        host().xg_sched_trace(self._h, rank, buf, n + 1)
+        return buf.value.decode()
+
+    def rank_timer(self, rank, step_done, step_post=None):
+        nd = (C.c_double * max(1, len(step_done)))(*step_done)
+        npost = (C.c_double * max(1, len(step_post)))(*step_post) if step_post is not None else None
+        t = Timer()
+        host().xg_sched_rank_timer(self._h, rank, nd, npost, C.byref(t))
+        return t
+
+    def gpu_of(self, ngpus, rank):
+        return host().xg_gpu_of(self.P, ngpus, rank)
+
+    def block_range(self, ngpus, g):
+        lo, hi = C.c_int(), C.c_int()
+        host().xg_block_range(self.P, ngpus, g, C.byref(lo), C.byref(hi))
+        return lo.value, hi.value
+
+    def send_offset(self, ngpus, rank):
+        return host().xg_send_offset(self._h, ngpus, rank)
+
+    def recv_offset(self, ngpus, rank):
+        return host().xg_recv_offset(self._h, ngpus, rank)
+
+    def region_bytes(self, ngpus, g, buf):
+        return host().xg_region_bytes(self._h, ngpus, g, buf)
+
+    def devplan(self, ngpus, g, pack_max_seg=1 << 20):
+        return DevicePlanView(self, ngpus, g, pack_max_seg)
+
+
+class DevicePlanView:
+    """Python view of xg_devplan (host memory), used by the CPU plan tests."""
+
+    def __init__(self, sched, ngpus, g, pack_max_seg):
+        self.sched = sched
+        self._p = host().xg_devplan_build(sched.handle, ngpus, g, pack_max_seg)
+        p = self._p.contents
+        self.gpu, self.ngpus, self.nsteps = p.gpu, p.ngpus, p.nsteps
+        self.region_bytes = list(p.region_bytes)
+        self.copies = [(c.src_buf, c.src_off, c.dst_buf, c.dst_off, c.len) for c in p.copies[:p.ncopy]]
+        self.p2p = [(o.peer, o.is_send, o.buf, o.off, o.len) for o in p.p2p[:p.np2p]]
+        self.steps = [(s.pre_begin, s.pre_count, s.p2p_begin, s.p2p_count, s.post_begin, s.post_count)
+                      for s in p.steps[:p.nsteps]]
+        self.local_bytes = p.local_bytes
+        self.remote_send_bytes = p.remote_send_bytes
+        self.remote_recv_bytes = p.remote_recv_bytes
+
+    @property
+    def ptr(self):
+        return self._p
+
+    def __del__(self):
+        if getattr(self, "_p", None) and _host is not None:
+            _host.xg_devplan_free(self._p)
+            self._p = None
+
+
+# --------------------------------------------------------------------------- device (libxg.so)
+class SegRun(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("seed0", C.c_int32), ("off", C.c_int64), ("nsegs", C.c_int32),
+                ("pad", C.c_int32)]
+
+
+class Slot(C.Structure):
+    _fields_ = [("src", C.c_int32), ("seed", C.c_int32), ("dst", C.c_int32), ("pad", C.c_int32),
+                ("off", C.c_int64)]
+
+
+def device():
+    """libxg.so -- the HIP/RCCL half.  Loading it does not touch the GPU."""
+    global _dev
+    if _dev is None:
+        host()
+        d = _load("libxg.so")
+        vp, ip, i64 = C.c_void_p, C.c_int, C.c_int64
+        d.xg_get_unique_id.argtypes = [vp]
+        d.xg_init.argtypes = [C.POINTER(vp), ip, ip, ip, vp]
+        d.xg_finalize.argtypes = [vp]
+        d.xg_barrier.argtypes = [vp]
+        d.xg_sync.argtypes = [vp]
+        d.xg_allreduce_max.argtypes = [vp, C.POINTER(C.c_double), ip]
+        d.xg_device_info.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(ip), C.POINTER(C.c_size_t)]
+        d.xg_now.restype = C.c_double
+        d.xg_regions_alloc.argtypes = [vp, C.POINTER(i64), C.POINTER(vp)]
+        d.xg_regions_free.argtypes = [vp]
+        d.xg_regions_poison.argtypes = [vp]
+        d.xg_regions_ptr.restype = vp
+        d.xg_regions_ptr.argtypes = [vp, ip]
+        d.xg_regions_read.argtypes = [vp, ip, i64, vp, i64]
+        d.xg_fill.argtypes = [vp, C.POINTER(SegRun), ip, i64, ip, ip]
+        d.xg_verify.argtypes = [vp, C.POINTER(Slot), ip, i64, ip, ip, C.POINTER(C.c_uint64),
+                                C.POINTER(i64), C.POINTER(i64)]
+        d.xg_plan_load.argtypes = [vp, vp, C.POINTER(DevPlan), C.POINTER(vp)]
+        d.xg_plan_free.argtypes = [vp]
+        d.xg_plan_nsteps.argtypes = [vp]
+        d.xg_plan_run.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        d.xg_plan_enqueue.argtypes = [vp]
+        d.xg_ktime_begin.argtypes = [vp, ip]
+        d.xg_ktime_end.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(ip), C.POINTER(i64)]
+        d.xg_set_copy_params.argtypes = [vp, i64, ip]
+        h = host()
+        h.xg_fill_runs.argtypes = [vp, ip, ip, C.POINTER(SegRun)]
+        h.xg_verify_slots.argtypes = [vp, ip, ip, C.POINTER(Slot)]
+        _dev = d
+    return _dev
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise XGError("%s failed with code %d (see stderr)" % (what, rc))
+
+
+def unique_id():
+    buf = C.create_string_buffer(128)
+    _check(device().xg_get_unique_id(buf), "xg_get_unique_id")
+    return buf.raw
+
+
+class Context:
+    """One process = one GPU (xg_init).  nranks > 1 needs rank 0's unique_id()."""
+
+    def __init__(self, rank=0, nranks=1, device_index=None, uid=None, device=None):
+        d = globals()["device"]()
+        dev = device if device is not None else (device_index if device_index is not None else rank)
+        self._c = C.c_void_p()
+        ub = C.create_string_buffer(uid, 128) if uid else None
+        _check(d.xg_init(C.byref(self._c), rank, nranks, dev, ub), "xg_init")
+        self.rank, self.nranks = rank, nranks
+
+    @property
+    def handle(self):
+        return self._c
+
+    def barrier(self):
+        _check(_dev.xg_barrier(self._c), "xg_barrier")
+
+    def sync(self):
+        _check(_dev.xg_sync(self._c), "xg_sync")
+
+    def allreduce_max(self, vals):
+        arr = (C.c_double * len(vals))(*vals)
+        _check(_dev.xg_allreduce_max(self._c, arr, len(vals)), "xg_allreduce_max")
+        return list(arr)
+
+    def info(self):
+        name = C.create_string_buffer(64)
+        cus, hbm = C.c_int(), C.c_size_t()
+        _check(_dev.xg_device_info(self._c, name, 64, C.byref(cus), C.byref(hbm)), "xg_device_info")
+        return name.value.decode(), cus.value, hbm.value
+
+    def set_copy_params(self, chunk=0, variant=0):
+        _check(_dev.xg_set_copy_params(self._c, chunk, variant), "xg_set_copy_params")
+
+    def ktime_begin(self, max_launches=4096):
+        _check(_dev.xg_ktime_begin(self._c, max_launches), "xg_ktime_begin")
+
+    def ktime_end(self):
+        ms, n, b = C.c_double(), C.c_int(), C.c_int64()
+        _check(_dev.xg_ktime_end(self._c, C.byref(ms), C.byref(n), C.byref(b)), "xg_ktime_end")
+        return ms.value, n.value, b.value
+
+    def close(self):
+        if self._c:
+            _check(_dev.xg_finalize(self._c), "xg_finalize")
+            self._c = None
+
+
+def now():
+    return device().xg_now()
+
+
+class MethodRun:
+    """prepare_*_data + the compiled plan of one method on this GPU:
+    HBM regions, fingerprint fill (untimed), plan upload."""
+
+    def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=1 << 20):
+        d = device()
+        self.ctx, self.sched, self.it, self.mode = ctx, sched, it, mode
+        G, g = ctx.nranks, ctx.rank
+        self.view = sched.devplan(G, g, pack_max_seg)
+        rb = (C.c_int64 * 4)(*self.view.region_bytes)
+        self._r = C.c_void_p()
+        _check(d.xg_regions_alloc(ctx.handle, rb, C.byref(self._r)), "xg_regions_alloc")
+        n = host().xg_fill_runs(sched.handle, G, g, None)
+        runs = (SegRun * max(1, n))()
+        host().xg_fill_runs(sched.handle, G, g, runs)
+        _check(d.xg_fill(self._r, runs, n, sched.d, it, mode), "xg_fill")
+        ns = host().xg_verify_slots(sched.handle, G, g, None)
+        self._slots = (Slot * max(1, ns))()
+        host().xg_verify_slots(sched.handle, G, g, self._slots)
+        self.nslots = ns
+        self.slots = [(s.src, s.seed, s.dst, s.off) for s in self._slots[:ns]]
+        self._p = C.c_void_p()
+        _check(d.xg_plan_load(ctx.handle, self._r, self.view.ptr, C.byref(self._p)), "xg_plan_load")
+        self.nsteps = d.xg_plan_nsteps(self._p)
+
+    def run_timed(self):
+        """barrier-free timed run; returns (step_done[], step_post[], wall)."""
+        n = max(1, self.nsteps)
+        done, post, wall = (C.c_double * n)(), (C.c_double * n)(), C.c_double()
+        _check(_dev.xg_plan_run(self._p, done, post, C.byref(wall)), "xg_plan_run")
+        return list(done)[:self.nsteps], list(post)[:self.nsteps], wall.value
+
+    def enqueue(self):
+        _check(_dev.xg_plan_enqueue(self._p), "xg_plan_enqueue")
+
+    def poison(self):
+        _check(_dev.xg_regions_poison(self._r), "xg_regions_poison")
+
+    def verify(self):
+        ns = max(1, self.nslots)
+        chk, bad, first = (C.c_uint64 * ns)(), (C.c_int64 * ns)(), (C.c_int64 * ns)()
+        _check(_dev.xg_verify(self._r, self._slots, self.nslots, self.sched.d, self.it, self.mode,
+                              chk, bad, first), "xg_verify")
+        return list(chk)[:self.nslots], list(bad)[:self.nslots], list(first)[:self.nslots]
+
+    def read(self, buf, off, length):
+        out = C.create_string_buffer(max(1, length))
+        _check(_dev.xg_regions_read(self._r, buf, off, out, length), "xg_regions_read")
+        return out.raw[:length]
+
+    def close(self):
+        if getattr(self, "_p", None):
+            _check(_dev.xg_plan_free(self._p), "xg_plan_free")
+            self._p = None
+        if getattr(self, "_r", None):
+            _check(_dev.xg_regions_free(self._r), "xg_regions_free")
+            self._r = None

@@ -1,0 +1,46 @@
+import gzip
+import json
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))      # the checker (xg_oracle)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    import __graft_entry__ as G
+    return G.load_package()
+
+
+@pytest.fixture(scope="session")
+def xg(pkg):
+    return pkg.xg
+
+
+def golden_configs():
+    return sorted(n for n in os.listdir(GOLDEN) if os.path.isdir(os.path.join(GOLDEN, n)))
+
+
+def load_golden(name):
+    p = os.path.join(GOLDEN, name)
+    meta = json.load(open(os.path.join(p, "meta.json")))
+    traces = {}
+    for line in gzip.open(os.path.join(p, "trace.txt.gz"), "rt"):
+        head, _, toks = line.rstrip("\n").partition(": ")
+        m, r = head.split()
+        traces[(int(m[1:]), int(r[1:]))] = toks
+    data = {}
+    for direction in ("a2m", "m2a"):
+        rows = gzip.open(os.path.join(p, "data_%s.csv.gz" % direction), "rt").read().split("\n")[1:]
+        data[direction] = {tuple(map(int, r.split(",")[:3])): (int(r.split(",")[3]), int(r.split(",")[4], 16))
+                           for r in rows if r}
+    return meta, traces, data
