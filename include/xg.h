@@ -57,7 +57,8 @@ int xg_rank(const xg_ctx *ctx);
 int xg_nranks(const xg_ctx *ctx);
 int xg_barrier(xg_ctx *ctx);
 int xg_allreduce_max(xg_ctx *ctx, double *vals, int n);       /* in place, MAX over all GPUs */
-int xg_sync(xg_ctx *ctx);
+int xg_sync(xg_ctx *ctx);                                      /* this context's stream */
+int xg_device_sync(xg_ctx *ctx);                               /* whole device (hipDeviceSynchronize) */
 /* device name, CU count, HBM bytes (any pointer may be NULL) */
 int xg_device_info(xg_ctx *ctx, char *name, size_t namelen, int *cus, size_t *hbm_bytes);
 double xg_now(void);                                           /* host seconds (monotonic) */
@@ -100,6 +101,50 @@ int xg_ktime_end(xg_ctx *ctx, double *total_ms, int *launches, int64_t *bytes);
 /* Tuning: chunk bytes per copy workgroup (default 65536), copy kernel
  * variant (0 = default).  Applied to plans loaded afterwards. */
 int xg_set_copy_params(xg_ctx *ctx, int64_t chunk_bytes, int variant);
+
+/* ------------------------------------------------------------------ method operators
+ * The reference's per-method operator API (e.g. all_to_many, mpi_test.c:1748):
+ *   int fn(int rank, int isagg, int procs, int cb_nodes, int data_size,
+ *          int *rank_list, int comm_size, Timer *timer, int iter, int ntimes)
+ * Here one call runs the method for EVERY logical rank this GPU hosts
+ * (xg_block_range), so `timers` holds one Timer per hosted rank (in rank
+ * order) -- the generalisation of "the calling rank's Timer"; rank and isagg
+ * are implied.  Like the reference, the callee owns its buffers (allocated,
+ * fingerprinted with `iter`, timed -k `ntimes` times, freed).  Returns 0, or
+ * an XG_E* code; XG_ESCHED when the schedule cannot complete under MPI
+ * semantics (the reference hangs there) -- err gets the reason. */
+#define XG_ESCHED 5
+
+typedef struct {
+    int verify;              /* 1: check every received byte afterwards (check_buffer, :83-92) */
+    int fingerprint;         /* XG_FP_REFERENCE (MAP_DATA) or XG_FP_STRONG                    */
+    int64_t eager_limit;     /* blocking sends <= this complete locally (XG_MPICH_EAGER_LIMIT)  */
+    int64_t pack_max_seg;    /* p2p staging threshold (xg_devplan_build)                       */
+} xg_run_opts;
+
+void xg_run_opts_default(xg_run_opts *o);
+
+/* bad_slots (may be NULL): receive slots of this GPU that failed verification. */
+int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list,
+                  int comm_size, xg_timer *timers, int iter, int ntimes, const xg_run_opts *opts,
+                  int64_t *bad_slots, char *err, size_t errlen);
+
+/* The twelve operators under the reference's names (mpi_test.c line of the original). */
+#define XG_METHOD_DECL(name)                                                                     \
+    int name(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size, \
+             xg_timer *timers, int iter, int ntimes)
+XG_METHOD_DECL(xg_all_to_many);                 /* m1  :1748 */
+XG_METHOD_DECL(xg_many_to_all);                 /* m2  :1871 */
+XG_METHOD_DECL(xg_all_to_many_balanced);        /* m3  :1422 */
+XG_METHOD_DECL(xg_many_to_all_balanced);        /* m4  :1576 */
+XG_METHOD_DECL(xg_many_to_all_benchmark);       /* m5  :599  */
+XG_METHOD_DECL(xg_all_to_many_sync);            /* m6  :1665 */
+XG_METHOD_DECL(xg_all_to_many_half_sync);       /* m7  :1055 */
+XG_METHOD_DECL(xg_all_to_many_benchmark);       /* m8  :885  */
+XG_METHOD_DECL(xg_all_to_many_pairwise);        /* m9  :510  */
+XG_METHOD_DECL(xg_many_to_all_pairwise);        /* m10 :421  */
+XG_METHOD_DECL(xg_many_to_all_half_sync);       /* m11 :942  */
+XG_METHOD_DECL(xg_all_to_many_half_sync2);      /* m12 :999  */
 
 #ifdef __cplusplus
 }

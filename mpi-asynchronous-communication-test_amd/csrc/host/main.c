@@ -132,84 +132,50 @@ static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
     const int g = xg_rank(ctx), G = xg_nranks(ctx);
     const char *label = xg_method_label(method);
     char err[512];
-    xg_sched *s = xg_sched_build(method, o->P, o->A, o->d, o->c, o->rank_list, o->ntimes, o->eager, err, sizeof err);
-    xg_devplan *dp;
-    xg_regions *reg;
-    xg_plan *plan;
-    xg_segrun *runs;
-    int nruns, nsteps, lo, hi, r;
-    double *done, *post, wall;
-    xg_timer t0 = {0, 0, 0, 0, 0}, tmax = {0, 0, 0, 0, 0};
-    double red[5];
+    int lo, hi, r, rc;
+    int64_t bad = 0;
+    xg_timer *timers, t0 = {0, 0, 0, 0, 0}, tmax = {0, 0, 0, 0, 0};
+    xg_run_opts ro;
+    double red[5], t_wall;
 
-    if (!s) {
+    xg_block_range(o->P, G, g, &lo, &hi);
+    timers = (xg_timer *)calloc(hi - lo + 1, sizeof(xg_timer));
+    xg_run_opts_default(&ro);
+    ro.verify = o->verify; ro.fingerprint = o->fp_mode; ro.eager_limit = o->eager; ro.pack_max_seg = o->pack_max;
+    t_wall = xg_now();
+    rc = xg_run_method(ctx, method, o->P, o->A, o->d, o->rank_list, o->c, timers, iter, o->ntimes, &ro, &bad,
+                       err, sizeof err);
+    t_wall = xg_now() - t_wall;
+    if (rc == XG_ESCHED) {          /* every process computes the same schedule */
         if (g == 0) fprintf(stderr, "| %s: %s\n", label, err);
+        free(timers);
         return;
     }
-    dp = xg_devplan_build(s, G, g, o->pack_max);
-    XGCALL(xg_regions_alloc(ctx, dp->region_bytes, &reg));
-    /* prepare_*_data: allocate + fill (untimed) */
-    nruns = xg_fill_runs(s, G, g, NULL);
-    runs = (xg_segrun *)malloc(sizeof(xg_segrun) * (nruns + 1));
-    xg_fill_runs(s, G, g, runs);
-    XGCALL(xg_fill(reg, runs, nruns, o->d, iter, o->fp_mode));
-    free(runs);
-    XGCALL(xg_plan_load(ctx, reg, dp, &plan));
-    nsteps = xg_sched_nsteps(s);
-    done = (double *)calloc(nsteps + 1, sizeof(double));
-    post = (double *)calloc(nsteps + 1, sizeof(double));
-    /* MPI_Barrier; total_start = MPI_Wtime(); ... timed loop ... */
-    XGCALL(xg_barrier(ctx));
-    XGCALL(xg_plan_run(plan, done, post, &wall));
-    /* per logical rank timers, then MPI_Reduce(MAX) (:2184) */
-    xg_block_range(o->P, G, g, &lo, &hi);
+    if (rc) DIE("%s failed: %s", label, err);
+    /* MPI_Reduce(&timer1, &max_timer1, 5, MPI_DOUBLE, MPI_MAX, 0, ...)  (:2184) */
     for (r = lo; r < hi; ++r) {
-        xg_timer t;
-        xg_sched_rank_timer(s, r, done, post, &t);
-        if (r == 0) t0 = t;
-        if (t.post_request_time > tmax.post_request_time) tmax.post_request_time = t.post_request_time;
-        if (t.send_wait_all_time > tmax.send_wait_all_time) tmax.send_wait_all_time = t.send_wait_all_time;
-        if (t.recv_wait_all_time > tmax.recv_wait_all_time) tmax.recv_wait_all_time = t.recv_wait_all_time;
-        if (t.total_time > tmax.total_time) tmax.total_time = t.total_time;
+        const xg_timer *t = &timers[r - lo];
+        if (r == 0) t0 = *t;
+        if (t->post_request_time > tmax.post_request_time) tmax.post_request_time = t->post_request_time;
+        if (t->send_wait_all_time > tmax.send_wait_all_time) tmax.send_wait_all_time = t->send_wait_all_time;
+        if (t->recv_wait_all_time > tmax.recv_wait_all_time) tmax.recv_wait_all_time = t->recv_wait_all_time;
+        if (t->total_time > tmax.total_time) tmax.total_time = t->total_time;
     }
     red[0] = tmax.post_request_time; red[1] = tmax.send_wait_all_time; red[2] = tmax.recv_wait_all_time;
-    red[3] = 0; red[4] = tmax.total_time;
+    red[3] = (double)bad; red[4] = tmax.total_time;
     XGCALL(xg_allreduce_max(ctx, red, 5));
     tmax.post_request_time = red[0]; tmax.send_wait_all_time = red[1]; tmax.recv_wait_all_time = red[2];
     tmax.barrier_time = 0; tmax.total_time = red[4];
-    if (g == 0)
+    if (g == 0) {
         xg_summarize_results(o->P, o->A, o->d, o->c, o->ntimes, o->type, "results.csv", label, t0, tmax);
-    if (o->verify) {
-        int ns = xg_verify_slots(s, G, g, NULL), i;
-        xg_slot *sl = (xg_slot *)malloc(sizeof(xg_slot) * (ns + 1));
-        int64_t *bad = (int64_t *)calloc(ns + 1, sizeof(int64_t)), *first = (int64_t *)calloc(ns + 1, sizeof(int64_t));
-        uint64_t *chk = (uint64_t *)calloc(ns + 1, sizeof(uint64_t)), cc = 0;
-        double v[2] = {0, 0};
-        xg_verify_slots(s, G, g, sl);
-        XGCALL(xg_verify(reg, sl, ns, o->d, iter, o->fp_mode, chk, bad, first));
-        for (i = 0; i < ns; ++i) {
-            if (bad[i]) {
-                if (v[0] == 0)
-                    fprintf(stderr, "rank %d, message is wrong from rank %d (first bad byte %lld)\n", sl[i].dst,
-                            sl[i].src, (long long)first[i]);
-                v[0] += 1;
-            }
-            cc += chk[i];
-        }
-        v[1] = (double)(cc >> 11);
-        XGCALL(xg_allreduce_max(ctx, v, 1));
-        if (g == 0) {
+        if (o->verify) {
             const double bytes = (double)o->P * o->A * o->d * o->ntimes;
-            printf("| %s verify = %s (%d slots on gpu 0, bad slots max over gpus = %.0f), aggregate = %.3f GB/s\n",
-                   label, v[0] == 0 ? "OK" : "FAILED", ns, v[0], tmax.total_time > 0 ? bytes / tmax.total_time / 1e9 : 0.0);
+            printf("| %s verify = %s (bad receive slots, max over gpus = %.0f), aggregate = %.3f GB/s\n", label,
+                   red[3] == 0 ? "OK" : "FAILED", red[3], tmax.total_time > 0 ? bytes / tmax.total_time / 1e9 : 0.0);
         }
-        free(sl); free(bad); free(first); free(chk);
     }
-    free(done); free(post);
-    XGCALL(xg_plan_free(plan));
-    XGCALL(xg_regions_free(reg));
-    xg_devplan_free(dp);
-    xg_sched_free(s);
+    (void)t_wall;
+    free(timers);
 }
 
 int main(int argc, char **argv)

@@ -1,0 +1,105 @@
+/*
+ * methods.c -- the reference's per-method operators on the MI355X runtime.
+ * One call = prepare_*_data (regions + fingerprint, untimed) -> MPI_Barrier ->
+ * the timed exchange -> Timer of every hosted logical rank -> clean_* ;
+ * plus optional verification (the reference's commented-out check_buffer).
+ * Compiled into libxg.so; links libxghost.so for schedules.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "xg.h"
+#include "xg_sched.h"
+
+void xg_run_opts_default(xg_run_opts *o)
+{
+    o->verify = 0;
+    o->fingerprint = XG_FP_REFERENCE;
+    o->eager_limit = XG_MPICH_EAGER_LIMIT;
+    o->pack_max_seg = 1 << 20;
+}
+
+#define TRY(x) do { rc = (x); if (rc) goto out; } while (0)
+
+int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list,
+                  int comm_size, xg_timer *timers, int iter, int ntimes, const xg_run_opts *opts,
+                  int64_t *bad_slots, char *err, size_t errlen)
+{
+    xg_run_opts dflt;
+    const int g = xg_rank(ctx), G = xg_nranks(ctx);
+    char ebuf[512];
+    xg_sched *s;
+    xg_devplan *dp = NULL;
+    xg_regions *reg = NULL;
+    xg_plan *plan = NULL;
+    xg_segrun *runs = NULL;
+    xg_slot *slots = NULL;
+    int64_t *bad = NULL;
+    double *done = NULL, *post = NULL, wall = 0;
+    int rc = 0, nruns, nsteps, lo, hi, r, i;
+    if (!opts) { xg_run_opts_default(&dflt); opts = &dflt; }
+    if (!err) { err = ebuf; errlen = sizeof ebuf; }
+    if (bad_slots) *bad_slots = 0;
+    s = xg_sched_build(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, opts->eager_limit,
+                       err, errlen);
+    if (!s) return XG_ESCHED;
+    dp = xg_devplan_build(s, G, g, opts->pack_max_seg);
+    TRY(xg_regions_alloc(ctx, dp->region_bytes, &reg));
+    nruns = xg_fill_runs(s, G, g, NULL);
+    runs = (xg_segrun *)malloc(sizeof(xg_segrun) * (nruns + 1));
+    xg_fill_runs(s, G, g, runs);
+    TRY(xg_fill(reg, runs, nruns, data_size, iter, opts->fingerprint));
+    TRY(xg_plan_load(ctx, reg, dp, &plan));
+    nsteps = xg_sched_nsteps(s);
+    done = (double *)calloc(nsteps + 1, sizeof(double));
+    post = (double *)calloc(nsteps + 1, sizeof(double));
+    TRY(xg_barrier(ctx));                                   /* MPI_Barrier before total_start */
+    TRY(xg_plan_run(plan, done, post, &wall));
+    xg_block_range(procs, G, g, &lo, &hi);
+    if (timers)
+        for (r = lo; r < hi; ++r) xg_sched_rank_timer(s, r, done, post, &timers[r - lo]);
+    if (opts->verify) {
+        int ns = xg_verify_slots(s, G, g, NULL);
+        slots = (xg_slot *)malloc(sizeof(xg_slot) * (ns + 1));
+        bad = (int64_t *)calloc(ns + 1, sizeof(int64_t));
+        xg_verify_slots(s, G, g, slots);
+        TRY(xg_verify(reg, slots, ns, data_size, iter, opts->fingerprint, NULL, bad, NULL));
+        for (i = 0; i < ns; ++i)
+            if (bad[i]) {
+                if (bad_slots && *bad_slots == 0)
+                    fprintf(stderr, "rank %d, message is wrong from rank %d\n", slots[i].dst, slots[i].src);
+                if (bad_slots) ++*bad_slots;
+            }
+    }
+out:
+    if (rc && err[0] == 0) snprintf(err, errlen, "device error %d (see stderr)", rc);
+    free(runs); free(slots); free(bad); free(done); free(post);
+    if (plan) xg_plan_free(plan);
+    if (reg) xg_regions_free(reg);
+    xg_devplan_free(dp);
+    xg_sched_free(s);
+    return rc;
+}
+
+#define XG_METHOD_DEF(name, m)                                                                    \
+    XG_METHOD_DECL(name)                                                                          \
+    {                                                                                             \
+        char e[512];                                                                              \
+        int rc = xg_run_method(ctx, m, procs, cb_nodes, data_size, rank_list, comm_size, timers,  \
+                               iter, ntimes, NULL, NULL, e, sizeof e);                            \
+        if (rc == XG_ESCHED) fprintf(stderr, "%s: %s\n", #name, e);                               \
+        return rc;                                                                                \
+    }
+XG_METHOD_DEF(xg_all_to_many, 1)
+XG_METHOD_DEF(xg_many_to_all, 2)
+XG_METHOD_DEF(xg_all_to_many_balanced, 3)
+XG_METHOD_DEF(xg_many_to_all_balanced, 4)
+XG_METHOD_DEF(xg_many_to_all_benchmark, 5)
+XG_METHOD_DEF(xg_all_to_many_sync, 6)
+XG_METHOD_DEF(xg_all_to_many_half_sync, 7)
+XG_METHOD_DEF(xg_all_to_many_benchmark, 8)
+XG_METHOD_DEF(xg_all_to_many_pairwise, 9)
+XG_METHOD_DEF(xg_many_to_all_pairwise, 10)
+XG_METHOD_DEF(xg_many_to_all_half_sync, 11)
+XG_METHOD_DEF(xg_all_to_many_half_sync2, 12)

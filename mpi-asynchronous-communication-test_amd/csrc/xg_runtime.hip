@@ -149,6 +149,13 @@ extern "C" int xg_sync(xg_ctx *c)
     return XG_OK;
 }
 
+extern "C" int xg_device_sync(xg_ctx *c)
+{
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    return XG_OK;
+}
+
 extern "C" int xg_allreduce_max(xg_ctx *c, double *vals, int n)
 {
     if (n < 0 || n > 64) return XG_EARG;

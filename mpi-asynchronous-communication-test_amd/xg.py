@@ -55,6 +55,16 @@ class DevPlan(C.Structure):
                 ("remote_recv_bytes", C.c_int64)]
 
 
+class SegRun(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("seed0", C.c_int32), ("off", C.c_int64), ("nsegs", C.c_int32),
+                ("pad", C.c_int32)]
+
+
+class Slot(C.Structure):
+    _fields_ = [("src", C.c_int32), ("seed", C.c_int32), ("dst", C.c_int32), ("pad", C.c_int32),
+                ("off", C.c_int64)]
+
+
 A2M, M2A = 0, 1
 BUF_SEND, BUF_RECV, BUF_STAGE_SEND, BUF_STAGE_RECV = 0, 1, 2, 3
 MPICH_EAGER_LIMIT = 65424
@@ -101,6 +111,9 @@ def host():
         h.xg_devplan_build.restype = C.POINTER(DevPlan)
         h.xg_devplan_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64]
         h.xg_devplan_free.argtypes = [C.POINTER(DevPlan)]
+        h.xg_fill_runs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(SegRun)]
+        h.xg_verify_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(Slot)]
+        h.xg_summarize_results.argtypes = [C.c_int] * 6 + [C.c_char_p, C.c_char_p, Timer, Timer]
         _host = h
     return _host
 
@@ -182,6 +195,18 @@ class Schedule:
     def devplan(self, ngpus, g, pack_max_seg=1 << 20):
         return DevicePlanView(self, ngpus, g, pack_max_seg)
 
+    def fill_runs(self, ngpus, g):
+        n = host().xg_fill_runs(self._h, ngpus, g, None)
+        runs = (SegRun * max(1, n))()
+        host().xg_fill_runs(self._h, ngpus, g, runs)
+        return [(r.rank, r.seed0, r.off, r.nsegs) for r in runs[:n]]
+
+    def verify_slots(self, ngpus, g):
+        n = host().xg_verify_slots(self._h, ngpus, g, None)
+        sl = (Slot * max(1, n))()
+        host().xg_verify_slots(self._h, ngpus, g, sl)
+        return [(x.src, x.seed, x.dst, x.off) for x in sl[:n]]
+
 
 class DevicePlanView:
     """Python view of xg_devplan (host memory), used by the CPU plan tests."""
@@ -211,16 +236,6 @@ class DevicePlanView:
 
 
 # --------------------------------------------------------------------------- device (libxg.so)
-class SegRun(C.Structure):
-    _fields_ = [("rank", C.c_int32), ("seed0", C.c_int32), ("off", C.c_int64), ("nsegs", C.c_int32),
-                ("pad", C.c_int32)]
-
-
-class Slot(C.Structure):
-    _fields_ = [("src", C.c_int32), ("seed", C.c_int32), ("dst", C.c_int32), ("pad", C.c_int32),
-                ("off", C.c_int64)]
-
-
 def device():
     """libxg.so -- the HIP/RCCL half.  Loading it does not touch the GPU."""
     global _dev
@@ -233,6 +248,7 @@ def device():
         d.xg_finalize.argtypes = [vp]
         d.xg_barrier.argtypes = [vp]
         d.xg_sync.argtypes = [vp]
+        d.xg_device_sync.argtypes = [vp]
         d.xg_allreduce_max.argtypes = [vp, C.POINTER(C.c_double), ip]
         d.xg_device_info.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(ip), C.POINTER(C.c_size_t)]
         d.xg_now.restype = C.c_double
@@ -253,9 +269,6 @@ def device():
         d.xg_ktime_begin.argtypes = [vp, ip]
         d.xg_ktime_end.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(ip), C.POINTER(i64)]
         d.xg_set_copy_params.argtypes = [vp, i64, ip]
-        h = host()
-        h.xg_fill_runs.argtypes = [vp, ip, ip, C.POINTER(SegRun)]
-        h.xg_verify_slots.argtypes = [vp, ip, ip, C.POINTER(Slot)]
         _dev = d
     return _dev
 
@@ -291,6 +304,9 @@ class Context:
 
     def sync(self):
         _check(_dev.xg_sync(self._c), "xg_sync")
+
+    def device_sync(self):
+        _check(_dev.xg_device_sync(self._c), "xg_device_sync")
 
     def allreduce_max(self, vals):
         arr = (C.c_double * len(vals))(*vals)

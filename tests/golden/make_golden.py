@@ -14,6 +14,7 @@ reduces the per-rank capture files to small fixtures:
                          (iter 0).  Tokens: B barrier, s<peer>:<cnt> send post,
                          r<peer>:<cnt> recv post, w<idx list> completion point, A alltoallw.
   <cfg>/report_m<N>.txt  the reference's stdout for -m N with every number masked '#'
+  usage.txt              the reference's `-h` text (stderr), argv0 replaced by {argv0}
 
 Each method's captured data is checked against the direction table while
 writing (all methods of one direction must deliver identical bytes); the
@@ -127,6 +128,11 @@ def run_one(P, args, method, workdir):
 
 def main(selected=None):
     subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True, capture_output=True)
+    # usage text (mpi_test.c:41-69), printed by `./test -h`; argv0 normalised to {argv0}
+    ref = os.path.join(REPO, "oracle", "_ref", "test")
+    u = subprocess.run([MPIEXEC, "-n", "1", ref, "-h"], capture_output=True, text=True, timeout=60)
+    with open(os.path.join(HERE, "usage.txt"), "w") as fp:
+        fp.write(u.stderr.replace(ref, "{argv0}"))
     work = tempfile.mkdtemp(prefix="xg_golden_")
     try:
         for name, (P, args) in CONFIGS.items():

@@ -1,0 +1,61 @@
+"""CPU executor of xg_devplan (TEST DOUBLE, never part of the product).
+
+Runs GPU g's plan on numpy regions exactly as libxg does on HBM: per step,
+pre copies (local gather/scatter + packs), the grouped p2p exchange (matched
+per ordered GPU pair in issue order, as RCCL does), then post copies (unpacks).
+"""
+import numpy as np
+
+import xg_oracle as O
+
+
+def make_regions(s, view, G, g, it, mode):
+    d = s.d
+    reg = [np.zeros(max(0, b), np.uint8) for b in view.region_bytes]
+    reg[1][:] = 0xA5
+    for rank, seed0, off, nsegs in s.fill_runs(G, g):
+        for k in range(nsegs):
+            reg[0][off + k * d: off + (k + 1) * d] = O.fingerprint(mode, rank, seed0 + k, it, d)
+    return reg
+
+
+def copies(reg, lst):
+    for sb, so, db, do, ln in lst:
+        assert 0 <= so and so + ln <= reg[sb].size and 0 <= do and do + ln <= reg[db].size
+        reg[db][do:do + ln] = reg[sb][so:so + ln]
+
+
+def step_parts(view, st):
+    pb, pc, qb, qc, ob, oc = view.steps[st]
+    return view.copies[pb:pb + pc], view.p2p[qb:qb + qc], view.copies[ob:ob + oc]
+
+
+def simulate(s, G, it=0, mode=0, pack=1 << 20):
+    views = [s.devplan(G, g, pack) for g in range(G)]
+    regs = [make_regions(s, v, G, g, it, mode) for g, v in enumerate(views)]
+    for st in range(views[0].nsteps):
+        parts = [step_parts(v, st) for v in views]
+        for g in range(G):
+            copies(regs[g], parts[g][0])
+        for g in range(G):
+            for p in range(G):
+                if p == g:
+                    continue
+                sends = [o for o in parts[g][1] if o[0] == p and o[1]]
+                recvs = [o for o in parts[p][1] if o[0] == g and not o[1]]
+                assert len(sends) == len(recvs), (st, g, p)
+                for (_, _, sb, so, sl), (_, _, rb, ro, rl) in zip(sends, recvs):
+                    assert sl == rl, (st, g, p)
+                    regs[p][rb][ro:ro + rl] = regs[g][sb][so:so + sl]
+        for g in range(G):
+            copies(regs[g], parts[g][2])
+    return views, regs
+
+
+def check_recv(s, G, regs, it=0, mode=0):
+    exp = O.expected_recv(s.method, s.P, s.A, s.d, s.rank_list, it, mode)
+    for r, buf in exp.items():
+        g = s.gpu_of(G, r)
+        off = s.recv_offset(G, r)
+        got = regs[g][1][off: off + buf.size]
+        assert (got == buf).all(), (s.method, G, r)

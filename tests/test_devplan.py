@@ -1,0 +1,64 @@
+"""Multi-GPU device plans (libxghost xg_devplan_build), executed on the CPU.
+
+Block mapping of logical ranks onto G GPUs, local copies vs grouped p2p,
+pack/unpack staging vs one op per segment: every received byte must equal
+the oracle's closed form, for every method, G in 1..8 and both p2p modes.
+"""
+import pytest
+
+import xg_oracle as O
+from plan_exec import check_recv, simulate
+
+CASES = [  # P, A, d, c, ntimes, type, proc_node
+    (32, 14, 40, 3, 2, 1, 1),      # README shape (reduced d), throttled
+    (20, 6, 24, 7, 3, 1, 1),
+    (24, 7, 16, 1, 1, 3, 4),       # unsorted aggregator list
+    (16, 16, 8, 5, 1, 0, 1),       # every rank an aggregator
+    (13, 4, 33, 200000000, 2, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("G", [1, 2, 3, 4, 8])
+def test_plans_deliver_every_byte(xg, case, G):
+    P, A, d, c, k, t, pn = case
+    if G > P:
+        pytest.skip("more GPUs than ranks")
+    rl = xg.aggregator_list(P, A, pn, t)
+    for m in range(1, 13):
+        s = xg.Schedule(m, P, A, d, c, rl, ntimes=k)
+        for pack in (0, 1 << 20):
+            views, regs = simulate(s, G, it=1, mode=1, pack=pack)
+            check_recv(s, G, regs, it=1, mode=1)
+
+
+def test_pack_decision_and_volume(xg):
+    """Packing: >= 2 segments to a peer with mean < pack_max_seg -> one RCCL op per peer."""
+    P, A, d = 32, 14, 1024
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(1, P, A, d, 200000000, rl)
+    G = 8
+    tot_local = tot_remote = 0
+    for g in range(G):
+        packed = s.devplan(G, g, pack_max_seg=1 << 20)
+        direct = s.devplan(G, g, pack_max_seg=0)
+        peers = {o[0] for o in packed.p2p}
+        # one send and one recv per peer in the single step when packed
+        assert len(packed.p2p) == 2 * len(peers)
+        assert len(direct.p2p) > len(packed.p2p)
+        assert packed.remote_send_bytes == direct.remote_send_bytes
+        assert packed.region_bytes[2] == packed.remote_send_bytes
+        tot_local += packed.local_bytes
+        tot_remote += packed.remote_send_bytes
+    assert tot_local + tot_remote == P * A * d
+
+
+def test_region_sizes(xg):
+    P, A, d = 32, 14, 4096
+    rl = xg.aggregator_list(P, A)
+    for m in (1, 2):
+        s = xg.Schedule(m, P, A, d, 200000000, rl)
+        for G in (1, 2, 4, 8):
+            tot_send = sum(s.region_bytes(G, g, 0) for g in range(G))
+            tot_recv = sum(s.region_bytes(G, g, 1) for g in range(G))
+            assert tot_send == tot_recv == P * A * d

@@ -1,0 +1,102 @@
+"""libxghost (the product's C host side) against the reference traces and the oracle."""
+import subprocess
+import os
+
+import pytest
+
+import xg_oracle as O
+from conftest import REPO, GOLDEN, golden_configs, load_golden
+
+CONFIGS = golden_configs()
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_traces_match_reference(xg, cfg):
+    meta, traces, _ = load_golden(cfg)
+    rl = xg.aggregator_list(meta["P"], meta["A"], meta["proc_node"], meta["type"])
+    assert rl == meta["aggregators"]
+    for m in range(1, 13):
+        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, ntimes=meta["ntimes"])
+        for r in range(meta["P"]):
+            assert s.trace(r) == traces[(m, r)], (cfg, m, r)
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_steps_match_oracle(xg, cfg):
+    meta, _, _ = load_golden(cfg)
+    rl = meta["aggregators"]
+    for m in range(1, 13):
+        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, ntimes=meta["ntimes"])
+        progs = O.programs(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, meta["ntimes"])
+        om = O.match(progs)
+        ost, ons = O.asap_steps(progs, om)
+        mine = sorted((a, b, c, d, n, st) for a, b, c, d, n, st, fl in s.messages() if not fl & 1)
+        ref = sorted((a, b, c, d, n, st) for (a, b, c, d, n, _sp, _rp), st in zip(om, ost))
+        assert mine == ref, (cfg, m)
+        assert s.nsteps >= ons
+
+
+def test_deadlock_is_reported_not_hung(xg):
+    rl = xg.aggregator_list(32, 14)
+    xg.Schedule(6, 32, 14, 65424, 3, rl)
+    with pytest.raises(xg.XGError, match="deadlocks"):
+        xg.Schedule(6, 32, 14, 65425, 3, rl)
+
+
+@pytest.mark.parametrize("t", [0, 1, 2, 3])
+def test_aggregator_types(xg, t):
+    for P, A, p in [(32, 14, 1), (24, 7, 4), (256, 64, 8), (12, 5, 3), (7, 7, 2)]:
+        assert xg.aggregator_list(P, A, p, t) == O.aggregator_list(P, A, p, t)
+
+
+def test_labels(xg):
+    for m, lab in O.LABELS.items():
+        assert xg.method_label(m) == lab
+    assert xg.method_label(13) is None
+
+
+def test_timer_semantics(xg):
+    """Logical clock: each wait advances a rank's clock to the completion time of the
+    step it waits on; the reference's MPI_Wtime brackets become clock intervals."""
+    rl = xg.aggregator_list(8, 3)
+    # m1 unordered: one step; every rank: post bracket, then recv bracket over the waitall
+    s = xg.Schedule(1, 8, 3, 64, 1000, rl)
+    assert s.nsteps == 1
+    t = s.rank_timer(0, [0.005], [0.001])
+    assert t.recv_wait_all_time == pytest.approx(0.005) and t.total_time == pytest.approx(0.005)
+    assert t.send_wait_all_time == 0
+    # m1 throttled (c=2 -> 4 receive phases): aggregator recv_wait = last phase end;
+    # a non-aggregator only waits for its sends (send_wait)
+    s = xg.Schedule(1, 8, 3, 64, 2, rl)
+    done = [0.001 * (i + 1) for i in range(s.nsteps)]
+    t_agg = s.rank_timer(0, done)
+    assert t_agg.recv_wait_all_time == pytest.approx(done[-1])
+    t_non = s.rank_timer(1, done)
+    assert t_non.recv_wait_all_time == 0 and t_non.send_wait_all_time > 0
+    assert t_non.total_time <= t_agg.total_time + 1e-12
+
+
+def test_summarize_results_format(xg, tmp_path, capfd):
+    """xg_summarize_results prints exactly the reference's report lines (masked golden)."""
+    import re
+    T = xg.Timer(0.1, 0.2, 0.3, 0.0, 0.4)
+    csvp = str(tmp_path / "results.csv")
+    import ctypes
+    xg.host().xg_summarize_results(32, 14, 2048, 3, 2, 1, csvp.encode(), b"All to many", T, T)
+    ctypes.CDLL(None).fflush(None)
+    out = capfd.readouterr().out
+    golden = open(os.path.join(GOLDEN, "readme_p32_a14", "report_m1.txt")).read().splitlines()
+    # golden = header (2 lines) + per-iteration blocks; one method block = 9 lines
+    block = golden[2:11]
+    assert re.sub(r"\d+(\.\d+)?", "#", out).splitlines() == block
+    rows = open(csvp).read().splitlines()
+    assert rows[0].startswith("Method,# of processes,# of aggregators,data size,max comm,ntimes,aggregator type")
+    assert rows[1].startswith("All to many,32,14,2048,3,2,1,0.100000,")
+
+
+def test_cli_usage_matches_reference(pkg):
+    exe = os.path.join(os.path.dirname(pkg.__file__), "bin", "test")
+    out = subprocess.run([exe, "-h"], capture_output=True, text=True, timeout=30)
+    assert out.returncode == 0
+    ref = open(os.path.join(GOLDEN, "usage.txt")).read().replace("{argv0}", exe)
+    assert out.stderr == ref

@@ -1,0 +1,83 @@
+"""world_size-2 run of the multi-GPU exchange on CPU: each process executes its
+GPU's device plan on numpy regions and moves every p2p op with torch.distributed
+(gloo), in the same per-peer issue order RCCL matches on.  Same bytes as the oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, results):
+    import sys
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import __graft_entry__ as G
+    import xg_oracle as O
+    from plan_exec import copies, make_regions, step_parts
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    xg = G.load_package().xg
+    ok = True
+    try:
+        for (P, A, d, c, k, m) in [(12, 5, 64, 3, 2, 1), (12, 5, 64, 3, 2, 2), (16, 5, 100, 4, 1, 4),
+                                   (16, 4, 32, 200000000, 1, 5), (12, 5, 48, 2, 1, 6), (16, 6, 40, 3, 1, 9),
+                                   (12, 5, 16, 2, 2, 11), (16, 5, 56, 3, 1, 12)]:
+            rl = xg.aggregator_list(P, A)
+            s = xg.Schedule(m, P, A, d, c, rl, ntimes=k)
+            for pack in (0, 1 << 20):
+                v = s.devplan(world, rank, pack)
+                reg = make_regions(s, v, world, rank, 2, 1)
+                seq = {}
+                for st in range(v.nsteps):
+                    pre, p2p, post = step_parts(v, st)
+                    copies(reg, pre)
+                    reqs, bufs = [], []
+                    for peer, is_send, buf, off, ln in p2p:
+                        key = (peer, is_send)
+                        tag = seq.get(key, 0)
+                        seq[key] = tag + 1
+                        if is_send:
+                            t = torch.from_numpy(reg[buf][off:off + ln].copy())
+                            reqs.append(dist.isend(t, dst=peer, tag=tag))
+                        else:
+                            t = torch.empty(ln, dtype=torch.uint8)
+                            reqs.append(dist.irecv(t, src=peer, tag=tag))
+                            bufs.append((t, buf, off, ln))
+                    for q in reqs:
+                        q.wait()
+                    for t, buf, off, ln in bufs:
+                        reg[buf][off:off + ln] = t.numpy()
+                    copies(reg, post)
+                exp = O.expected_recv(m, P, A, d, rl, 2, 1)
+                lo, hi = s.block_range(world, rank)
+                for r in range(lo, hi):
+                    off = s.recv_offset(world, r)
+                    if off < 0:
+                        continue
+                    got = reg[1][off: off + exp[r].size]
+                    ok &= bool((got == exp[r]).all())
+        dist.barrier()
+    finally:
+        results[rank] = ok
+        dist.destroy_process_group()
+
+
+def test_two_process_exchange():
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), results), nprocs=2, join=True)
+    assert results[0] and results[1]
