@@ -155,12 +155,13 @@ def main():
     uid, rdzv = (None, None)
     if world > 1:
         uid, rdzv = rendezvous_uid(xg, rank, world)
-    ctx = xg.Context(rank=rank, nranks=world, device=local, uid=uid)
+    dev = int(os.environ.get("XG_DEVICE", local))   # XG_DEVICE: test hook (several ranks on one GPU)
+    ctx = xg.Context(rank=rank, nranks=world, device=dev, uid=uid)
     ctx.barrier()
     if rdzv:
         os.unlink(rdzv)
     if a.copy_variant >= 0 or a.chunk:
-        ctx.set_copy_params(a.chunk, max(a.copy_variant, 0))
+        ctx.set_copy_params(a.chunk, a.copy_variant)
     arch, cus, hbm = ctx.info()
 
     rl = xg.aggregator_list(a.procs, a.aggs)
@@ -172,7 +173,7 @@ def main():
         ctx.barrier()
         done, post, _wall = r.run_timed()
         lo, hi = s.block_range(world, rank)
-        tmax = max(s.rank_timer(q, done, post).total_time for q in range(lo, hi)) if hi > lo else 0.0
+        tmax = max(s.rank_timer(q, done, post, world).total_time for q in range(lo, hi)) if hi > lo else 0.0
         _chk, bad, _first = r.verify()
         nbad = float(sum(1 for b in bad if b))
         tmax, nbad = ctx.allreduce_max([tmax, nbad])
@@ -204,6 +205,23 @@ def main():
 
     seg_bytes = float(a.procs) * a.aggs * a.size * len(methods) * a.steps
     value = seg_bytes / elapsed / 1e9
+
+    # N > 1: cross-GPU (xGMI) bytes of the timed region vs the measured RCCL all-pairs ceiling
+    xgmi = None
+    if world > 1:
+        cross_step = 0      # every rank derives every GPU's plan (deterministic, cheap)
+        for r in runs:
+            for g in range(world):
+                cross_step += r.sched.devplan(world, g, a.pack_max_seg).remote_send_bytes
+        per_pair = max(65536, (cross_step // max(1, len(methods) * world * (world - 1)) + 4095) & ~4095)
+        ceil_gbps, _ = ctx.p2p_bench(per_pair, mode=0, reps=20)
+        ceil_min = -ctx.allreduce_max([-ceil_gbps])[0]          # slowest GPU's egress
+        achieved = cross_step * a.steps / elapsed / 1e9
+        xgmi = {"achieved": round(achieved, 1), "peak": round(ceil_min * world, 1), "unit": "GB/s",
+                "frac": round(achieved / (ceil_min * world), 4) if ceil_min > 0 else None,
+                "cross_gpu_bytes_per_step": int(cross_step),
+                "peak_source": "measured: RCCL all-pairs send/recv, %d B per GPU pair, slowest GPU egress x %d "
+                               "(xg_p2p_bench mode 0)" % (per_pair, world)}
     if rank != 0:
         ctx.close()
         return
@@ -236,6 +254,7 @@ def main():
                    "parallelism": "block-mapped logical ranks; intra-GPU copy_kernel + grouped RCCL p2p"},
         "max_total_time_s": max_total,
         "roofline": roof,
+        "xgmi": xgmi,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out))

@@ -98,8 +98,20 @@ int xg_plan_enqueue(xg_plan *p);
 int xg_ktime_begin(xg_ctx *ctx, int max_launches);
 int xg_ktime_end(xg_ctx *ctx, double *total_ms, int *launches, int64_t *bytes);
 
-/* Tuning: chunk bytes per copy workgroup (default 65536), copy kernel
- * variant (0 = default).  Applied to plans loaded afterwards. */
+/* HBM copy ceiling microbenchmark on `bytes` contiguous bytes: kind 0 grid-stride
+ * float4 copy, 1 copy_kernel over 64 KiB pieces, 2 span_copy_kernel; *gbps counts
+ * read + write bytes. */
+int xg_copy_ceiling(xg_ctx *ctx, int64_t bytes, int kind, int reps, double *gbps);
+
+/* RCCL point-to-point ceiling (rccl-tests sendrecv analogue; GPU version of
+ * pt2pt_test, mpi_sendrecv_test.c:15-74).  mode 0: all pairs, 1: ring,
+ * 2: one direction rank 1 -> rank 0.  *gbps = bytes sent by this rank per
+ * second (mode 2: bytes moved 1 -> 0), *sec = seconds per repetition. */
+int xg_p2p_bench(xg_ctx *ctx, int64_t bytes, int mode, int reps, double *gbps, double *sec);
+
+/* Tuning: bytes per copy workgroup (default 32768) and copy kernel variant
+ * (default 5 = copy_kernel_g<4>; variant < 0 keeps the current one; see
+ * DESIGN.md and profiles/r01_copy_ab.txt).  Applied to plans loaded afterwards. */
 int xg_set_copy_params(xg_ctx *ctx, int64_t chunk_bytes, int variant);
 
 /* ------------------------------------------------------------------ method operators

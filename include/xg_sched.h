@@ -91,14 +91,16 @@ int xg_sched_procs(const xg_sched *s);
  * buflen-1) or the needed length if buf is NULL. */
 size_t xg_sched_trace(const xg_sched *s, int rank, char *buf, size_t buflen);
 
-/* Per-rank timer from device step timestamps:
+/* Per-rank timer from device step timestamps (ranks block-mapped on ngpus):
  *   step_done[s]  seconds from the timed-region start until step s completed
  *                 on the GPU that hosts `rank`;
- *   step_post[s]  host seconds spent enqueuing step s on that GPU (may be NULL).
+ *   step_post[s]  host seconds spent enqueuing step s on that GPU (may be NULL);
+ *                 it is shared out over the requests that GPU's ranks post in s.
  * Each reference timer bracket (MPI_Wtime pairs) becomes an interval of the
  * rank's logical clock, which advances at completion points to the step
- * completion time of the awaited messages. */
-int xg_sched_rank_timer(const xg_sched *s, int rank, const double *step_done,
+ * completion time of the awaited messages; a post bracket adds the share of
+ * enqueue time of the requests it posts. */
+int xg_sched_rank_timer(xg_sched *s, int ngpus, int rank, const double *step_done,
                         const double *step_post, xg_timer *out);
 
 /* ---------------------------------------------------------------- device plan

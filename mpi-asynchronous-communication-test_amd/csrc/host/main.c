@@ -28,6 +28,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include "rdzv.h"
 #include "xg.h"
 #include "xg_sched.h"
 
@@ -59,63 +60,6 @@ static void usage(const char *argv0)   /* mpi_test.c:41-69 */
     fprintf(stderr, help, argv0);
 }
 
-static int env_int(const char *a, const char *b, int dflt)
-{
-    const char *v = getenv(a);
-    if (!v && b) v = getenv(b);
-    return v ? atoi(v) : dflt;
-}
-
-static double now_s(void)
-{
-    struct timespec ts;
-    clock_gettime(CLOCK_REALTIME, &ts);
-    return ts.tv_sec + ts.tv_nsec * 1e-9;
-}
-
-/* RCCL unique-id hand-over through a file (single node). */
-static int rendezvous(int rank, int nranks, unsigned char uid[XG_UNIQUE_ID_BYTES], char *path, size_t pathlen)
-{
-    const char *dir = getenv("XG_RDZV_DIR");
-    const char *key = getenv("XG_RDZV_KEY");
-    char kbuf[128];
-    double t_start = now_s();
-    if (!dir) dir = "/tmp";
-    if (!key) {
-        const char *port = getenv("MASTER_PORT"), *run = getenv("TORCHELASTIC_RUN_ID");
-        if (port) snprintf(kbuf, sizeof kbuf, "p%s_%s", port, run ? run : "");
-        else snprintf(kbuf, sizeof kbuf, "pp%ld", (long)getppid());
-        key = kbuf;
-    }
-    snprintf(path, pathlen, "%s/xg_rdzv_%s.bin", dir, key);
-    if (rank == 0) {
-        char tmp[4200];
-        FILE *f;
-        if (xg_get_unique_id(uid)) return -1;
-        snprintf(tmp, sizeof tmp, "%s.%ld", path, (long)getpid());
-        f = fopen(tmp, "wb");
-        if (!f || fwrite(uid, 1, XG_UNIQUE_ID_BYTES, f) != XG_UNIQUE_ID_BYTES) { perror(tmp); return -1; }
-        fclose(f);
-        if (rename(tmp, path)) { perror(path); return -1; }
-        return 0;
-    }
-    for (;;) {
-        struct stat st;
-        if (stat(path, &st) == 0 && st.st_mtime >= (time_t)t_start - 30) {
-            FILE *f = fopen(path, "rb");
-            if (f) {
-                size_t n = fread(uid, 1, XG_UNIQUE_ID_BYTES, f);
-                fclose(f);
-                if (n == XG_UNIQUE_ID_BYTES) return 0;
-            }
-        }
-        if (now_s() - t_start > 120) {
-            fprintf(stderr, "rank %d/%d: no RCCL id at %s after 120 s\n", rank, nranks, path);
-            return -1;
-        }
-        { struct timespec ts = {0, 2000000}; nanosleep(&ts, NULL); }
-    }
-}
 
 #define DIE(...) do { fprintf(stderr, __VA_ARGS__); fputc('\n', stderr); exit(1); } while (0)
 #define XGCALL(x) do { int rc_ = (x); if (rc_) DIE("xg call failed (%d): %s", rc_, #x); } while (0)
@@ -199,11 +143,11 @@ int main(int argc, char **argv)
         {0, 0, 0, 0}};
     prefix[0] = '\0';
 
-    rank = env_int("RANK", "PMI_RANK", 0);
-    nranks = env_int("WORLD_SIZE", "PMI_SIZE", 1);
-    device = env_int("LOCAL_RANK", "MPI_LOCALRANKID", rank);
-    procs = env_int("XG_PROCS", NULL, 0);
-    verify = env_int("XG_VERIFY", NULL, 0);
+    rank = xg_env_int("RANK", "PMI_RANK", 0);
+    nranks = xg_env_int("WORLD_SIZE", "PMI_SIZE", 1);
+    device = xg_env_int("LOCAL_RANK", "MPI_LOCALRANKID", rank);
+    procs = xg_env_int("XG_PROCS", NULL, 0);
+    verify = xg_env_int("XG_VERIFY", NULL, 0);
     if (getenv("XG_FINGERPRINT") && !strcmp(getenv("XG_FINGERPRINT"), "strong")) fp_mode = XG_FP_STRONG;
     if (getenv("XG_EAGER_LIMIT")) eager = atoll(getenv("XG_EAGER_LIMIT"));
     if (getenv("XG_PACK_MAX_SEG")) pack_max = atoll(getenv("XG_PACK_MAX_SEG"));
@@ -236,7 +180,7 @@ int main(int argc, char **argv)
     if (cb_nodes < 1 || cb_nodes > procs) DIE("-a %d: need 1 <= aggregators <= ranks (%d)", cb_nodes, procs);
     if (data_size < 0) DIE("-d must be >= 0");
 
-    if (nranks > 1 && rendezvous(rank, nranks, uid, rdzv_path, sizeof rdzv_path)) DIE("rendezvous failed");
+    if (nranks > 1 && xg_rendezvous(rank, nranks, uid, rdzv_path, sizeof rdzv_path)) DIE("rendezvous failed");
     ngpu_dev = device;
     XGCALL(xg_init(&ctx, rank, nranks, ngpu_dev, uid));
     XGCALL(xg_barrier(ctx));

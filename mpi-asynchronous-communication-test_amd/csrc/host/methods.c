@@ -58,7 +58,7 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
     TRY(xg_plan_run(plan, done, post, &wall));
     xg_block_range(procs, G, g, &lo, &hi);
     if (timers)
-        for (r = lo; r < hi; ++r) xg_sched_rank_timer(s, r, done, post, &timers[r - lo]);
+        for (r = lo; r < hi; ++r) xg_sched_rank_timer(s, G, r, done, post, &timers[r - lo]);
     if (opts->verify) {
         int ns = xg_verify_slots(s, G, g, NULL);
         slots = (xg_slot *)malloc(sizeof(xg_slot) * (ns + 1));

@@ -52,6 +52,8 @@ struct xg_sched {
     int32_t **post_msg;          /* [rank][post] -> message */
     uint8_t **post_eager;        /* [rank][post] -> blocking send <= eager limit   */
     int nsteps;
+    int pc_ngpus;                /* posts per (gpu, step), cached for one ngpus    */
+    int32_t *post_count;
 };
 
 /* ------------------------------------------------------------------ helpers */
@@ -732,7 +734,7 @@ void xg_sched_free(xg_sched *s)
     if (s->post_msg)
         for (r = 0; r < s->P; ++r) { free(s->post_msg[r]); free(s->post_eager[r]); }
     free(s->post_msg); free(s->post_eager);
-    free(s->progs); free(s->msgs); free(s->msg_spost); free(s->msg_rpost);
+    free(s->progs); free(s->msgs); free(s->msg_spost); free(s->msg_rpost); free(s->post_count);
     free(s->rank_list); free(s->isagg); free(s->agg_prefix);
     free(s);
 }
@@ -866,29 +868,52 @@ size_t xg_sched_trace(const xg_sched *s, int rank, char *buf, size_t buflen)
 }
 
 /* ------------------------------------------------------------------ timers */
-int xg_sched_rank_timer(const xg_sched *s, int rank, const double *step_done,
+static void count_posts(xg_sched *s, int ngpus)
+{
+    int r, i;
+    if (s->post_count && s->pc_ngpus == ngpus) return;
+    free(s->post_count);
+    s->post_count = (int32_t *)calloc((size_t)ngpus * (s->nsteps + 1), sizeof(int32_t));
+    s->pc_ngpus = ngpus;
+    for (r = 0; r < s->P; ++r) {
+        const prog_t *p = &s->progs[r];
+        int g = xg_gpu_of(s->P, ngpus, r);
+        for (i = 0; i < p->nops; ++i)
+            if (p->ops[i].kind == OP_SEND || p->ops[i].kind == OP_RECV) {
+                int st = s->msgs[s->post_msg[r][p->ops[i].post]].step;
+                if (st >= 0) s->post_count[(size_t)g * (s->nsteps + 1) + st]++;
+            }
+    }
+}
+
+int xg_sched_rank_timer(xg_sched *s, int ngpus, int rank, const double *step_done,
                         const double *step_post, xg_timer *out)
 {
     const prog_t *p = &s->progs[rank];
     double clock = 0, open[4] = {0, 0, 0, 0}, acc[4] = {0, 0, 0, 0}, postacc = 0;
     int depth[4] = {0, 0, 0, 0};
-    int i, interval = 0;
-    int *stamp = (int *)calloc(s->nsteps + 1, sizeof(int));
+    int i;
+    const int32_t *pc = NULL;
+    if (ngpus < 1 || rank < 0 || rank >= s->P) return -1;
+    if (step_post) {
+        count_posts(s, ngpus);
+        pc = s->post_count + (size_t)xg_gpu_of(s->P, ngpus, rank) * (s->nsteps + 1);
+    }
     for (i = 0; i < p->nops; ++i) {
         const op_t *o = &p->ops[i];
         if (o->kind == OP_TMARK) {
             if (o->sign > 0) {
                 if (depth[o->field]++ == 0) {
                     open[o->field] = clock;
-                    if (o->field == F_POST) { postacc = 0; ++interval; }
+                    if (o->field == F_POST) postacc = 0;
                 }
             } else if (--depth[o->field] == 0) {
                 acc[o->field] += clock - open[o->field];
                 if (o->field == F_POST) acc[F_POST] += postacc;
             }
-        } else if ((o->kind == OP_SEND || o->kind == OP_RECV) && depth[F_POST] && step_post) {
+        } else if ((o->kind == OP_SEND || o->kind == OP_RECV) && depth[F_POST] && pc) {
             int st = s->msgs[s->post_msg[rank][o->post]].step;
-            if (st >= 0 && stamp[st] != interval) { stamp[st] = interval; postacc += step_post[st]; }
+            if (st >= 0 && pc[st] > 0) postacc += step_post[st] / pc[st];
         } else if (o->kind == OP_WAIT) {
             int q;
             for (q = 0; q < o->wcnt; ++q) {
@@ -900,7 +925,6 @@ int xg_sched_rank_timer(const xg_sched *s, int rank, const double *step_done,
             }
         }
     }
-    free(stamp);
     out->post_request_time = acc[F_POST];
     out->send_wait_all_time = acc[F_SEND];
     out->recv_wait_all_time = acc[F_RECV];

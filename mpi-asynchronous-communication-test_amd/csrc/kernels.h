@@ -165,6 +165,156 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(const DCopy *__restrict_
     }
 }
 
+// Global-address-space, software-pipelined variant: the next U 16-B loads of a
+// lane are issued before the current U stores, so U..2U loads stay in flight
+// and the compiler emits global_load/store_dwordx4 (vmcnt only) instead of
+// flat ops (which also wait on lgkmcnt).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_cu4;
+typedef __attribute__((address_space(1))) u32x4 g_u4;
+
+template <int U>
+__device__ __forceinline__ void pipelined_copy16(g_cu4 *__restrict__ s4, g_u4 *__restrict__ t4, int64_t n4)
+{
+    int64_t i = threadIdx.x;
+    const int64_t step = (int64_t)U * kThreads;
+    if (i + (U - 1) * (int64_t)kThreads < n4) {
+        u32x4 cur[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = s4[i + u * kThreads];
+        for (; i + step + (U - 1) * (int64_t)kThreads < n4; i += step) {
+            u32x4 nxt[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) nxt[u] = s4[i + step + u * kThreads];
+#pragma unroll
+            for (int u = 0; u < U; ++u) t4[i + u * kThreads] = cur[u];
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) t4[i + u * kThreads] = cur[u];
+        i += step;
+    }
+    for (; i < n4; i += kThreads) t4[i] = s4[i];
+}
+
+template <int U>
+__global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restrict__ pieces)
+{
+    const DCopy c = pieces[blockIdx.x];
+    const int64_t n = c.len;
+    if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)n) & 15) == 0) {
+        pipelined_copy16<U>((g_cu4 *)c.src, (g_u4 *)c.dst, n >> 4);
+    } else {
+        for (int64_t i = threadIdx.x; i < n; i += kThreads) c.dst[i] = c.src[i];
+    }
+}
+
+// ---------------------------------------------------------------- balanced byte-range copy
+// The launch's copies form one virtual byte space [0, total) (prefix[k] =
+// start of copy k, an exclusive scan of the lengths).  Workgroup b streams the
+// contiguous virtual range [b*per, (b+1)*per) -- equal bytes per workgroup, so
+// no tail wave; it crosses copy boundaries as it goes.  per is a multiple of
+// 16 and every copy length/pointer is 16-B aligned in this fast path (the
+// host falls back to copy_kernel otherwise).
+struct DSpan {
+    const uint8_t *src;
+    uint8_t *dst;
+    int64_t len;
+    int64_t start;      // exclusive prefix of len
+};
+
+template <int U>
+__global__ __launch_bounds__(kThreads) void span_copy_kernel(const DSpan *__restrict__ spans, int nspans,
+                                                             int64_t total, int64_t per)
+{
+    int64_t pos = (int64_t)blockIdx.x * per;
+    const int64_t end = pos + per < total ? pos + per : total;
+    if (pos >= end) return;
+    // first span containing pos (binary search, wave-uniform)
+    int lo = 0, hi = nspans - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (spans[mid].start <= pos) lo = mid; else hi = mid - 1;
+    }
+    int k = lo;
+    while (pos < end) {
+        const DSpan sp = spans[k];
+        const int64_t off = pos - sp.start;
+        const int64_t stop = (sp.start + sp.len < end ? sp.start + sp.len : end) - sp.start;
+        const uint4 *__restrict__ s4 = reinterpret_cast<const uint4 *>(sp.src + off);
+        uint4 *__restrict__ t4 = reinterpret_cast<uint4 *>(sp.dst + off);
+        const int64_t n4 = (stop - off) >> 4;
+        int64_t i = threadIdx.x;
+        for (; i + (int64_t)(U - 1) * kThreads < n4; i += (int64_t)U * kThreads) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = s4[i + u * kThreads];
+#pragma unroll
+            for (int u = 0; u < U; ++u) t4[i + u * kThreads] = v[u];
+        }
+        for (; i < n4; i += kThreads) t4[i] = s4[i];
+        pos = sp.start + stop;
+        ++k;
+    }
+}
+
+// exclusive prefix scan of span lengths, one workgroup (wave64 shuffles +
+// LDS across the 4 waves), carried across 256-span tiles -- the device
+// replacement of the displacement loops of *_alltoall_translate (:233-302)
+__global__ __launch_bounds__(kThreads) void span_scan_kernel(DSpan *spans, int n, int64_t *total)
+{
+    __shared__ int64_t wsum[kThreads / 64];
+    __shared__ int64_t carry;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += kThreads) {
+        const int i = base + threadIdx.x;
+        const int64_t v = i < n ? spans[i].len : 0;
+        int64_t x = v;                                 // inclusive scan inside the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        int64_t before = carry;
+        for (int w = 0; w < wave; ++w) before += wsum[w];
+        if (i < n) spans[i].start = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == kThreads - 1) carry = before + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// ---------------------------------------------------------------- microbenchmarks
+__global__ __launch_bounds__(kThreads) void read_only_kernel(g_cu4 *__restrict__ s, int64_t n4, unsigned *sink)
+{
+    uint32_t x = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads) {
+        const u32x4 v = s[i];
+        x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (x == 0x9e3779b9u) atomicAdd(sink, 1u);
+}
+
+__global__ __launch_bounds__(kThreads) void write_only_kernel(g_u4 *__restrict__ t, int64_t n4)
+{
+    const u32x4 v = {1u, 2u, 3u, 4u};
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads)
+        t[i] = v;
+}
+
+__global__ __launch_bounds__(kThreads) void gridstride_copy_kernel(const uint4 *__restrict__ s, uint4 *__restrict__ t,
+                                                                   int64_t n4)
+{
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads)
+        t[i] = s[i];
+}
+
 // ---------------------------------------------------------------- verify
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v)
 {

@@ -110,7 +110,7 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     HIPCHK(hipSetDevice(device));
     xg_ctx *c = new xg_ctx();
     c->rank = rank; c->nranks = nranks; c->device = device; c->comm = nullptr;
-    c->chunk = 65536; c->variant = 0; c->kt_on = false; c->nk = 0;
+    c->chunk = 32768; c->variant = 5; c->kt_on = false; c->nk = 0;   // measured best: profiles/r01_copy_ab.txt
     const char *env = getenv("XG_COPY_CHUNK");
     if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
     env = getenv("XG_COPY_VARIANT");
@@ -190,7 +190,7 @@ extern "C" int xg_device_info(xg_ctx *c, char *name, size_t namelen, int *cus, s
 extern "C" int xg_set_copy_params(xg_ctx *c, int64_t chunk, int variant)
 {
     if (chunk >= 4096) c->chunk = chunk & ~(int64_t)15;
-    c->variant = variant;
+    if (variant >= 0) c->variant = variant;
     return XG_OK;
 }
 
@@ -416,7 +416,10 @@ static int launch_copy(xg_plan *p, int b, int n)
     case 2: hipLaunchKernelGGL((xgk::copy_kernel<8, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 3: hipLaunchKernelGGL((xgk::copy_kernel<8, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 4: hipLaunchKernelGGL((xgk::copy_kernel<2, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    default: hipLaunchKernelGGL((xgk::copy_kernel<4, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 5: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 6: hipLaunchKernelGGL((xgk::copy_kernel_g<2>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 0: hipLaunchKernelGGL((xgk::copy_kernel<4, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     }
     HIPCHK(hipGetLastError());
     return XG_OK;
@@ -518,4 +521,129 @@ extern "C" int xg_ktime_end(xg_ctx *c, double *total_ms, int *launches, int64_t 
     if (launches) *launches = c->nk;
     if (bytes) *bytes = b;
     return XG_OK;
+}
+
+// ------------------------------------------------------------------ microbenchmark: HBM copy ceiling
+// kind 0: grid-stride float4 copy (the canonical copy), grid = 256 CUs x 8 blocks
+// kind 1: copy_kernel<4> over 64 KiB pieces (the exchange's default)
+// kind 2: span_copy_kernel<4>, 2048 workgroups, equal contiguous byte ranges
+// gbps = 2 * bytes / average time (read + write)
+extern "C" int xg_copy_ceiling(xg_ctx *c, int64_t bytes, int kind, int reps, double *gbps)
+{
+    HIPCHK(hipSetDevice(c->device));
+    bytes &= ~(int64_t)65535;
+    if (bytes <= 0 || reps < 1) return XG_EARG;
+    uint8_t *a, *b;
+    HIPCHK(hipMalloc(&a, bytes));
+    HIPCHK(hipMalloc(&b, bytes));
+    HIPCHK(hipMemsetAsync(a, 1, bytes, c->stream));
+    std::vector<xgk::DCopy> pieces;
+    for (int64_t o = 0; o < bytes; o += 65536) pieces.push_back({a + o, b + o, 65536});
+    xgk::DCopy *dp;
+    xgk::DSpan sp = {a, b, bytes, 0}, *ds;
+    HIPCHK(hipMalloc(&dp, sizeof(xgk::DCopy) * pieces.size()));
+    HIPCHK(hipMemcpy(dp, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&ds, sizeof sp));
+    HIPCHK(hipMemcpy(ds, &sp, sizeof sp, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    const int nb = 2048;
+    const int64_t per = ((bytes + nb - 1) / nb + 4095) & ~(int64_t)4095;
+    for (int r = -2; r < reps; ++r) {          // 2 warm-up launches
+        if (r == 0) HIPCHK(hipEventRecord(e0, c->stream));
+        if (kind == 0)
+            hipLaunchKernelGGL(xgk::gridstride_copy_kernel, dim3(nb), dim3(xgk::kThreads), 0, c->stream,
+                               (const uint4 *)a, (uint4 *)b, bytes / 16);
+        else if (kind == 1)
+            hipLaunchKernelGGL((xgk::copy_kernel<4, false>), dim3((unsigned)pieces.size()), dim3(xgk::kThreads), 0,
+                               c->stream, dp);
+        else if (kind == 2)
+            hipLaunchKernelGGL((xgk::span_copy_kernel<4>), dim3(nb), dim3(xgk::kThreads), 0, c->stream, ds, 1, bytes,
+                               per);
+        else if (kind == 3)
+            hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3((unsigned)pieces.size()), dim3(xgk::kThreads), 0,
+                               c->stream, dp);
+        else if (kind == 4)
+            hipLaunchKernelGGL((xgk::copy_kernel_g<2>), dim3((unsigned)pieces.size()), dim3(xgk::kThreads), 0,
+                               c->stream, dp);
+        else if (kind == 5)
+            hipLaunchKernelGGL(xgk::read_only_kernel, dim3(nb * 2), dim3(xgk::kThreads), 0, c->stream,
+                               (xgk::g_cu4 *)a, bytes / 16, (unsigned *)ds);
+        else
+            hipLaunchKernelGGL(xgk::write_only_kernel, dim3(nb * 2), dim3(xgk::kThreads), 0, c->stream,
+                               (xgk::g_u4 *)b, bytes / 16);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(e1, c->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    *gbps = (kind >= 5 ? 1.0 : 2.0) * (double)bytes * reps / (ms * 1e-3) / 1e9;
+    HIPCHK(hipEventDestroy(e0));
+    HIPCHK(hipEventDestroy(e1));
+    HIPCHK(hipFree(a));
+    HIPCHK(hipFree(b));
+    HIPCHK(hipFree(dp));
+    HIPCHK(hipFree(ds));
+    return XG_OK;
+}
+
+// ------------------------------------------------------------------ microbenchmark: RCCL p2p ceiling
+// The rccl-tests sendrecv analogue (and the GPU version of pt2pt_test,
+// mpi_sendrecv_test.c:15-74).  mode 0: all pairs (every rank sends `bytes` to
+// every other rank, one group); mode 1: ring (send to r+1, receive from r-1);
+// mode 2: one direction 1 -> 0 (pt2pt_test's Issend/Irecv pair), other ranks idle.
+// *gbps = bytes this rank sent (mode 2: received on rank 0) per second; *sec = seconds per rep.
+extern "C" int xg_p2p_bench(xg_ctx *c, int64_t bytes, int mode, int reps, double *gbps, double *sec)
+{
+    const int n = c->nranks, r = c->rank;
+    if (n < 2 || bytes <= 0 || reps < 1 || mode < 0 || mode > 2) return XG_EARG;
+    HIPCHK(hipSetDevice(c->device));
+    const int npeer = mode == 0 ? n - 1 : 1;
+    uint8_t *sb, *rb;
+    HIPCHK(hipMalloc(&sb, bytes * npeer));
+    HIPCHK(hipMalloc(&rb, bytes * npeer));
+    HIPCHK(hipMemsetAsync(sb, r & 0xff, bytes * npeer, c->stream));
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    int rc = XG_OK;
+    auto one = [&]() -> int {
+        NCCLCHK(ncclGroupStart());
+        if (mode == 0) {
+            for (int k = 1; k < n; ++k) {
+                const int to = (r + k) % n, from = (r - k + n) % n;
+                NCCLCHK(ncclSend(sb + (int64_t)(k - 1) * bytes, (size_t)bytes, ncclUint8, to, c->comm, c->stream));
+                NCCLCHK(ncclRecv(rb + (int64_t)(k - 1) * bytes, (size_t)bytes, ncclUint8, from, c->comm, c->stream));
+            }
+        } else if (mode == 1) {
+            NCCLCHK(ncclSend(sb, (size_t)bytes, ncclUint8, (r + 1) % n, c->comm, c->stream));
+            NCCLCHK(ncclRecv(rb, (size_t)bytes, ncclUint8, (r - 1 + n) % n, c->comm, c->stream));
+        } else if (r == 1) {
+            NCCLCHK(ncclSend(sb, (size_t)bytes, ncclUint8, 0, c->comm, c->stream));
+        } else if (r == 0) {
+            NCCLCHK(ncclRecv(rb, (size_t)bytes, ncclUint8, 1, c->comm, c->stream));
+        }
+        NCCLCHK(ncclGroupEnd());
+        return XG_OK;
+    };
+    for (int w = 0; w < 2 && !rc; ++w) rc = one();          // connection set-up + warm-up
+    if (!rc) rc = xg_barrier(c);
+    if (!rc) {
+        HIPCHK(hipEventRecord(e0, c->stream));
+        for (int k = 0; k < reps && !rc; ++k) rc = one();
+        HIPCHK(hipEventRecord(e1, c->stream));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        const double s_rep = ms * 1e-3 / reps;
+        if (sec) *sec = s_rep;
+        if (gbps) *gbps = (mode == 2 ? (r < 2 ? (double)bytes : 0.0) : (double)bytes * npeer) / s_rep / 1e9;
+    }
+    HIPCHK(hipEventDestroy(e0));
+    HIPCHK(hipEventDestroy(e1));
+    HIPCHK(hipFree(sb));
+    HIPCHK(hipFree(rb));
+    return rc;
 }

@@ -99,7 +99,7 @@ def host():
         h.xg_sched_msgs.argtypes = [C.c_void_p]
         h.xg_sched_trace.restype = C.c_size_t
         h.xg_sched_trace.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_size_t]
-        h.xg_sched_rank_timer.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double),
+        h.xg_sched_rank_timer.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
                                           C.POINTER(C.c_double), C.POINTER(Timer)]
         h.xg_block_range.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         h.xg_gpu_of.argtypes = [C.c_int, C.c_int, C.c_int]
@@ -168,11 +168,12 @@ class Schedule:
         host().xg_sched_trace(self._h, rank, buf, n + 1)
         return buf.value.decode()
 
-    def rank_timer(self, rank, step_done, step_post=None):
+    def rank_timer(self, rank, step_done, step_post=None, ngpus=1):
         nd = (C.c_double * max(1, len(step_done)))(*step_done)
         npost = (C.c_double * max(1, len(step_post)))(*step_post) if step_post is not None else None
         t = Timer()
-        host().xg_sched_rank_timer(self._h, rank, nd, npost, C.byref(t))
+        if host().xg_sched_rank_timer(self._h, ngpus, rank, nd, npost, C.byref(t)) != 0:
+            raise XGError("xg_sched_rank_timer: bad rank/ngpus")
         return t
 
     def gpu_of(self, ngpus, rank):
@@ -269,6 +270,8 @@ def device():
         d.xg_ktime_begin.argtypes = [vp, ip]
         d.xg_ktime_end.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(ip), C.POINTER(i64)]
         d.xg_set_copy_params.argtypes = [vp, i64, ip]
+        d.xg_copy_ceiling.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double)]
+        d.xg_p2p_bench.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         _dev = d
     return _dev
 
@@ -321,6 +324,16 @@ class Context:
 
     def set_copy_params(self, chunk=0, variant=0):
         _check(_dev.xg_set_copy_params(self._c, chunk, variant), "xg_set_copy_params")
+
+    def copy_ceiling(self, nbytes, kind, reps=20):
+        g = C.c_double()
+        _check(_dev.xg_copy_ceiling(self._c, nbytes, kind, reps, C.byref(g)), "xg_copy_ceiling")
+        return g.value
+
+    def p2p_bench(self, nbytes, mode=0, reps=20):
+        g, sec = C.c_double(), C.c_double()
+        _check(_dev.xg_p2p_bench(self._c, nbytes, mode, reps, C.byref(g), C.byref(sec)), "xg_p2p_bench")
+        return g.value, sec.value
 
     def ktime_begin(self, max_launches=4096):
         _check(_dev.xg_ktime_begin(self._c, max_launches), "xg_ktime_begin")

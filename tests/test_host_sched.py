@@ -76,6 +76,20 @@ def test_timer_semantics(xg):
     assert t_non.total_time <= t_agg.total_time + 1e-12
 
 
+def test_post_time_is_shared_over_posted_requests(xg):
+    """A step's host enqueue time is shared over the requests posted in it, so the
+    post times of all ranks of one GPU sum to the GPU's enqueue time."""
+    rl = xg.aggregator_list(8, 3)
+    s = xg.Schedule(1, 8, 3, 64, 1000, rl)       # one step; 8*3 sends + 3*8 recvs = 48 posts
+    posts = [s.rank_timer(r, [0.002], [0.008]).post_request_time for r in range(8)]
+    assert sum(posts) == pytest.approx(0.008)
+    assert posts[0] == pytest.approx(0.008 * 11 / 48)          # aggregator: 8 recvs + 3 sends
+    assert posts[1] == pytest.approx(0.008 * 3 / 48)           # non-aggregator: 3 sends
+    # two GPUs: each GPU's enqueue time is shared over its own ranks' posts
+    posts2 = [s.rank_timer(r, [0.002], [0.008], ngpus=2).post_request_time for r in range(8)]
+    assert sum(posts2[:4]) == pytest.approx(0.008) and sum(posts2[4:]) == pytest.approx(0.008)
+
+
 def test_summarize_results_format(xg, tmp_path, capfd):
     """xg_summarize_results prints exactly the reference's report lines (masked golden)."""
     import re
