@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--size", type=int, default=1 << 20)
     ap.add_argument("--comm-size", type=int, default=200000000)
     ap.add_argument("--methods", default="1,2,3,4")
-    ap.add_argument("--pack-max-seg", type=int, default=1 << 20)
+    ap.add_argument("--pack-max-seg", type=int, default=4 << 20)
     ap.add_argument("--copy-variant", type=int, default=-1)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -127,7 +127,7 @@ int main(int argc, char **argv)
     /* defaults of mpi_test.c:2121 */
     int cb_nodes = 1, method = 0, data_size = 0, proc_node = 1, i, comm_size = 200000000, iter = 1, ntimes = 1;
     int aggregator_type = 1, barrier_type = 0, procs = 0, verify = 0, fp_mode = XG_FP_REFERENCE;
-    int64_t eager = XG_MPICH_EAGER_LIMIT, pack_max = 1 << 20;
+    int64_t eager = XG_MPICH_EAGER_LIMIT, pack_max = 4 << 20;
     char prefix[200];
     int rank, nranks, device, ngpu_dev;
     unsigned char uid[XG_UNIQUE_ID_BYTES];

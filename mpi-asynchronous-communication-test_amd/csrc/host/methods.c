@@ -17,7 +17,7 @@ void xg_run_opts_default(xg_run_opts *o)
     o->verify = 0;
     o->fingerprint = XG_FP_REFERENCE;
     o->eager_limit = XG_MPICH_EAGER_LIMIT;
-    o->pack_max_seg = 1 << 20;
+    o->pack_max_seg = 4 << 20;
 }
 
 #define TRY(x) do { rc = (x); if (rc) goto out; } while (0)

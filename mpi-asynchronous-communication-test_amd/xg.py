@@ -193,7 +193,7 @@ class Schedule:
     def region_bytes(self, ngpus, g, buf):
         return host().xg_region_bytes(self._h, ngpus, g, buf)
 
-    def devplan(self, ngpus, g, pack_max_seg=1 << 20):
+    def devplan(self, ngpus, g, pack_max_seg=4 << 20):
         return DevicePlanView(self, ngpus, g, pack_max_seg)
 
     def fill_runs(self, ngpus, g):
@@ -357,7 +357,7 @@ class MethodRun:
     """prepare_*_data + the compiled plan of one method on this GPU:
     HBM regions, fingerprint fill (untimed), plan upload."""
 
-    def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=1 << 20):
+    def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20):
         d = device()
         self.ctx, self.sched, self.it, self.mode = ctx, sched, it, mode
         G, g = ctx.nranks, ctx.rank

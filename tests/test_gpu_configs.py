@@ -1,0 +1,62 @@
+"""BASELINE.json configs as GPU parity cases (1 MI355X hosts every logical rank).
+
+At these sizes the oracle cannot replay the bytes on the CPU in seconds, so the
+checks are size-independent: every received byte is compared on the device with
+the closed-form fingerprint (xg_verify: zero mismatching bytes, strong mode so a
+misroute cannot hide), the CPU oracle confirms the schedule (every rank's MPI
+call trace equals the oracle's restatement), and the sum of the per-slot
+checksums equals the oracle's closed-form value for a sample of slots.
+"""
+import pytest
+
+import xg_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (name, P, A, d, c, methods, k)
+    ("config2_p32_a14_d1m", 32, 14, 1 << 20, 200000000, range(1, 13), 2),
+    ("config3_p64_a16_d256k", 64, 16, 256 << 10, 200000000, range(1, 13), 1),
+    ("config4_p256_a32_d4m", 256, 32, 4 << 20, 200000000, (1, 2, 9, 10), 1),
+    ("config5_p256_a64_d256k_c1", 256, 64, 256 << 10, 1, (7, 11, 12), 1),
+    ("config5_p256_a64_d256k_c3", 256, 64, 256 << 10, 3, (7, 11, 12), 1),
+    ("config5_p256_a64_d256k_c8", 256, 64, 256 << 10, 8, (7, 11, 12), 1),
+]
+
+
+@pytest.fixture(scope="module")
+def ctx(xg):
+    c = xg.Context(rank=0, nranks=1, device=0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_config(xg, ctx, case):
+    _name, P, A, d, c, methods, k = case
+    rl = xg.aggregator_list(P, A)
+    for m in methods:
+        try:
+            s = xg.Schedule(m, P, A, d, c, rl, ntimes=k)
+        except xg.XGError as e:
+            # the only refusal allowed: a schedule the reference itself deadlocks on
+            assert "deadlocks" in str(e) and m == 6, e
+            with pytest.raises(RuntimeError, match="deadlock"):
+                O.asap_steps(O.programs(m, P, A, d, c, rl, k))
+            continue
+        run = xg.MethodRun(ctx, s, it=1, mode=1)
+        try:
+            done, _post, _wall = run.run_timed()
+            assert len(done) == s.nsteps and all(t >= 0 for t in done)
+            chk, bad, first = run.verify()
+            assert sum(1 for b in bad if b) == 0, (m, [(sl, b, f) for sl, b, f in zip(run.slots, bad, first) if b][:3])
+            # sampled slots: checksum equals the oracle closed form
+            for i in range(0, len(run.slots), max(1, len(run.slots) // 7)):
+                src, seed, dst, _off = run.slots[i]
+                assert chk[i] == O.chk64(O.fingerprint(1, src, seed, 1, d)), (m, i)
+        finally:
+            run.close()
+        # the schedule: per-rank trace identical to the oracle's restatement (sampled ranks)
+        progs = O.programs(m, P, A, d, c, rl, k)
+        for r in range(0, P, max(1, P // 16)):
+            assert s.trace(r) == O.trace_tokens(progs[r]), (m, r)
