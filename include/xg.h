@@ -56,7 +56,7 @@ int xg_finalize(xg_ctx *ctx);
 int xg_rank(const xg_ctx *ctx);
 int xg_nranks(const xg_ctx *ctx);
 int xg_barrier(xg_ctx *ctx);
-int xg_allreduce_max(xg_ctx *ctx, double *vals, int n);       /* in place, MAX over all GPUs */
+int xg_allreduce_max(xg_ctx *ctx, double *vals, int n);       /* in place, MAX over all GPUs (any n) */
 int xg_sync(xg_ctx *ctx);                                      /* this context's stream */
 int xg_device_sync(xg_ctx *ctx);                               /* whole device (hipDeviceSynchronize) */
 /* device name, CU count, HBM bytes (any pointer may be NULL) */
@@ -132,6 +132,9 @@ typedef struct {
     int fingerprint;         /* XG_FP_REFERENCE (MAP_DATA) or XG_FP_STRONG                    */
     int64_t eager_limit;     /* blocking sends <= this complete locally (XG_MPICH_EAGER_LIMIT)  */
     int64_t pack_max_seg;    /* p2p staging threshold (xg_devplan_build)                       */
+    int proc_node;           /* -p (m17's node_robin_map)                                       */
+    int barrier_type;        /* -b (m13)                                                        */
+    xg_timer *rep_timers;    /* out, optional: hosted ranks x ntimes timers[m] (m13)            */
 } xg_run_opts;
 
 void xg_run_opts_default(xg_run_opts *o);
@@ -141,7 +144,7 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
                   int comm_size, xg_timer *timers, int iter, int ntimes, const xg_run_opts *opts,
                   int64_t *bad_slots, char *err, size_t errlen);
 
-/* The twelve operators under the reference's names (mpi_test.c line of the original). */
+/* The operators under the reference's names (mpi_test.c line of the original). */
 #define XG_METHOD_DECL(name)                                                                     \
     int name(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size, \
              xg_timer *timers, int iter, int ntimes)
@@ -157,6 +160,15 @@ XG_METHOD_DECL(xg_all_to_many_pairwise);        /* m9  :510  */
 XG_METHOD_DECL(xg_many_to_all_pairwise);        /* m10 :421  */
 XG_METHOD_DECL(xg_many_to_all_half_sync);       /* m11 :942  */
 XG_METHOD_DECL(xg_all_to_many_half_sync2);      /* m12 :999  */
+XG_METHOD_DECL(xg_many_to_all_scattered);       /* m14 :656  */
+XG_METHOD_DECL(xg_all_to_many_balanced_control);/* m18 :1229 */
+XG_METHOD_DECL(xg_all_to_many_scattered_isend); /* m19 :722  */
+XG_METHOD_DECL(xg_all_to_many_balanced_pre_send);/* m20 :1338 */
+/* m13 / m17 take the reference's extra arguments (:797, :1135) */
+int xg_all_to_many_scattered(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
+                             int barrier_type, xg_timer *timers, xg_timer *rep_timers, int iter, int ntimes);
+int xg_all_to_many_node_robin(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
+                              int proc_node, xg_timer *timers, int iter, int ntimes);
 
 #ifdef __cplusplus
 }

@@ -65,19 +65,21 @@ typedef struct xg_sched xg_sched;
  * aggregator type the reference does not define. */
 int xg_aggregator_list(int procs, int cb_nodes, int proc_node, int type, int *rank_list);
 
-/* Label printed by summarize_results for a method (mpi_test.c:2186-2271), NULL if out of scope. */
+/* Label printed by summarize_results for a method (mpi_test.c:2186-2337), NULL if not 1..20. */
 const char *xg_method_label(int method);
-/* XG_A2M or XG_M2A, -1 if method not in 1..12. */
+/* XG_A2M or XG_M2A; -1 for a method this build does not run (15, 16, or not 1..20). */
 int xg_method_direction(int method);
 
-/* Build the schedule of one method run (all `ntimes` repetitions).
- * eager_limit: blocking sends of <= eager_limit bytes complete locally
- * (XG_MPICH_EAGER_LIMIT reproduces the reference built on the image's MPICH).
+/* Build the schedule of one method run (all `ntimes` repetitions).  Methods
+ * 1..14 and 17..20 (15/16 = TAM are not part of this build).  proc_node (-p)
+ * matters to m17 only (node_robin_map, :1116-1133); barrier_type (-b) to m13.
+ * eager_limit: blocking sends and Isends of <= eager_limit bytes complete
+ * locally (XG_MPICH_EAGER_LIMIT reproduces the reference on the image's MPICH).
  * Returns NULL and writes a message into err on failure, e.g. when the
  * programs deadlock under MPI semantics (the reference hangs there too). */
 xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size, int comm_size,
-                         const int *rank_list, int ntimes, int64_t eager_limit,
-                         char *err, size_t errlen);
+                         const int *rank_list, int ntimes, int proc_node, int barrier_type,
+                         int64_t eager_limit, char *err, size_t errlen);
 void xg_sched_free(xg_sched *s);
 
 int xg_sched_nmsg(const xg_sched *s);
@@ -102,6 +104,14 @@ size_t xg_sched_trace(const xg_sched *s, int rank, char *buf, size_t buflen);
  * enqueue time of the requests it posts. */
 int xg_sched_rank_timer(xg_sched *s, int ngpus, int rank, const double *step_done,
                         const double *step_post, xg_timer *out);
+/* timers[m] of every repetition (m13, mpi_test.c:829-874; zero for other methods):
+ * reps has xg_sched_ntimes(s) entries. */
+int xg_sched_rank_rep_timers(xg_sched *s, int ngpus, int rank, const double *step_done,
+                             const double *step_post, xg_timer *reps);
+int xg_sched_ntimes(const xg_sched *s);
+/* step after which the k-th MPI_Barrier of the method completes (-1: before step 0);
+ * returns the number of barriers (out may be NULL). */
+int xg_sched_barrier_epochs(const xg_sched *s, int32_t *out);
 
 /* ---------------------------------------------------------------- device plan
  * Block mapping of logical ranks onto G GPUs: gpu(r) = r / ceil(P/G).
@@ -130,6 +140,7 @@ typedef struct {
     int32_t pre_begin, pre_count;     /* local copies + packs   (before the exchange) */
     int32_t p2p_begin, p2p_count;     /* grouped RCCL send/recv                       */
     int32_t post_begin, post_count;   /* unpacks                (after the exchange)  */
+    int32_t sync_after, pad;          /* 1: device-side barrier of all GPUs after it  */
 } xg_stepplan;
 
 typedef struct {
@@ -171,6 +182,11 @@ enum { XG_FP_REFERENCE = 0, XG_FP_STRONG = 1 };   /* fingerprint modes (DESIGN.m
  * Return the count; out may be NULL to query it. */
 int xg_fill_runs(const xg_sched *s, int ngpus, int g, xg_segrun *out);
 int xg_verify_slots(const xg_sched *s, int ngpus, int g, xg_slot *out);
+
+/* save_all_timing (mpi_test.c:2008-2066): the four per-repetition CSVs of m13,
+ * <prefix>send_wait_all_times_<c>.csv, total_times, post_request_time,
+ * barrier_time; timers = procs x ntimes, rank-major. */
+int xg_save_all_timing(int procs, int ntimes, int comm_size, const xg_timer *timers, const char *prefix);
 
 /* ---------------------------------------------------------------- report
  * summarize_results (mpi_test.c:2068-2118): 8 "| ..." lines on stdout and one

@@ -12,8 +12,8 @@
  *  - Launch: single process, or any launcher that sets RANK/WORLD_SIZE
  *    (torchrun --no-python) or PMI_RANK/PMI_SIZE (mpiexec).  The RCCL unique
  *    id is handed over through a file in $XG_RDZV_DIR (default /tmp).
- *  - -m 0 runs methods 1..12; 13..20 are outside this build's scope and are
- *    reported as skipped on stderr.
+ *  - -m 0 runs methods 1..14 and 17..20; 15/16 (TAM, lustre_driver_test.c)
+ *    are not part of this build and are reported as skipped on stderr.
  *  - Extra, opt-in: --verify (or XG_VERIFY=1) checks every received byte on
  *    the GPU and prints one extra "| <label> verify ..." line per method;
  *    --fingerprint strong switches to the collision-free fingerprint.
@@ -65,10 +65,11 @@ static void usage(const char *argv0)   /* mpi_test.c:41-69 */
 #define XGCALL(x) do { int rc_ = (x); if (rc_) DIE("xg call failed (%d): %s", rc_, #x); } while (0)
 
 typedef struct {
-    int P, A, d, c, ntimes, type, proc_node;
+    int P, A, d, c, ntimes, type, proc_node, barrier_type;
     int verify, fp_mode;
     int64_t eager, pack_max;
     int *rank_list;
+    const char *prefix;
 } opts_t;
 
 static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
@@ -78,7 +79,7 @@ static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
     char err[512];
     int lo, hi, r, rc;
     int64_t bad = 0;
-    xg_timer *timers, t0 = {0, 0, 0, 0, 0}, tmax = {0, 0, 0, 0, 0};
+    xg_timer *timers, *reps = NULL, t0 = {0, 0, 0, 0, 0}, tmax = {0, 0, 0, 0, 0};
     xg_run_opts ro;
     double red[5], t_wall;
 
@@ -86,6 +87,9 @@ static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
     timers = (xg_timer *)calloc(hi - lo + 1, sizeof(xg_timer));
     xg_run_opts_default(&ro);
     ro.verify = o->verify; ro.fingerprint = o->fp_mode; ro.eager_limit = o->eager; ro.pack_max_seg = o->pack_max;
+    ro.proc_node = o->proc_node; ro.barrier_type = o->barrier_type;
+    if (method == 13 && o->ntimes > 0)
+        ro.rep_timers = reps = (xg_timer *)calloc((size_t)(hi - lo + 1) * o->ntimes, sizeof(xg_timer));
     t_wall = xg_now();
     rc = xg_run_method(ctx, method, o->P, o->A, o->d, o->rank_list, o->c, timers, iter, o->ntimes, &ro, &bad,
                        err, sizeof err);
@@ -93,6 +97,7 @@ static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
     if (rc == XG_ESCHED) {          /* every process computes the same schedule */
         if (g == 0) fprintf(stderr, "| %s: %s\n", label, err);
         free(timers);
+        free(reps);
         return;
     }
     if (rc) DIE("%s failed: %s", label, err);
@@ -110,6 +115,15 @@ static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
     XGCALL(xg_allreduce_max(ctx, red, 5));
     tmax.post_request_time = red[0]; tmax.send_wait_all_time = red[1]; tmax.recv_wait_all_time = red[2];
     tmax.barrier_time = 0; tmax.total_time = red[4];
+    if (reps) {   /* save_all_timing (:2279): gather every rank's timers[m] to rank 0, write the CSVs */
+        size_t n = (size_t)o->P * o->ntimes * 5;
+        double *all = (double *)calloc(n, sizeof(double));
+        memcpy(all + (size_t)lo * o->ntimes * 5, reps, sizeof(xg_timer) * (size_t)(hi - lo) * o->ntimes);
+        XGCALL(xg_allreduce_max(ctx, all, (int)n));       /* timers are >= 0: MAX = gather */
+        if (g == 0) xg_save_all_timing(o->P, o->ntimes, o->c, (const xg_timer *)all, o->prefix);
+        free(all);
+        free(reps);
+    }
     if (g == 0) {
         xg_summarize_results(o->P, o->A, o->d, o->c, o->ntimes, o->type, "results.csv", label, t0, tmax);
         if (o->verify) {
@@ -174,7 +188,7 @@ int main(int argc, char **argv)
             return 0;
         }
     }
-    (void)barrier_type;   /* -b only affects method 13 (out of scope) */
+
     if (procs <= 0) procs = nranks;
     if (nranks > procs) DIE("more GPU processes (%d) than logical ranks (%d)", nranks, procs);
     if (cb_nodes < 1 || cb_nodes > procs) DIE("-a %d: need 1 <= aggregators <= ranks (%d)", cb_nodes, procs);
@@ -188,6 +202,7 @@ int main(int argc, char **argv)
 
     o.P = procs; o.A = cb_nodes; o.d = data_size; o.c = comm_size; o.ntimes = ntimes; o.type = aggregator_type;
     o.proc_node = proc_node; o.verify = verify; o.fp_mode = fp_mode; o.eager = eager; o.pack_max = pack_max;
+    o.barrier_type = barrier_type; o.prefix = prefix;
     o.rank_list = (int *)malloc(sizeof(int) * cb_nodes);
     if (xg_aggregator_list(procs, cb_nodes, proc_node, aggregator_type, o.rank_list))
         DIE("-t %d: aggregator type not defined by the reference", aggregator_type);
@@ -198,13 +213,14 @@ int main(int argc, char **argv)
         printf("aggregators = ");
         for (i = 0; i < cb_nodes; ++i) printf("%d, ", o.rank_list[i]);
         printf("\n");
-        if (method > 12) fprintf(stderr, "method %d is outside this build's scope (1..12)\n", method);
-        if (method == 0) fprintf(stderr, "-m 0: running methods 1..12 (13..20 are outside this build's scope)\n");
+        if (method == 15 || method == 16)
+            fprintf(stderr, "method %d (TAM, lustre_driver_test.c) is not part of this build\n", method);
+        if (method == 0) fprintf(stderr, "-m 0: running methods 1..14, 17..20 (15/16 = TAM are not part of this build)\n");
     }
     for (i = 0; i < iter; ++i) {   /* :2181-2343 */
         int m;
-        for (m = 1; m <= 12; ++m)
-            if (method == 0 || method == m) run_method(ctx, &o, m, i);
+        for (m = 1; m <= 20; ++m)
+            if ((method == 0 || method == m) && xg_method_direction(m) >= 0) run_method(ctx, &o, m, i);
         if (rank == 0) {
             printf("| --------------------------------------\n");
             fflush(stdout);

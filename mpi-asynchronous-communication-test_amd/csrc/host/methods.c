@@ -18,6 +18,9 @@ void xg_run_opts_default(xg_run_opts *o)
     o->fingerprint = XG_FP_REFERENCE;
     o->eager_limit = XG_MPICH_EAGER_LIMIT;
     o->pack_max_seg = 4 << 20;
+    o->proc_node = 1;
+    o->barrier_type = 0;
+    o->rep_timers = NULL;
 }
 
 #define TRY(x) do { rc = (x); if (rc) goto out; } while (0)
@@ -41,8 +44,8 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
     if (!opts) { xg_run_opts_default(&dflt); opts = &dflt; }
     if (!err) { err = ebuf; errlen = sizeof ebuf; }
     if (bad_slots) *bad_slots = 0;
-    s = xg_sched_build(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, opts->eager_limit,
-                       err, errlen);
+    s = xg_sched_build(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, opts->proc_node,
+                       opts->barrier_type, opts->eager_limit, err, errlen);
     if (!s) return XG_ESCHED;
     dp = xg_devplan_build(s, G, g, opts->pack_max_seg);
     TRY(xg_regions_alloc(ctx, dp->region_bytes, &reg));
@@ -59,6 +62,9 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
     xg_block_range(procs, G, g, &lo, &hi);
     if (timers)
         for (r = lo; r < hi; ++r) xg_sched_rank_timer(s, G, r, done, post, &timers[r - lo]);
+    if (opts->rep_timers && ntimes > 0)
+        for (r = lo; r < hi; ++r)
+            xg_sched_rank_rep_timers(s, G, r, done, post, opts->rep_timers + (size_t)(r - lo) * ntimes);
     if (opts->verify) {
         int ns = xg_verify_slots(s, G, g, NULL);
         slots = (xg_slot *)malloc(sizeof(xg_slot) * (ns + 1));
@@ -103,3 +109,36 @@ XG_METHOD_DEF(xg_all_to_many_pairwise, 9)
 XG_METHOD_DEF(xg_many_to_all_pairwise, 10)
 XG_METHOD_DEF(xg_many_to_all_half_sync, 11)
 XG_METHOD_DEF(xg_all_to_many_half_sync2, 12)
+XG_METHOD_DEF(xg_many_to_all_scattered, 14)
+XG_METHOD_DEF(xg_all_to_many_balanced_control, 18)
+XG_METHOD_DEF(xg_all_to_many_scattered_isend, 19)
+XG_METHOD_DEF(xg_all_to_many_balanced_pre_send, 20)
+
+int xg_all_to_many_scattered(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
+                             int barrier_type, xg_timer *timers, xg_timer *rep_timers, int iter, int ntimes)
+{
+    xg_run_opts o;
+    char e[512];
+    int rc;
+    xg_run_opts_default(&o);
+    o.barrier_type = barrier_type;
+    o.rep_timers = rep_timers;
+    rc = xg_run_method(ctx, 13, procs, cb_nodes, data_size, rank_list, comm_size, timers, iter, ntimes, &o, NULL,
+                       e, sizeof e);
+    if (rc == XG_ESCHED) fprintf(stderr, "xg_all_to_many_scattered: %s\n", e);
+    return rc;
+}
+
+int xg_all_to_many_node_robin(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
+                              int proc_node, xg_timer *timers, int iter, int ntimes)
+{
+    xg_run_opts o;
+    char e[512];
+    int rc;
+    xg_run_opts_default(&o);
+    o.proc_node = proc_node;
+    rc = xg_run_method(ctx, 17, procs, cb_nodes, data_size, rank_list, comm_size, timers, iter, ntimes, &o, NULL,
+                       e, sizeof e);
+    if (rc == XG_ESCHED) fprintf(stderr, "xg_all_to_many_node_robin: %s\n", e);
+    return rc;
+}

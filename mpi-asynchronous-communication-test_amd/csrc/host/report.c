@@ -41,3 +41,25 @@ int xg_summarize_results(int procs, int cb_nodes, int data_size, int comm_size, 
     fclose(f);
     return 0;
 }
+
+/* save_all_timing, mpi_test.c:2008-2066 (rank 0 part, after the gather) */
+int xg_save_all_timing(int procs, int ntimes, int comm_size, const xg_timer *timers, const char *prefix)
+{
+    static const char *names[4] = {"send_wait_all_times", "total_times", "post_request_time", "barrier_time"};
+    static const int fields[4] = {1, 4, 0, 3};     /* xg_timer field index */
+    char fn[512];
+    int k, i, j;
+    for (k = 0; k < 4; ++k) {
+        FILE *f;
+        snprintf(fn, sizeof fn, "%s%s_%d.csv", prefix ? prefix : "", names[k], comm_size);
+        f = fopen(fn, "w");
+        if (!f) return -1;
+        for (i = 0; i < procs; ++i) {
+            fprintf(f, "%d", i);
+            for (j = 0; j < ntimes; ++j) fprintf(f, ",%lf", ((const double *)&timers[(size_t)i * ntimes + j])[fields[k]]);
+            fprintf(f, "\n");
+        }
+        fclose(f);
+    }
+    return 0;
+}

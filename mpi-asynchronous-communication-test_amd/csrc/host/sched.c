@@ -18,16 +18,23 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { OP_BARRIER, OP_SEND, OP_RECV, OP_WAIT, OP_A2AW, OP_COPY, OP_TMARK };
-enum { F_POST = 0, F_SEND = 1, F_RECV = 2, F_TOTAL = 3 };
+enum { OP_BARRIER, OP_SEND, OP_RECV, OP_WAIT, OP_A2AW, OP_COPY, OP_TMARK,
+       OP_REP, OP_MARK, OP_DELTA, OP_ACC, OP_COPYT, OP_ZERO };
+/* timer fields in xg_timer order */
+enum { F_POST = 0, F_SEND = 1, F_RECV = 2, F_BARRIER = 3, F_TOTAL = 4, NF = 5 };
+/* per-repetition timer DSL (m13's timers[m], mpi_test.c:829-874): targets and registers */
+enum { TG_G = 0, TG_R = 1 };
+enum { REG_S = 0, REG_T2 = 1, NREG = 2 };
 
 typedef struct {
-    int8_t kind, blocking, field, sign;
+    int8_t kind, eager_ok, field, sign;   /* eager_ok: Send / Sendrecv / Isend (not Issend)  */
+    int8_t isend, comm, tgt, tgt2;        /* comm 0 = MPI_COMM_WORLD; tgt*: timer DSL        */
     int32_t coll;           /* -1: point-to-point; k: the rank's k-th Alltoallw */
     int32_t peer;
-    int32_t idx;            /* send: segment; recv: slot; copy: segment      */
-    int32_t idx2;           /* copy: slot                                     */
-    int32_t post;           /* send/recv: post index; copy: message index      */
+    int32_t tag;            /* matching tag (reference: rank + peer on WORLD)     */
+    int32_t idx;            /* send: segment; recv: slot; copy: segment; DSL: rep / reg */
+    int32_t idx2;           /* copy: slot; DSL: source field / mode               */
+    int32_t post;           /* send/recv: post index; copy: message index; barrier: ordinal */
     int32_t wbeg, wcnt;     /* wait: range in the rank's pool                 */
     int64_t cnt;
 } op_t;
@@ -37,11 +44,13 @@ typedef struct {
     int nops, cap;
     int32_t *pool;
     int npool, poolcap;
-    int nposts, ncoll;
+    int nposts, ncoll, nbarrier, rank;
 } prog_t;
 
 struct xg_sched {
-    int method, P, A, ntimes, dir, c;
+    int method, P, A, ntimes, dir, c, proc_node, barrier_type;
+    int nbarrier;                /* barriers per rank (same for every rank)          */
+    int32_t *barrier_epoch;      /* step after which barrier k has completed (-1: none) */
     int64_t d, eager;
     int *rank_list;
     int *isagg, *agg_prefix;     /* agg_prefix[r] = number of aggregator ranks < r */
@@ -77,20 +86,55 @@ static op_t *push(prog_t *p)
     return o;
 }
 
-static int post_send(prog_t *p, int peer, int64_t cnt, int seg, int blocking)
+/* send post; tag < 0 means the reference's rank + peer on MPI_COMM_WORLD */
+static int post_send_ex(prog_t *p, int peer, int64_t cnt, int seg, int eager_ok, int isend, int comm, int tag)
 {
     op_t *o = push(p);
-    o->kind = OP_SEND; o->peer = peer; o->cnt = cnt; o->idx = seg; o->blocking = (int8_t)blocking;
+    o->kind = OP_SEND; o->peer = peer; o->cnt = cnt; o->idx = seg;
+    o->eager_ok = (int8_t)(eager_ok || isend); o->isend = (int8_t)isend; o->comm = (int8_t)comm;
+    o->tag = tag >= 0 ? tag : p->rank + peer;
     o->post = p->nposts++;
     return o->post;
 }
 
-static int post_recv(prog_t *p, int peer, int64_t cnt, int slot)
+static int post_recv_ex(prog_t *p, int peer, int64_t cnt, int slot, int comm, int tag)
 {
     op_t *o = push(p);
-    o->kind = OP_RECV; o->peer = peer; o->cnt = cnt; o->idx = slot;
+    o->kind = OP_RECV; o->peer = peer; o->cnt = cnt; o->idx = slot; o->comm = (int8_t)comm;
+    o->tag = tag >= 0 ? tag : p->rank + peer;
     o->post = p->nposts++;
     return o->post;
+}
+
+static int post_send(prog_t *p, int peer, int64_t cnt, int seg, int blocking)
+{
+    return post_send_ex(p, peer, cnt, seg, blocking, 0, 0, -1);
+}
+
+static int post_recv(prog_t *p, int peer, int64_t cnt, int slot) { return post_recv_ex(p, peer, cnt, slot, 0, -1); }
+
+static void barrier(prog_t *p)
+{
+    op_t *o = push(p);
+    o->kind = OP_BARRIER;
+    o->post = p->nbarrier++;
+}
+
+/* timer DSL (m13) */
+static void t_rep(prog_t *p, int m) { op_t *o = push(p); o->kind = OP_REP; o->idx = m; }
+static void t_mark(prog_t *p, int reg) { op_t *o = push(p); o->kind = OP_MARK; o->idx = reg; }
+static void t_zero(prog_t *p, int tgt, int f) { op_t *o = push(p); o->kind = OP_ZERO; o->tgt = (int8_t)tgt; o->field = (int8_t)f; }
+/* tgt.f (=|+=) clock - reg */
+static void t_delta(prog_t *p, int tgt, int f, int reg, int add)
+{
+    op_t *o = push(p);
+    o->kind = OP_DELTA; o->tgt = (int8_t)tgt; o->field = (int8_t)f; o->idx = reg; o->idx2 = add;
+}
+/* tgt.f += tgt2.f2  (kind OP_ACC) or  tgt.f = tgt2.f2 (OP_COPYT) */
+static void t_acc(prog_t *p, int kind, int tgt, int f, int tgt2, int f2)
+{
+    op_t *o = push(p);
+    o->kind = (int8_t)kind; o->tgt = (int8_t)tgt; o->field = (int8_t)f; o->tgt2 = (int8_t)tgt2; o->idx2 = f2;
 }
 
 static void wait_list(prog_t *p, const int *idx, int n)
@@ -145,7 +189,7 @@ static void il_push(ilist *l, int x)
 
 typedef struct {
     prog_t *p;
-    int rank, isagg, myindex, P, A, c, ntimes;
+    int rank, isagg, myindex, P, A, c, ntimes, proc_node, barrier_type;
     int64_t d;
     const int *rl;
 } ctx_t;
@@ -516,6 +560,268 @@ static void m_pairwise(ctx_t *x, int dir)
     free(sc);
 }
 
+static int scattered_block(int P, int c)    /* :674-684, :740-750, :815-825 */
+{
+    if (c > P) c = P;
+    return c != 0 ? c : P;
+}
+
+static void wait_bracket(prog_t *p, const ilist *l, int isagg)   /* recv (+send for non-aggregators) */
+{
+    tstart(p, F_RECV);
+    if (!isagg) tstart(p, F_SEND);
+    wait_list(p, l->v, l->n);
+    tstop(p, F_RECV);
+    if (!isagg) tstop(p, F_SEND);
+}
+
+/* all_to_many_scattered, mpi_test.c:797-882 (barrier type -b, per-repetition timers[m]) */
+static void m13_scattered(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, m, i, ii, dst;
+    int64_t *sc = xmalloc(sizeof(int64_t) * 4 * P), *sd = sc + P, *rc = sc + 2 * P, *rd = sc + 3 * P;
+    int bblock = scattered_block(P, x->c);
+    ilist l = {0};
+    translate(x, XG_A2M, sc, sd, rc, rd);
+    for (m = 0; m < x->ntimes; ++m) {
+        t_rep(p, m);
+        t_mark(p, REG_T2);
+        t_zero(p, TG_R, F_BARRIER);
+        for (ii = 0; ii < P; ii += bblock) {
+            int ss = P - ii < bblock ? P - ii : bblock;
+            l.n = 0;
+            t_mark(p, REG_S);
+            for (i = 0; i < ss; ++i) {
+                dst = (x->rank + i + ii) % P;
+                if (rc[dst]) il_push(&l, post_recv(p, dst, rc[dst], (int)(rd[dst] / x->d)));
+            }
+            for (i = 0; i < ss; ++i) {
+                dst = (x->rank - i - ii + P) % P;
+                if (sc[dst]) il_push(&l, post_send(p, dst, sc[dst], (int)(sd[dst] / x->d), 0));
+            }
+            t_delta(p, TG_R, F_POST, REG_S, 0);
+            t_acc(p, OP_ACC, TG_G, F_POST, TG_R, F_POST);
+            if (l.n) {
+                t_mark(p, REG_S);
+                wait_list(p, l.v, l.n);
+                t_delta(p, TG_R, F_RECV, REG_S, 0);
+                t_acc(p, OP_ACC, TG_G, F_RECV, TG_R, F_RECV);
+                if (!x->isagg) {
+                    t_acc(p, OP_ACC, TG_G, F_SEND, TG_R, F_RECV);
+                    t_acc(p, OP_COPYT, TG_R, F_SEND, TG_R, F_RECV);
+                }
+            }
+            if (x->barrier_type == 2) {
+                t_mark(p, REG_S);
+                barrier(p);
+                t_delta(p, TG_R, F_BARRIER, REG_S, 1);
+                t_acc(p, OP_ACC, TG_G, F_BARRIER, TG_R, F_BARRIER);
+            }
+        }
+        t_delta(p, TG_R, F_TOTAL, REG_T2, 0);
+        if (x->barrier_type == 1) {
+            t_mark(p, REG_S);
+            barrier(p);
+            t_delta(p, TG_R, F_BARRIER, REG_S, 0);
+            t_acc(p, OP_ACC, TG_G, F_BARRIER, TG_R, F_BARRIER);
+        }
+    }
+    free(l.v);
+    free(sc);
+}
+
+/* many_to_all_scattered, mpi_test.c:656-720 */
+static void m14_scattered(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, m, i, ii, dst;
+    int64_t *sc = xmalloc(sizeof(int64_t) * 4 * P), *sd = sc + P, *rc = sc + 2 * P, *rd = sc + 3 * P;
+    int bblock = scattered_block(P, x->c);
+    ilist l = {0};
+    translate(x, XG_M2A, sc, sd, rc, rd);
+    for (m = 0; m < x->ntimes; ++m)
+        for (ii = 0; ii < P; ii += bblock) {
+            int ss = P - ii < bblock ? P - ii : bblock;
+            l.n = 0;
+            tstart(p, F_POST);
+            for (i = 0; i < ss; ++i) {
+                dst = (x->rank + i + ii) % P;
+                if (rc[dst]) il_push(&l, post_recv(p, dst, rc[dst], (int)(rd[dst] / x->d)));
+            }
+            for (i = 0; i < ss; ++i) {
+                dst = (x->rank - i - ii + P) % P;
+                if (sc[dst]) il_push(&l, post_send(p, dst, sc[dst], (int)(sd[dst] / x->d), 0));
+            }
+            tstop(p, F_POST);
+            if (l.n) { tstart(p, F_RECV); wait_list(p, l.v, l.n); tstop(p, F_RECV); }
+        }
+    free(l.v);
+    free(sc);
+}
+
+/* node_robin_map, mpi_test.c:1116-1133 */
+static void node_robin(int rank, int proc_node, int P, int *map, int *rank_index)
+{
+    int i, j = 0, count = 0;
+    *rank_index = 0;
+    for (i = 0; i < P; ++i) {
+        map[i] = count;
+        if (count == rank) *rank_index = i;
+        count += proc_node;
+        if (count >= P) { j++; count = j; }
+    }
+}
+
+/* all_to_many_node_robin, mpi_test.c:1135-1227 (a barrier inside every round) */
+static void m17_node_robin(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, A = x->A, m, i, k, xx, cs, rank_index;
+    int ceiling = (P + A - 1) / A, floor_ = P / A, remainder = P % A;
+    int *map = (int *)xmalloc(sizeof(int) * P), bblock, send_start;
+    ilist l = {0};
+    node_robin(x->rank, x->proc_node, P, map, &rank_index);
+    bblock = x->c > P ? P : x->c;
+    send_start = send_start0(rank_index, ceiling, floor_, remainder);
+    for (m = 0; m < x->ntimes; ++m) {
+        cs = bblock;
+        for (k = 0; k < P; k += cs) {
+            if (P - k < cs) cs = P - k;
+            l.n = 0;
+            tstart(p, F_POST);
+            if (x->isagg)
+                for (i = 0; i < cs; ++i) {
+                    int temp = map[win_start(x->myindex, (long)k + i, ceiling, floor_, remainder) % P];
+                    il_push(&l, post_recv(p, temp, x->d, temp));
+                }
+            barrier(p);
+            for (xx = 0; xx < A; ++xx) {
+                long temp = win_start(send_start, k, ceiling, floor_, remainder);
+                if (!in_window(rank_index, temp, cs, P)) break;
+                il_push(&l, post_send(p, x->rl[send_start], x->d, send_start, 0));
+                send_start = (send_start - 1 + A) % A;
+            }
+            tstop(p, F_POST);
+            if (l.n) wait_bracket(p, &l, x->isagg);
+        }
+    }
+    free(l.v);
+    free(map);
+}
+
+/* all_to_many_balanced_control, mpi_test.c:1229-1336 (0-byte go-signals on a dup'd communicator) */
+static void m18_balanced_control(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, A = x->A, m, i, k, xx, cs;
+    int ceiling = (P + A - 1) / A, floor_ = P / A, remainder = P % A;
+    int bblock = x->c > P ? P : x->c;
+    int send_start = send_start0(x->rank, ceiling, floor_, remainder);
+    ilist l = {0};
+    for (m = 0; m < x->ntimes; ++m) {
+        cs = bblock;
+        for (k = 0; k < P; k += cs) {
+            if (P - k < cs) cs = P - k;
+            l.n = 0;
+            tstart(p, F_POST);
+            if (x->isagg)
+                for (i = 0; i < cs; ++i) {
+                    int temp = (int)(win_start(x->myindex, (long)k + i, ceiling, floor_, remainder) % P);
+                    if (temp != x->rank) {
+                        il_push(&l, post_recv(p, temp, x->d, temp));
+                        il_push(&l, post_send_ex(p, temp, 0, -1, 1, 1, 1, x->rank + temp * 100));  /* :1283 */
+                    } else {
+                        copy_op(p, x->myindex, temp, x->d);                                       /* :1285 */
+                    }
+                }
+            for (xx = 0; xx < A; ++xx) {
+                long temp = win_start(send_start, k, ceiling, floor_, remainder);
+                if (!in_window(x->rank, temp, cs, P)) break;
+                if (x->rl[send_start] != x->rank) {
+                    int peer = x->rl[send_start];
+                    wait1(p, post_recv_ex(p, peer, 0, -1, 1, x->rank * 100 + peer));              /* :1299 */
+                    il_push(&l, post_send(p, peer, x->d, send_start, 0));
+                }
+                send_start = (send_start - 1 + A) % A;
+            }
+            tstop(p, F_POST);
+            if (l.n) wait_bracket(p, &l, x->isagg);
+        }
+    }
+    free(l.v);
+}
+
+/* all_to_many_scattered_isend, mpi_test.c:722-795 (MPI_Isend; barrier before the total stop) */
+static void m19_scattered_isend(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, m, i, ii, dst;
+    int64_t *sc = xmalloc(sizeof(int64_t) * 4 * P), *sd = sc + P, *rc = sc + 2 * P, *rd = sc + 3 * P;
+    int bblock = scattered_block(P, x->c);
+    ilist l = {0};
+    translate(x, XG_A2M, sc, sd, rc, rd);
+    for (m = 0; m < x->ntimes; ++m)
+        for (ii = 0; ii < P; ii += bblock) {
+            int ss = P - ii < bblock ? P - ii : bblock;
+            l.n = 0;
+            for (i = 0; i < ss; ++i) {
+                dst = (x->rank + i + ii) % P;
+                if (rc[dst]) il_push(&l, post_recv(p, dst, rc[dst], (int)(rd[dst] / x->d)));
+            }
+            for (i = 0; i < ss; ++i) {
+                dst = (x->rank - i - ii + P) % P;
+                if (sc[dst]) {
+                    if (!x->isagg) tstart(p, F_POST);
+                    il_push(&l, post_send_ex(p, dst, sc[dst], (int)(sd[dst] / x->d), 1, 1, 0, -1));
+                    if (!x->isagg) tstop(p, F_POST);
+                }
+            }
+            if (l.n) wait_bracket(p, &l, x->isagg);
+        }
+    barrier(p);
+    free(l.v);
+    free(sc);
+}
+
+/* all_to_many_balanced_pre_send, mpi_test.c:1338-1419 */
+static void m20_balanced_presend(ctx_t *x)
+{
+    prog_t *p = x->p;
+    int P = x->P, A = x->A, m, i, k, cs;
+    int ceiling = (P + A - 1) / A, floor_ = P / A, remainder = P % A;
+    int bblock = x->c > P ? P : x->c;
+    int send_start = send_start0(x->rank, ceiling, floor_, remainder);
+    ilist l = {0}, sends = {0};
+    for (m = 0; m < x->ntimes; ++m) {
+        cs = bblock;
+        sends.n = 0;
+        for (k = 0; k < A; ++k) {
+            i = (send_start - k + A) % A;
+            if (x->rl[i] != x->rank) il_push(&sends, post_send(p, x->rl[i], x->d, i, 0));
+        }
+        for (k = 0; k < P; k += cs) {
+            if (P - k < cs) cs = P - k;
+            l.n = 0;
+            if (x->isagg)
+                for (i = 0; i < cs; ++i) {
+                    int temp = (int)(win_start(x->myindex, (long)k + i, ceiling, floor_, remainder) % P);
+                    if (temp != x->rank) {
+                        tstart(p, F_POST);
+                        il_push(&l, post_recv(p, temp, x->d, temp));
+                        tstop(p, F_POST);
+                    } else {
+                        copy_op(p, x->myindex, temp, x->d);                                       /* :1398 */
+                    }
+                }
+            if (l.n) { tstart(p, F_RECV); wait_list(p, l.v, l.n); tstop(p, F_RECV); }
+        }
+        if (sends.n) { tstart(p, F_SEND); wait_list(p, sends.v, sends.n); tstop(p, F_SEND); }
+    }
+    free(l.v);
+    free(sends.v);
+}
+
 /* ------------------------------------------------------------------ public: placement / labels */
 int xg_aggregator_list(int procs, int cb_nodes, int proc_node, int type, int *rl)
 {
@@ -543,38 +849,50 @@ int xg_aggregator_list(int procs, int cb_nodes, int proc_node, int type, int *rl
     return 0;
 }
 
-const char *xg_method_label(int method)
+const char *xg_method_label(int method)   /* mpi_test.c:2186-2337 */
 {
     static const char *labels[] = {
         NULL, "All to many", "Many to all", "All to many balanced", "Many to all balanced",
         "Many to all benchmark", "All to many sync", "All to many half sync", "All to many benchmark",
         "All to many pairwise", "Many to all pairwise", "Many to all half sync", "All to many half sync 2",
+        "All to many scattered", "Many to all scattered", "All to many TAM", "Many to all TAM",
+        "All to many node robin", "All to many balanced control", "All to many scattered isend",
+        "All to many balanced presend",
     };
-    return method >= 1 && method <= 12 ? labels[method] : NULL;
+    return method >= 1 && method <= 20 ? labels[method] : NULL;
 }
 
 int xg_method_direction(int method)
 {
     switch (method) {
-    case 1: case 3: case 6: case 7: case 8: case 9: case 12: return XG_A2M;
-    case 2: case 4: case 5: case 10: case 11: return XG_M2A;
-    default: return -1;
+    case 1: case 3: case 6: case 7: case 8: case 9: case 12: case 13: case 17: case 18: case 19: case 20:
+        return XG_A2M;
+    case 2: case 4: case 5: case 10: case 11: case 14: return XG_M2A;
+    default: return -1;      /* 15/16 (TAM) are not part of this build */
     }
 }
 
 /* ------------------------------------------------------------------ matching */
 typedef struct {
-    int32_t coll, a, b, rank, post, idx;
+    int32_t coll, comm, a, b, tag, rank, post, idx;
     int64_t cnt;
 } pst_t;
 
+/* channel = (collective, communicator, src, dst, tag); FIFO inside a channel */
 static int pst_cmp(const void *x_, const void *y_)
 {
     const pst_t *x = (const pst_t *)x_, *y = (const pst_t *)y_;
     if (x->coll != y->coll) return x->coll < y->coll ? -1 : 1;
+    if (x->comm != y->comm) return x->comm < y->comm ? -1 : 1;
     if (x->a != y->a) return x->a < y->a ? -1 : 1;
     if (x->b != y->b) return x->b < y->b ? -1 : 1;
+    if (x->tag != y->tag) return x->tag < y->tag ? -1 : 1;
     return x->post < y->post ? -1 : x->post > y->post;
+}
+
+static int same_channel(const pst_t *x, const pst_t *y)
+{
+    return x->coll == y->coll && x->comm == y->comm && x->a == y->a && x->b == y->b && x->tag == y->tag;
 }
 
 static xg_msg *new_msg(xg_sched *s)
@@ -608,10 +926,10 @@ static int do_match(xg_sched *s, char *err, size_t errlen)
         for (i = 0; i < p->nops; ++i) {
             const op_t *o = &p->ops[i];
             if (o->kind == OP_SEND) {
-                pst_t t = { o->coll, r, o->peer, r, o->post, o->idx, o->cnt };
+                pst_t t = { o->coll, o->comm, r, o->peer, o->coll >= 0 ? 0 : o->tag, r, o->post, o->idx, o->cnt };
                 S[ns++] = t;
             } else if (o->kind == OP_RECV) {
-                pst_t t = { o->coll, o->peer, r, r, o->post, o->idx, o->cnt };
+                pst_t t = { o->coll, o->comm, o->peer, r, o->coll >= 0 ? 0 : o->tag, r, o->post, o->idx, o->cnt };
                 R[nr++] = t;
             }
         }
@@ -620,7 +938,7 @@ static int do_match(xg_sched *s, char *err, size_t errlen)
     qsort(R, nr, sizeof(pst_t), pst_cmp);
     for (i = 0, j = 0; i < ns || j < nr; ++i, ++j) {
         xg_msg *m;
-        if (i >= ns || j >= nr || S[i].coll != R[j].coll || S[i].a != R[j].a || S[i].b != R[j].b) {
+        if (i >= ns || j >= nr || !same_channel(&S[i], &R[j])) {
             const pst_t *u = i < ns ? &S[i] : &R[j];
             snprintf(err, errlen, "unmatched point-to-point traffic %d -> %d (the reference would hang)", u->a, u->b);
             free(S); free(R);
@@ -658,9 +976,20 @@ static int do_match(xg_sched *s, char *err, size_t errlen)
 /* ------------------------------------------------------------------ step compiler */
 static int compile_steps(xg_sched *s, char *err, size_t errlen)
 {
-    int P = s->P, r, progress = 1, maxstep = -1;
+    int P = s->P, r, progress = 1, maxstep = -1, b;
     int *pc = (int *)xmalloc(sizeof(int) * P), *epoch = (int *)xmalloc(sizeof(int) * P);
     int32_t **pe = (int32_t **)xmalloc(sizeof(int32_t *) * P);     /* post epoch */
+    int nb = s->progs[0].nbarrier;
+    int *arrived = (int *)calloc(nb + 1, sizeof(int)), *arr_epoch = (int *)xmalloc(sizeof(int) * (nb + 1));
+    for (r = 1; r < P; ++r)
+        if (s->progs[r].nbarrier != nb) {
+            snprintf(err, errlen, "ranks disagree on the number of MPI_Barrier calls");
+            free(arrived); free(arr_epoch); free(pc); free(epoch); free(pe);
+            return -1;
+        }
+    s->nbarrier = nb;
+    s->barrier_epoch = (int32_t *)xmalloc(sizeof(int32_t) * (nb + 1));
+    for (b = 0; b < nb; ++b) { arr_epoch[b] = -1; s->barrier_epoch[b] = INT_MIN; }
     for (r = 0; r < P; ++r) {
         int q;
         pc[r] = 0; epoch[r] = -1;
@@ -673,7 +1002,18 @@ static int compile_steps(xg_sched *s, char *err, size_t errlen)
             prog_t *p = &s->progs[r];
             while (pc[r] < p->nops) {
                 op_t *o = &p->ops[pc[r]];
-                if (o->kind == OP_SEND || o->kind == OP_RECV) {
+                if (o->kind == OP_BARRIER) {
+                    /* collective: every rank arrives, all leave at the latest arrival epoch */
+                    b = o->post;
+                    if (o->eager_ok == 0) {                 /* first visit: register arrival */
+                        o->eager_ok = 1;
+                        arrived[b]++;
+                        if (epoch[r] > arr_epoch[b]) arr_epoch[b] = epoch[r];
+                    }
+                    if (arrived[b] < P) break;
+                    s->barrier_epoch[b] = arr_epoch[b];
+                    if (arr_epoch[b] > epoch[r]) epoch[r] = arr_epoch[b];
+                } else if (o->kind == OP_SEND || o->kind == OP_RECV) {
                     pe[r][o->post] = epoch[r];
                 } else if (o->kind == OP_COPY) {
                     s->msgs[o->post].step = epoch[r] + 1;
@@ -718,8 +1058,13 @@ static int compile_steps(xg_sched *s, char *err, size_t errlen)
                 if (s->msgs[i].step > maxstep) maxstep = s->msgs[i].step;
             }
         for (r = 0; r < P; ++r) free(pe[r]);
-        free(pe); free(pc); free(epoch);
+        free(pe); free(pc); free(epoch); free(arrived); free(arr_epoch);
         s->nsteps = maxstep + 1;
+        for (r = 0; r < P; ++r) {       /* reset the arrival marks used above */
+            int i;
+            for (i = 0; i < s->progs[r].nops; ++i)
+                if (s->progs[r].ops[i].kind == OP_BARRIER) s->progs[r].ops[i].eager_ok = 0;
+        }
         return bad ? -1 : 0;
     }
 }
@@ -735,19 +1080,25 @@ void xg_sched_free(xg_sched *s)
         for (r = 0; r < s->P; ++r) { free(s->post_msg[r]); free(s->post_eager[r]); }
     free(s->post_msg); free(s->post_eager);
     free(s->progs); free(s->msgs); free(s->msg_spost); free(s->msg_rpost); free(s->post_count);
+    free(s->barrier_epoch);
     free(s->rank_list); free(s->isagg); free(s->agg_prefix);
     free(s);
 }
 
 xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size, int comm_size,
-                         const int *rank_list, int ntimes, int64_t eager_limit, char *err, size_t errlen)
+                         const int *rank_list, int ntimes, int proc_node, int barrier_type,
+                         int64_t eager_limit, char *err, size_t errlen)
 {
     xg_sched *s;
     int r, i;
     char dummy[8];
     if (!err) { err = dummy; errlen = sizeof dummy; }
     err[0] = 0;
-    if (method < 1 || method > 12) { snprintf(err, errlen, "method %d is out of scope (1..12)", method); return NULL; }
+    if (xg_method_direction(method) < 0) {
+        snprintf(err, errlen, "method %d is not part of this build (1..14, 17..20)", method);
+        return NULL;
+    }
+    if (proc_node < 1) proc_node = 1;
     if (procs < 1 || cb_nodes < 1 || cb_nodes > procs || data_size < 0 || ntimes < 0) {
         snprintf(err, errlen, "bad sizes P=%d A=%d d=%lld k=%d", procs, cb_nodes, (long long)data_size, ntimes);
         return NULL;
@@ -758,6 +1109,7 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
     s = (xg_sched *)calloc(1, sizeof *s);
     s->method = method; s->P = procs; s->A = cb_nodes; s->d = data_size; s->c = comm_size;
     s->ntimes = ntimes; s->eager = eager_limit; s->dir = xg_method_direction(method);
+    s->proc_node = proc_node; s->barrier_type = barrier_type;
     s->rank_list = (int *)xmalloc(sizeof(int) * cb_nodes);
     memcpy(s->rank_list, rank_list, sizeof(int) * cb_nodes);
     s->isagg = (int *)calloc(procs, sizeof(int));
@@ -771,9 +1123,11 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
         prog_t *p = &s->progs[r];
         x.p = p; x.rank = r; x.isagg = s->isagg[r]; x.myindex = 0;
         x.P = procs; x.A = cb_nodes; x.c = comm_size; x.ntimes = ntimes; x.d = data_size; x.rl = rank_list;
+        x.proc_node = proc_node; x.barrier_type = barrier_type;
+        p->rank = r;
         for (i = 0; i < cb_nodes; ++i)            /* last match, :111-115 / :183-187 */
             if (rank_list[i] == r) x.myindex = i;
-        push(p)->kind = OP_BARRIER;
+        barrier(p);                                   /* MPI_Barrier before total_start */
         tstart(p, F_TOTAL);
         switch (method) {
         case 1: m1_all_to_many(&x); break;
@@ -788,6 +1142,12 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
         case 10: m_pairwise(&x, XG_M2A); break;
         case 11: m11_half_sync(&x); break;
         case 12: m12_half_sync2(&x); break;
+        case 13: m13_scattered(&x); break;
+        case 14: m14_scattered(&x); break;
+        case 17: m17_node_robin(&x); break;
+        case 18: m18_balanced_control(&x); break;
+        case 19: m19_scattered_isend(&x); break;
+        case 20: m20_balanced_presend(&x); break;
         }
         tstop(p, F_TOTAL);
     }
@@ -798,7 +1158,7 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
         s->post_msg[r] = (int32_t *)xmalloc(sizeof(int32_t) * (p->nposts + 1));
         s->post_eager[r] = (uint8_t *)calloc(p->nposts + 1, 1);
         for (i = 0; i < p->nops; ++i)
-            if (p->ops[i].kind == OP_SEND && p->ops[i].blocking && p->ops[i].cnt <= eager_limit)
+            if (p->ops[i].kind == OP_SEND && p->ops[i].eager_ok && p->ops[i].cnt <= eager_limit)
                 s->post_eager[r][p->ops[i].post] = 1;
     }
     if (do_match(s, err, errlen) || compile_steps(s, err, errlen)) {
@@ -839,8 +1199,11 @@ size_t xg_sched_trace(const xg_sched *s, int rank, char *buf, size_t buflen)
         if (o->kind == OP_BARRIER) strcpy(tok, "B");
         else if (o->kind == OP_A2AW) strcpy(tok, "A");
         else if (o->coll >= 0) continue;
-        else if (o->kind == OP_SEND) snprintf(tok, sizeof tok, "s%d:%lld", o->peer, (long long)o->cnt);
-        else if (o->kind == OP_RECV) snprintf(tok, sizeof tok, "r%d:%lld", o->peer, (long long)o->cnt);
+        else if (o->kind == OP_SEND || o->kind == OP_RECV) {
+            const char k = o->kind == OP_RECV ? 'r' : (o->isend ? 'i' : 's');
+            if (o->comm == 0) snprintf(tok, sizeof tok, "%c%d:%lld", k, o->peer, (long long)o->cnt);
+            else snprintf(tok, sizeof tok, "%c%d:%lld@%d#%d", k, o->peer, (long long)o->cnt, o->comm, o->tag);
+        }
         else if (o->kind == OP_WAIT) {
             int *v = (int *)xmalloc(sizeof(int) * (o->wcnt + 1)), a = 0;
             memcpy(v, p->pool + o->wbeg, sizeof(int) * o->wcnt);
@@ -886,51 +1249,100 @@ static void count_posts(xg_sched *s, int ngpus)
     }
 }
 
-int xg_sched_rank_timer(xg_sched *s, int ngpus, int rank, const double *step_done,
-                        const double *step_post, xg_timer *out)
+static void set_field(xg_timer *t, int f, double v)
+{
+    double *d = (double *)t;
+    d[f] = v;
+}
+
+static double get_field(const xg_timer *t, int f) { return ((const double *)t)[f]; }
+
+/* Replays rank `rank`'s program on the logical clock.  G: the method Timer;
+ * R (may be NULL): timers[m] of every repetition m (m13). */
+static int rank_timers(xg_sched *s, int ngpus, int rank, const double *step_done, const double *step_post,
+                       xg_timer *G, xg_timer *R)
 {
     const prog_t *p = &s->progs[rank];
-    double clock = 0, open[4] = {0, 0, 0, 0}, acc[4] = {0, 0, 0, 0}, postacc = 0;
-    int depth[4] = {0, 0, 0, 0};
-    int i;
+    double clock = 0, postacc = 0, open_c[NF], open_p[NF], reg_c[NREG] = {0, 0}, reg_p[NREG] = {0, 0};
+    int depth[NF] = {0, 0, 0, 0, 0}, i, rep = 0;
     const int32_t *pc = NULL;
+    xg_timer dummy;
     if (ngpus < 1 || rank < 0 || rank >= s->P) return -1;
     if (step_post) {
         count_posts(s, ngpus);
         pc = s->post_count + (size_t)xg_gpu_of(s->P, ngpus, rank) * (s->nsteps + 1);
     }
+    memset(G, 0, sizeof *G);
+    if (R) memset(R, 0, sizeof(xg_timer) * (s->ntimes > 0 ? s->ntimes : 1));
     for (i = 0; i < p->nops; ++i) {
         const op_t *o = &p->ops[i];
-        if (o->kind == OP_TMARK) {
-            if (o->sign > 0) {
-                if (depth[o->field]++ == 0) {
-                    open[o->field] = clock;
-                    if (o->field == F_POST) postacc = 0;
-                }
-            } else if (--depth[o->field] == 0) {
-                acc[o->field] += clock - open[o->field];
-                if (o->field == F_POST) acc[F_POST] += postacc;
-            }
-        } else if ((o->kind == OP_SEND || o->kind == OP_RECV) && depth[F_POST] && pc) {
+        xg_timer *tg = o->tgt == TG_R ? (R ? &R[rep] : &dummy) : G;
+        xg_timer *src = o->tgt2 == TG_R ? (R ? &R[rep] : &dummy) : G;
+        switch (o->kind) {
+        case OP_SEND:
+        case OP_RECV: {
             int st = s->msgs[s->post_msg[rank][o->post]].step;
-            if (st >= 0 && pc[st] > 0) postacc += step_post[st] / pc[st];
-        } else if (o->kind == OP_WAIT) {
+            if (pc && st >= 0 && pc[st] > 0) postacc += step_post[st] / pc[st];
+            break;
+        }
+        case OP_WAIT: {
             int q;
             for (q = 0; q < o->wcnt; ++q) {
-                int post = p->pool[o->wbeg + q];
-                int st;
-                if (s->post_eager[rank][post]) continue;
+                int post = p->pool[o->wbeg + q], st;
+                if (s->post_eager[rank][post]) continue;       /* eager send: completes locally */
                 st = s->msgs[s->post_msg[rank][post]].step;
                 if (st >= 0 && step_done[st] > clock) clock = step_done[st];
             }
+            break;
+        }
+        case OP_BARRIER: {
+            int e = s->barrier_epoch[o->post];
+            if (e >= 0 && step_done[e] > clock) clock = step_done[e];
+            break;
+        }
+        case OP_TMARK:
+            if (o->sign > 0) {
+                if (depth[o->field]++ == 0) { open_c[o->field] = clock; open_p[o->field] = postacc; }
+            } else if (--depth[o->field] == 0) {
+                double v = clock - open_c[o->field] + (o->field == F_POST ? postacc - open_p[o->field] : 0);
+                set_field(G, o->field, get_field(G, o->field) + v);
+            }
+            break;
+        case OP_REP: rep = o->idx < s->ntimes ? o->idx : 0; break;
+        case OP_MARK: reg_c[o->idx] = clock; reg_p[o->idx] = postacc; break;
+        case OP_ZERO: set_field(tg, o->field, 0); break;
+        case OP_DELTA: {
+            double v = clock - reg_c[o->idx] + (o->field == F_POST ? postacc - reg_p[o->idx] : 0);
+            set_field(tg, o->field, (o->idx2 ? get_field(tg, o->field) : 0) + v);
+            break;
+        }
+        case OP_ACC: set_field(tg, o->field, get_field(tg, o->field) + get_field(src, o->idx2)); break;
+        case OP_COPYT: set_field(tg, o->field, get_field(src, o->idx2)); break;
+        default: break;
         }
     }
-    out->post_request_time = acc[F_POST];
-    out->send_wait_all_time = acc[F_SEND];
-    out->recv_wait_all_time = acc[F_RECV];
-    out->barrier_time = 0;
-    out->total_time = acc[F_TOTAL];
     return 0;
+}
+
+int xg_sched_rank_timer(xg_sched *s, int ngpus, int rank, const double *step_done,
+                        const double *step_post, xg_timer *out)
+{
+    return rank_timers(s, ngpus, rank, step_done, step_post, out, NULL);
+}
+
+int xg_sched_rank_rep_timers(xg_sched *s, int ngpus, int rank, const double *step_done,
+                             const double *step_post, xg_timer *reps)
+{
+    xg_timer g;
+    return rank_timers(s, ngpus, rank, step_done, step_post, &g, reps);
+}
+
+int xg_sched_ntimes(const xg_sched *s) { return s->ntimes; }
+
+int xg_sched_barrier_epochs(const xg_sched *s, int32_t *out)
+{
+    if (out) memcpy(out, s->barrier_epoch, sizeof(int32_t) * s->nbarrier);
+    return s->nbarrier;
 }
 
 /* ------------------------------------------------------------------ block mapping / layout */
@@ -1024,6 +1436,9 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
     int64_t *bucket_b = (int64_t *)calloc((size_t)G * 2, sizeof(int64_t));
     dp->gpu = g; dp->ngpus = G; dp->nsteps = nst;
     dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan));
+    /* in-loop MPI_Barrier -> device-side barrier after the step it completes at (G > 1) */
+    for (i = 0; i < s->nbarrier; ++i)
+        if (G > 1 && s->barrier_epoch[i] >= 0 && s->barrier_epoch[i] < nst) dp->steps[s->barrier_epoch[i]].sync_after = 1;
     /* counting sort of messages by step, stable in message order */
     for (i = 0; i < s->nmsg; ++i) cnt[s->msgs[i].step + 1]++;
     for (st = 0; st < nst; ++st) cnt[st + 1] += cnt[st];

@@ -64,7 +64,7 @@ struct xg_regions {
 };
 
 struct StepR {
-    int pre_b, pre_n, post_b, post_n, p2p_b, p2p_n;
+    int pre_b, pre_n, post_b, post_n, p2p_b, p2p_n, sync_after;
     int64_t pre_bytes, post_bytes;   // bytes copied by each launch (read once + written once)
 };
 
@@ -158,12 +158,15 @@ extern "C" int xg_device_sync(xg_ctx *c)
 
 extern "C" int xg_allreduce_max(xg_ctx *c, double *vals, int n)
 {
-    if (n < 0 || n > 64) return XG_EARG;
+    if (n < 0) return XG_EARG;
     if (c->nranks == 1 || n == 0) return XG_OK;
-    HIPCHK(hipMemcpyAsync(c->d_red, vals, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
-    NCCLCHK(ncclAllReduce(c->d_red, c->d_red, n, ncclFloat64, ncclMax, c->comm, c->stream));
-    HIPCHK(hipMemcpyAsync(vals, c->d_red, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    double *buf = c->d_red;
+    if (n > 64) HIPCHK(hipMalloc(&buf, sizeof(double) * n));
+    HIPCHK(hipMemcpyAsync(buf, vals, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(ncclAllReduce(buf, buf, n, ncclFloat64, ncclMax, c->comm, c->stream));
+    HIPCHK(hipMemcpyAsync(vals, buf, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (buf != c->d_red) HIPCHK(hipFree(buf));
     return XG_OK;
 }
 
@@ -376,6 +379,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             p->p2p.push_back(o);
         }
         st.p2p_n = (int)p->p2p.size() - st.p2p_b;
+        st.sync_after = sp.sync_after && c->nranks > 1;
     }
     p->npieces = (int)pieces.size();
     p->d_pieces = nullptr;
@@ -455,6 +459,8 @@ static int enqueue_step(xg_plan *p, int s)
         NCCLCHK(ncclGroupEnd());
     }
     if (st.post_n && (rc = timed(st.post_b, st.post_n, st.post_bytes))) return rc;
+    if (st.sync_after)   /* in-loop MPI_Barrier: every GPU finishes this step before any goes on */
+        NCCLCHK(ncclAllReduce(c->d_red, c->d_red, 1, ncclFloat64, ncclMax, c->comm, c->stream));
     return XG_OK;
 }
 

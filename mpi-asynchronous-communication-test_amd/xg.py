@@ -44,7 +44,8 @@ class P2P(C.Structure):
 
 class StepPlan(C.Structure):
     _fields_ = [("pre_begin", C.c_int32), ("pre_count", C.c_int32), ("p2p_begin", C.c_int32),
-                ("p2p_count", C.c_int32), ("post_begin", C.c_int32), ("post_count", C.c_int32)]
+                ("p2p_count", C.c_int32), ("post_begin", C.c_int32), ("post_count", C.c_int32),
+                ("sync_after", C.c_int32), ("pad", C.c_int32)]
 
 
 class DevPlan(C.Structure):
@@ -91,7 +92,7 @@ def host():
         h.xg_method_direction.argtypes = [C.c_int]
         h.xg_sched_build.restype = C.c_void_p
         h.xg_sched_build.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_int),
-                                     C.c_int, C.c_int64, C.c_char_p, C.c_size_t]
+                                     C.c_int, C.c_int, C.c_int, C.c_int64, C.c_char_p, C.c_size_t]
         h.xg_sched_free.argtypes = [C.c_void_p]
         for fn in ("xg_sched_nmsg", "xg_sched_nsteps", "xg_sched_direction", "xg_sched_procs"):
             getattr(h, fn).argtypes = [C.c_void_p]
@@ -101,6 +102,11 @@ def host():
         h.xg_sched_trace.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_size_t]
         h.xg_sched_rank_timer.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
                                           C.POINTER(C.c_double), C.POINTER(Timer)]
+        h.xg_sched_rank_rep_timers.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                               C.POINTER(C.c_double), C.POINTER(Timer)]
+        h.xg_sched_ntimes.argtypes = [C.c_void_p]
+        h.xg_sched_barrier_epochs.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+        h.xg_save_all_timing.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(Timer), C.c_char_p]
         h.xg_block_range.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         h.xg_gpu_of.argtypes = [C.c_int, C.c_int, C.c_int]
         for fn in ("xg_send_offset", "xg_recv_offset"):
@@ -134,7 +140,7 @@ class Schedule:
     """One method run (all -k repetitions), compiled to device-wide steps."""
 
     def __init__(self, method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes=1,
-                 eager_limit=MPICH_EAGER_LIMIT):
+                 eager_limit=MPICH_EAGER_LIMIT, proc_node=1, barrier_type=0):
         h = host()
         self.method, self.P, self.A, self.d, self.c = method, procs, cb_nodes, data_size, comm_size
         self.rank_list = list(rank_list)
@@ -142,7 +148,7 @@ class Schedule:
         err = C.create_string_buffer(512)
         rl = (C.c_int * cb_nodes)(*rank_list)
         self._h = h.xg_sched_build(method, procs, cb_nodes, data_size, comm_size, rl, ntimes,
-                                   eager_limit, err, 512)
+                                   proc_node, barrier_type, eager_limit, err, 512)
         if not self._h:
             raise XGError(err.value.decode())
         self.nsteps = h.xg_sched_nsteps(self._h)
@@ -175,6 +181,21 @@ class Schedule:
         if host().xg_sched_rank_timer(self._h, ngpus, rank, nd, npost, C.byref(t)) != 0:
             raise XGError("xg_sched_rank_timer: bad rank/ngpus")
         return t
+
+    def rank_rep_timers(self, rank, step_done, step_post=None, ngpus=1):
+        """timers[m] of every repetition (m13)."""
+        nd = (C.c_double * max(1, len(step_done)))(*step_done)
+        npost = (C.c_double * max(1, len(step_post)))(*step_post) if step_post is not None else None
+        reps = (Timer * max(1, self.ntimes))()
+        if host().xg_sched_rank_rep_timers(self._h, ngpus, rank, nd, npost, reps) != 0:
+            raise XGError("xg_sched_rank_rep_timers: bad rank/ngpus")
+        return list(reps)[:self.ntimes]
+
+    def barrier_epochs(self):
+        n = host().xg_sched_barrier_epochs(self._h, None)
+        out = (C.c_int32 * max(1, n))()
+        host().xg_sched_barrier_epochs(self._h, out)
+        return list(out)[:n]
 
     def gpu_of(self, ngpus, rank):
         return host().xg_gpu_of(self.P, ngpus, rank)
@@ -222,6 +243,7 @@ class DevicePlanView:
         self.p2p = [(o.peer, o.is_send, o.buf, o.off, o.len) for o in p.p2p[:p.np2p]]
         self.steps = [(s.pre_begin, s.pre_count, s.p2p_begin, s.p2p_count, s.post_begin, s.post_count)
                       for s in p.steps[:p.nsteps]]
+        self.sync_after = [s.sync_after for s in p.steps[:p.nsteps]]
         self.local_bytes = p.local_bytes
         self.remote_send_bytes = p.remote_send_bytes
         self.remote_recv_bytes = p.remote_recv_bytes

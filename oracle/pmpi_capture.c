@@ -7,9 +7,11 @@
  * records, per MPI rank, every point-to-point call the reference makes on the
  * hot path (methods 1-12) plus a checksum of every received segment:
  *
- *   B                         MPI_Barrier            (e.g. mpi_test.c:1762)
- *   S <idx> <peer> <cnt> <tag>  send post            (Issend :1776, Send :1099, Sendrecv :1706)
- *   R <idx> <peer> <cnt> <tag> <addr>  recv post     (Irecv :1772, Recv :982, Sendrecv :1706)
+ *   B                         MPI_Barrier            (e.g. mpi_test.c:1762, :863, :1188)
+ *   S <idx> <peer> <cnt> <tag> <comm> <mode>  send post; mode n = Issend (:1776),
+ *                             i = Isend (:771, :1283), b = Send (:1099), r = Sendrecv (:1706)
+ *   R <idx> <peer> <cnt> <tag> <comm> <addr>  recv post (Irecv :1772, Recv :982, Sendrecv :1706)
+ *                             comm: 0 = MPI_COMM_WORLD, k = k-th other communicator seen
  *   W <idx> <idx> ...         one completion point   (Waitall :1781, blocking calls)
  *   D <src> <cnt> <addr> <chk>  bytes received       (checked when the wait returns)
  *   A <recvcounts...>         MPI_Alltoallw           (:627, :637, :912, :922)
@@ -28,6 +30,18 @@
 #include <string.h>
 
 static FILE *cap_fp;
+static MPI_Comm comms[16];
+static int ncomms;
+
+static int comm_id(MPI_Comm c)
+{
+    int i;
+    if (c == MPI_COMM_WORLD) return 0;
+    for (i = 0; i < ncomms; ++i)
+        if (comms[i] == c) return i + 1;
+    if (ncomms < 16) comms[ncomms++] = c;
+    return ncomms;
+}
 static int cap_rank = -1;
 static long post_idx;
 
@@ -95,6 +109,7 @@ static void drop_live(int i) { live[i] = live[--nlive]; }
 
 static void emit_data(int src, int count, const void *buf)
 {
+    if (count <= 0) return;   /* zero-byte messages carry no data (pairwise m9/m10, m18 signals) */
     fprintf(cap_fp, "D %d %d %p %016llx\n", src, count, buf,
             (unsigned long long)chk64((const unsigned char *)buf, count));
 }
@@ -123,7 +138,7 @@ static int isend_common(int sync, const void *buf, int count, MPI_Datatype dt, i
     cap_open();
     rc = sync ? PMPI_Issend(buf, count, dt, dest, tag, comm, req)
               : PMPI_Isend(buf, count, dt, dest, tag, comm, req);
-    fprintf(cap_fp, "S %ld %d %d %d\n", post_idx, dest, count, tag);
+    fprintf(cap_fp, "S %ld %d %d %d %d %c\n", post_idx, dest, count, tag, comm_id(comm), sync ? 'n' : 'i');
     add_live(*req, post_idx, 0, dest, count, buf);
     post_idx++;
     return rc;
@@ -140,7 +155,7 @@ int MPI_Irecv(void *buf, int count, MPI_Datatype dt, int src, int tag, MPI_Comm 
     int rc;
     cap_open();
     rc = PMPI_Irecv(buf, count, dt, src, tag, comm, req);
-    fprintf(cap_fp, "R %ld %d %d %d %p\n", post_idx, src, count, tag, buf);
+    fprintf(cap_fp, "R %ld %d %d %d %d %p\n", post_idx, src, count, tag, comm_id(comm), buf);
     add_live(*req, post_idx, 1, src, count, buf);
     post_idx++;
     return rc;
@@ -186,7 +201,7 @@ int MPI_Send(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI
 {
     int rc;
     cap_open();
-    fprintf(cap_fp, "S %ld %d %d %d\nW %ld\n", post_idx, dest, count, tag, post_idx);
+    fprintf(cap_fp, "S %ld %d %d %d %d b\nW %ld\n", post_idx, dest, count, tag, comm_id(comm), post_idx);
     post_idx++;
     rc = PMPI_Send(buf, count, dt, dest, tag, comm);
     return rc;
@@ -196,7 +211,7 @@ int MPI_Recv(void *buf, int count, MPI_Datatype dt, int src, int tag, MPI_Comm c
 {
     int rc;
     cap_open();
-    fprintf(cap_fp, "R %ld %d %d %d %p\nW %ld\n", post_idx, src, count, tag, buf, post_idx);
+    fprintf(cap_fp, "R %ld %d %d %d %d %p\nW %ld\n", post_idx, src, count, tag, comm_id(comm), buf, post_idx);
     post_idx++;
     rc = PMPI_Recv(buf, count, dt, src, tag, comm, st);
     emit_data(src, count, buf);
@@ -209,8 +224,8 @@ int MPI_Sendrecv(const void *sbuf, int scount, MPI_Datatype sdt, int dest, int s
 {
     int rc;
     cap_open();
-    fprintf(cap_fp, "S %ld %d %d %d\nR %ld %d %d %d %p\nW %ld %ld\n",
-            post_idx, dest, scount, stag, post_idx + 1, src, rcount, rtag, rbuf, post_idx, post_idx + 1);
+    fprintf(cap_fp, "S %ld %d %d %d %d r\nR %ld %d %d %d %d %p\nW %ld %ld\n", post_idx, dest, scount, stag,
+            comm_id(comm), post_idx + 1, src, rcount, rtag, comm_id(comm), rbuf, post_idx, post_idx + 1);
     post_idx += 2;
     rc = PMPI_Sendrecv(sbuf, scount, sdt, dest, stag, rbuf, rcount, rdt, src, rtag, comm, st);
     if (rbuf && rcount > 0) emit_data(src, rcount, rbuf);

@@ -9,7 +9,8 @@ What it restates (every function cites the reference line it follows):
   * segment fingerprint             MAP_DATA / fill_buffer   mpi_test.c:23, :71-77
   * buffer layouts                  prepare_*_data           mpi_test.c:94-133, :162-202
   * alltoallw counts/displacements  *_alltoall_translate     mpi_test.c:233-302
-  * the per-rank MPI programs of methods 1..12                mpi_test.c:421-1950
+  * the per-rank MPI programs of methods 1..14, 17..20         mpi_test.c:421-1950
+    (15/16 = TAM via lustre_driver_test.c are not part of this build)
   * MPI point-to-point matching (non-overtaking per (src,dst,tag)) and
     collective matching for MPI_Alltoallw, executed with byte copies.
 
@@ -19,24 +20,34 @@ from the reference binary (tests/golden/make_golden.py); tests/test_oracle.py
 checks this module against every one of them.
 
 Program ops (one list per rank, in program order):
-  ('B',)                               MPI_Barrier before the timed region
-  ('s', peer, cnt, seg, blocking)      send post (Issend: blocking=False; Send / Sendrecv half: True)
-  ('r', peer, cnt, slot)               recv post (Irecv / Recv / Sendrecv half)
+  ('B',)                               MPI_Barrier (collective; before or inside the timed region)
+  ('s', peer, cnt, seg, eager_ok, comm, tag, isend)
+                                       send post.  Issend: eager_ok False; Send / Sendrecv half /
+                                       Isend: eager_ok True (complete locally when cnt <= eager
+                                       limit).  comm 0 = MPI_COMM_WORLD; tag None = rank + peer.
+  ('r', peer, cnt, slot, comm, tag)    recv post (Irecv / Recv / Sendrecv half)
   ('w', [post indices])                one completion point (Waitall / blocking call)
   ('A', [(peer,cnt,seg)], [(peer,cnt,slot)])   MPI_Alltoallw (posts + completion)
-  ('c', seg, slot, cnt)                self memcpy (mpi_test.c:1473, :1646, :1714)
-  ('t', field, +1|-1)                  timer bracket: field in post|send|recv|total
+  ('c', seg, slot, cnt)                self memcpy (mpi_test.c:1473, :1646, :1714, :1285, :1398)
+  ('t', field, +1|-1)                  timer bracket: field in post|send|recv|barrier|total
+  ('rep', m) ('mark', reg) ('delta', tgt, field, reg, mode) ('acc', dst, dfield, src, sfield)
+  ('copyt', dst, dfield, src, sfield) ('zero', tgt, field)
+                                       per-repetition timers of m13 (timers[m], :829-874):
+                                       tgt 'G' = the method Timer, 'R' = timers[m]
 Post indices count 's' and 'r' ops (and the posts of an 'A') in program order.
 """
 import numpy as np
 
-A2M_METHODS = (1, 3, 6, 7, 8, 9, 12)
-M2A_METHODS = (2, 4, 5, 10, 11)
-LABELS = {  # mpi_test.c:2186 ... :2271
+A2M_METHODS = (1, 3, 6, 7, 8, 9, 12, 13, 17, 18, 19, 20)
+M2A_METHODS = (2, 4, 5, 10, 11, 14)
+METHODS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 17, 18, 19, 20)
+LABELS = {  # mpi_test.c:2186 ... :2337
     1: "All to many", 2: "Many to all", 3: "All to many balanced", 4: "Many to all balanced",
     5: "Many to all benchmark", 6: "All to many sync", 7: "All to many half sync",
     8: "All to many benchmark", 9: "All to many pairwise", 10: "Many to all pairwise",
-    11: "Many to all half sync", 12: "All to many half sync 2",
+    11: "Many to all half sync", 12: "All to many half sync 2", 13: "All to many scattered",
+    14: "Many to all scattered", 17: "All to many node robin", 18: "All to many balanced control",
+    19: "All to many scattered isend", 20: "All to many balanced presend",
 }
 
 
@@ -154,13 +165,13 @@ class _Prog:
         self.ops = []
         self.nposts = 0
 
-    def s(self, peer, cnt, seg, blocking=False):
-        self.ops.append(("s", peer, cnt, seg, blocking))
+    def s(self, peer, cnt, seg, eager_ok=False, comm=0, tag=None, isend=False):
+        self.ops.append(("s", peer, cnt, seg, eager_ok or isend, comm, tag, isend))
         self.nposts += 1
         return self.nposts - 1
 
-    def r(self, peer, cnt, slot):
-        self.ops.append(("r", peer, cnt, slot))
+    def r(self, peer, cnt, slot, comm=0, tag=None):
+        self.ops.append(("r", peer, cnt, slot, comm, tag))
         self.nposts += 1
         return self.nposts - 1
 
@@ -170,8 +181,8 @@ class _Prog:
     def send(self, peer, cnt, seg):          # blocking MPI_Send
         self.w([self.s(peer, cnt, seg, True)])
 
-    def recv(self, peer, cnt, slot):         # blocking MPI_Recv
-        self.w([self.r(peer, cnt, slot)])
+    def recv(self, peer, cnt, slot, comm=0, tag=None):   # blocking MPI_Recv
+        self.w([self.r(peer, cnt, slot, comm, tag)])
 
     def sendrecv(self, dst, scnt, seg, src, rcnt, slot):   # MPI_Sendrecv
         a = self.s(dst, scnt, seg, True)
@@ -180,6 +191,9 @@ class _Prog:
 
     def t(self, field, sign):
         self.ops.append(("t", field, sign))
+
+    def op(self, *args):
+        self.ops.append(tuple(args))
 
     def alltoallw(self, sends, recvs):
         self.ops.append(("A", list(sends), list(recvs)))
@@ -198,7 +212,7 @@ def _in_window(rank, temp, cs, P):
     return rank >= temp or rank < (temp + cs) % P
 
 
-def programs(method, P, A, d, c, rank_list, ntimes):
+def programs(method, P, A, d, c, rank_list, ntimes, proc_node=1, barrier_type=0):
     """Per-rank op lists of method `method` exactly as the reference issues them."""
     aggidx = {g: i for i, g in enumerate(rank_list)}
     progs = []
@@ -209,7 +223,11 @@ def programs(method, P, A, d, c, rank_list, ntimes):
         p = _Prog()
         p.ops.append(("B",))
         p.t("total", +1)
-        _METHODS[method](p, rank, isagg, myindex, P, A, d, c, rank_list, ntimes)
+        fn = _METHODS[method]
+        if method in (13, 17):
+            fn(p, rank, isagg, myindex, P, A, d, c, rank_list, ntimes, proc_node, barrier_type)
+        else:
+            fn(p, rank, isagg, myindex, P, A, d, c, rank_list, ntimes)
         p.t("total", -1)
         progs.append(p.ops)
     return progs
@@ -505,10 +523,239 @@ def _pairwise(translate):
     return run
 
 
+def _scattered_block(P, c):
+    # :740-750 / :815-825 / :674-684
+    if c > P:
+        c = P
+    return c if c != 0 else P
+
+
+def _m13(p, rank, isagg, myindex, P, A, d, c, rl, ntimes, proc_node=1, barrier_type=0):
+    """all_to_many_scattered, mpi_test.c:797-882 (barrier type -b, per-repetition timers[m])."""
+    sc, sd, rc, rd = _a2m_translate(rank, isagg, P, A, d, rl)
+    bblock = _scattered_block(P, c)
+    for m in range(ntimes):
+        p.op("rep", m)
+        p.op("mark", "T2")
+        p.op("zero", "R", "barrier")
+        for ii in range(0, P, bblock):
+            ss = min(P - ii, bblock)
+            idx = []
+            p.op("mark", "S")
+            for i in range(ss):
+                dst = (rank + i + ii) % P
+                if rc[dst]:
+                    idx.append(p.r(dst, rc[dst], rd[dst] // d if d else 0))
+            for i in range(ss):
+                dst = (rank - i - ii + P) % P
+                if sc[dst]:
+                    idx.append(p.s(dst, sc[dst], sd[dst] // d if d else 0))
+            p.op("delta", "R", "post", "S", "set")
+            p.op("acc", "G", "post", "R", "post")
+            if idx:
+                p.op("mark", "S")
+                p.w(idx)
+                p.op("delta", "R", "recv", "S", "set")
+                p.op("acc", "G", "recv", "R", "recv")
+                if not isagg:
+                    p.op("acc", "G", "send", "R", "recv")
+                    p.op("copyt", "R", "send", "R", "recv")
+            if barrier_type == 2:
+                p.op("mark", "S")
+                p.ops.append(("B",))
+                p.op("delta", "R", "barrier", "S", "add")
+                p.op("acc", "G", "barrier", "R", "barrier")
+        p.op("delta", "R", "total", "T2", "set")
+        if barrier_type == 1:
+            p.op("mark", "S")
+            p.ops.append(("B",))
+            p.op("delta", "R", "barrier", "S", "set")
+            p.op("acc", "G", "barrier", "R", "barrier")
+
+
+def _m14(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):
+    """many_to_all_scattered, mpi_test.c:656-720."""
+    sc, sd, rc, rd = _m2a_translate(rank, isagg, P, A, d, rl)
+    bblock = _scattered_block(P, c)
+    for _ in range(ntimes):
+        for ii in range(0, P, bblock):
+            ss = min(P - ii, bblock)
+            idx = []
+            p.t("post", +1)
+            for i in range(ss):
+                dst = (rank + i + ii) % P
+                if rc[dst]:
+                    idx.append(p.r(dst, rc[dst], rd[dst] // d if d else 0))
+            for i in range(ss):
+                dst = (rank - i - ii + P) % P
+                if sc[dst]:
+                    idx.append(p.s(dst, sc[dst], sd[dst] // d if d else 0))
+            p.t("post", -1)
+            if idx:
+                p.t("recv", +1); p.w(idx); p.t("recv", -1)
+
+
+def node_robin_map(rank, proc_node, P):
+    """node_robin_map, mpi_test.c:1116-1133 -> (map, rank_index)."""
+    mp, count, j, rank_index = [0] * P, 0, 0, 0
+    for i in range(P):
+        mp[i] = count
+        if count == rank:
+            rank_index = i
+        count += proc_node
+        if count >= P:
+            j += 1
+            count = j
+    return mp, rank_index
+
+
+def _m17(p, rank, isagg, myindex, P, A, d, c, rl, ntimes, proc_node=1, barrier_type=0):
+    """all_to_many_node_robin, mpi_test.c:1135-1227 (barrier inside every round)."""
+    mp, rank_index = node_robin_map(rank, proc_node, P)
+    if c > P:
+        c = P
+    bblock = c
+    ceiling, floor, remainder = _split(P, A)
+    send_start = _send_start(rank_index, ceiling, floor, remainder)
+    for _ in range(ntimes):
+        cs = bblock
+        k = 0
+        while k < P:
+            if P - k < cs:
+                cs = P - k
+            idx = []
+            p.t("post", +1)
+            if isagg:
+                for i in range(cs):
+                    temp = mp[_window_start(myindex, k + i, ceiling, floor, remainder) % P]
+                    idx.append(p.r(temp, d, temp))
+            p.ops.append(("B",))
+            for _x in range(A):
+                temp = _window_start(send_start, k, ceiling, floor, remainder)
+                if not _in_window(rank_index, temp, cs, P):
+                    break
+                idx.append(p.s(rl[send_start], d, send_start))
+                send_start = (send_start - 1 + A) % A
+            p.t("post", -1)
+            if idx:
+                fields = ("recv",) if isagg else ("recv", "send")
+                for f in fields:
+                    p.t(f, +1)
+                p.w(idx)
+                for f in fields:
+                    p.t(f, -1)
+            k += cs
+
+
+def _m18(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):
+    """all_to_many_balanced_control, mpi_test.c:1229-1336 (0-byte go-signals on a dup'd comm)."""
+    if c > P:
+        c = P
+    bblock = c
+    ceiling, floor, remainder = _split(P, A)
+    send_start = _send_start(rank, ceiling, floor, remainder)
+    for _ in range(ntimes):
+        cs = bblock
+        k = 0
+        while k < P:
+            if P - k < cs:
+                cs = P - k
+            idx = []
+            p.t("post", +1)
+            if isagg:
+                for i in range(cs):
+                    temp = _window_start(myindex, k + i, ceiling, floor, remainder) % P
+                    if temp != rank:
+                        idx.append(p.r(temp, d, temp))
+                        idx.append(p.s(temp, 0, -1, comm=1, tag=rank + temp * 100, isend=True))
+                    else:
+                        p.ops.append(("c", myindex, temp, d))
+            for _x in range(A):
+                temp = _window_start(send_start, k, ceiling, floor, remainder)
+                if not _in_window(rank, temp, cs, P):
+                    break
+                if rl[send_start] != rank:
+                    p.recv(rl[send_start], 0, -1, comm=1, tag=rank * 100 + rl[send_start])
+                    idx.append(p.s(rl[send_start], d, send_start))
+                send_start = (send_start - 1 + A) % A
+            p.t("post", -1)
+            if idx:
+                fields = ("recv",) if isagg else ("recv", "send")
+                for f in fields:
+                    p.t(f, +1)
+                p.w(idx)
+                for f in fields:
+                    p.t(f, -1)
+            k += cs
+
+
+def _m19(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):
+    """all_to_many_scattered_isend, mpi_test.c:722-795 (MPI_Isend; barrier before the total stop)."""
+    sc, sd, rc, rd = _a2m_translate(rank, isagg, P, A, d, rl)
+    bblock = _scattered_block(P, c)
+    for _ in range(ntimes):
+        for ii in range(0, P, bblock):
+            ss = min(P - ii, bblock)
+            idx = []
+            for i in range(ss):
+                dst = (rank + i + ii) % P
+                if rc[dst]:
+                    idx.append(p.r(dst, rc[dst], rd[dst] // d if d else 0))
+            for i in range(ss):
+                dst = (rank - i - ii + P) % P
+                if sc[dst]:
+                    if not isagg:
+                        p.t("post", +1)
+                    idx.append(p.s(dst, sc[dst], sd[dst] // d if d else 0, isend=True))
+                    if not isagg:
+                        p.t("post", -1)
+            if idx:
+                fields = ("recv",) if isagg else ("recv", "send")
+                for f in fields:
+                    p.t(f, +1)
+                p.w(idx)
+                for f in fields:
+                    p.t(f, -1)
+    p.ops.append(("B",))
+
+
+def _m20(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):
+    """all_to_many_balanced_pre_send, mpi_test.c:1338-1419."""
+    if c > P:
+        c = P
+    bblock = c
+    ceiling, floor, remainder = _split(P, A)
+    send_start = _send_start(rank, ceiling, floor, remainder)
+    for _ in range(ntimes):
+        cs = bblock
+        sends = []
+        for k in range(A):
+            i = (send_start - k + A) % A
+            if rl[i] != rank:
+                sends.append(p.s(rl[i], d, i))
+        k = 0
+        while k < P:
+            if P - k < cs:
+                cs = P - k
+            idx = []
+            if isagg:
+                for i in range(cs):
+                    temp = _window_start(myindex, k + i, ceiling, floor, remainder) % P
+                    if temp != rank:
+                        p.t("post", +1); idx.append(p.r(temp, d, temp)); p.t("post", -1)
+                    else:
+                        p.ops.append(("c", myindex, temp, d))
+            if idx:
+                p.t("recv", +1); p.w(idx); p.t("recv", -1)
+            k += cs
+        if sends:
+            p.t("send", +1); p.w(sends); p.t("send", -1)
+
+
 _METHODS = {
     1: _m1, 2: _m2, 3: _m3, 4: _m4, 5: _alltoallw(_m2a_translate), 6: _m6, 7: _m7,
     8: _alltoallw(_a2m_translate), 9: _pairwise(_a2m_translate), 10: _pairwise(_m2a_translate),
-    11: _m11, 12: _m12,
+    11: _m11, 12: _m12, 13: _m13, 14: _m14, 17: _m17, 18: _m18, 19: _m19, 20: _m20,
 }
 
 
@@ -533,9 +780,12 @@ def trace_tokens(ops, ntimes_split=False):
         if k == "B":
             toks.append("B")
         elif k == "s":
-            toks.append("s%d:%d" % (op[1], op[2]))
+            kind = "i" if op[7] else "s"
+            toks.append(("%s%d:%d" % (kind, op[1], op[2])) if op[5] == 0 else
+                        ("%s%d:%d@%d#%d" % (kind, op[1], op[2], op[5], op[6])))
         elif k == "r":
-            toks.append("r%d:%d" % (op[1], op[2]))
+            toks.append(("r%d:%d" % (op[1], op[2])) if op[4] == 0 else
+                        ("r%d:%d@%d#%d" % (op[1], op[2], op[4], op[5])))
         elif k == "w":
             toks.append("w" + _idx_list(op[1]))
         elif k == "A":
@@ -547,8 +797,9 @@ def trace_tokens(ops, ntimes_split=False):
 def match(progs):
     """MPI matching.  Returns the message list [(src, seg, dst, slot, cnt, s_post, r_post)]
     where s_post / r_post are the post indices at the sender / receiver.
-    Point-to-point: FIFO per (src, dst, tag=src+dst) (MPI non-overtaking).
-    Alltoallw: the k-th call of every rank forms one collective."""
+    Point-to-point: FIFO per (communicator, src, dst, tag) (MPI non-overtaking); the
+    reference's tag is src+dst on MPI_COMM_WORLD.  Alltoallw: the k-th call of every
+    rank forms one collective."""
     from collections import defaultdict, deque
     sends = defaultdict(deque)
     recvs = defaultdict(deque)
@@ -558,9 +809,11 @@ def match(progs):
         post, ncoll = 0, 0
         for op in ops:
             if op[0] == "s":
-                sends[(r, op[1])].append((op[3], op[2], post)); post += 1
+                tag = r + op[1] if op[6] is None else op[6]
+                sends[(op[5], r, op[1], tag)].append((op[3], op[2], post)); post += 1
             elif op[0] == "r":
-                recvs[(op[1], r)].append((op[3], op[2], post)); post += 1
+                tag = r + op[1] if op[5] is None else op[5]
+                recvs[(op[4], op[1], r, tag)].append((op[3], op[2], post)); post += 1
             elif op[0] == "A":
                 for q, cnt, seg in op[1]:
                     coll_s[ncoll][(r, q)] = (cnt, seg, post); post += 1
@@ -575,7 +828,7 @@ def match(progs):
         for (seg, scnt, sp), (slot, rcnt, rp) in zip(s, rq):
             if scnt > rcnt:
                 raise RuntimeError("message truncated on %s" % (key,))
-            msgs.append((key[0], seg, key[1], slot, scnt, sp, rp))
+            msgs.append((key[1], seg, key[2], slot, scnt, sp, rp))
     for k in coll_s:
         if set(coll_s[k]) != set(coll_r[k]):
             raise RuntimeError("alltoallw count mismatch")
@@ -592,7 +845,7 @@ def execute(method, P, A, d, rank_list, progs, it, mode=0):
             if n else np.zeros(0, np.uint8) for r, (n, _) in lay.items()}
     recv = {r: np.full(m * d, 0xA5, np.uint8) for r, (_, m) in lay.items()}
     for src, seg, dst, slot, cnt, _sp, _rp in match(progs):
-        if cnt:
+        if cnt > 0:
             recv[dst][slot * d: slot * d + cnt] = send[src][seg * d: seg * d + cnt]
     for r, ops in enumerate(progs):
         for op in ops:
@@ -605,7 +858,7 @@ def execute(method, P, A, d, rank_list, progs, it, mode=0):
 MPICH_EAGER_LIMIT = 65424   # measured on the image's MPICH 3.3.2 ch3:nemesis
 
 
-def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT):
+def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT, info=None):
     """Earliest-step schedule of the matched messages: a message moves in step
     1 + max(step of every message completed by an earlier completion point of
     EITHER endpoint before it was posted).  Issend is synchronous; a blocking
@@ -621,7 +874,7 @@ def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT):
         post = 0
         for op in ops:
             if op[0] == "s":
-                if op[4] and op[2] <= eager_limit:
+                if op[4] and op[2] <= eager_limit:      # blocking send / Isend of <= eager limit
                     eager.add((r, post))
                 post += 1
             elif op[0] == "r":
@@ -638,6 +891,9 @@ def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT):
     epoch = [-1] * P
     npost = [0] * P
     done = [False] * P
+    nbar = [0] * P                  # barriers passed per rank
+    arrivals = {}                   # barrier k -> {rank: epoch at arrival}
+    barrier_epochs = []             # epoch at which barrier k completes (global)
     progress = True
     while progress:
         progress = False
@@ -646,7 +902,18 @@ def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT):
             while pc[r] < len(ops):
                 op = ops[pc[r]]
                 k = op[0]
-                if k in ("s", "r"):
+                if k == "B":        # collective: completes when every rank has arrived
+                    b = nbar[r]
+                    arr = arrivals.setdefault(b, {})
+                    arr[r] = epoch[r]
+                    if len(arr) < P:
+                        break
+                    e = max(arr.values())
+                    if len(barrier_epochs) <= b:
+                        barrier_epochs.append(e)
+                    epoch[r] = max(epoch[r], e)
+                    nbar[r] += 1
+                elif k in ("s", "r"):
                     post_epoch[(r, npost[r])] = epoch[r]
                     npost[r] += 1
                 elif k == "A":
@@ -670,7 +937,9 @@ def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT):
                 done[r] = True
     if not all(done):
         raise RuntimeError("deadlock: ranks %s blocked" % [r for r in range(P) if not done[r]])
-    nsteps = max([s for s in step if s is not None], default=-1) + 1
+    nsteps = max([s for s in step if s is not None] + [-1]) + 1
+    if info is not None:
+        info["barrier_epochs"] = barrier_epochs
     return step, nsteps
 
 

@@ -33,6 +33,9 @@ def golden_configs():
 def load_golden(name):
     p = os.path.join(GOLDEN, name)
     meta = json.load(open(os.path.join(p, "meta.json")))
+    opts = dict(zip(meta["args"].split()[0::2], meta["args"].split()[1::2]))
+    meta["barrier"] = int(opts.get("-b", 0))
+    meta["method_list"] = sorted(int(m) for m, v in meta["methods"].items() if v.get("status") == "ok")
     traces = {}
     for line in gzip.open(os.path.join(p, "trace.txt.gz"), "rt"):
         head, _, toks = line.rstrip("\n").partition(": ")

@@ -14,6 +14,8 @@ reduces the per-rank capture files to small fixtures:
                          (iter 0).  Tokens: B barrier, s<peer>:<cnt> send post,
                          r<peer>:<cnt> recv post, w<idx list> completion point, A alltoallw.
   <cfg>/report_m<N>.txt  the reference's stdout for -m N with every number masked '#'
+  methods: 1..14 and 17..20 (15/16 = TAM are not part of this build); tokens on a
+  communicator other than MPI_COMM_WORLD carry @<comm>#<tag>; MPI_Isend is 'i'.
   usage.txt              the reference's `-h` text (stderr), argv0 replaced by {argv0}
 
 Each method's captured data is checked against the direction table while
@@ -35,8 +37,9 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 MPIEXEC = "/opt/conda/bin/mpiexec"
 CAPTURE = os.path.join(REPO, "oracle", "_ref", "test_capture")
 
-A2M_METHODS = {1, 3, 6, 7, 8, 9, 12}
-M2A_METHODS = {2, 4, 5, 10, 11}
+A2M_METHODS = {1, 3, 6, 7, 8, 9, 12, 13, 17, 18, 19, 20}
+M2A_METHODS = {2, 4, 5, 10, 11, 14}
+METHODS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 17, 18, 19, 20]   # 15/16 (TAM): not built
 
 # name: (P, args)
 CONFIGS = {
@@ -50,6 +53,8 @@ CONFIGS = {
     "p32_a1_c4": (32, "-a 1 -d 128 -c 4 -i 1 -k 1"),
     "p8_a3_d1m_c2": (8, "-a 3 -d 1048576 -c 2 -i 1 -k 2"),
     "p20_a6_c7": (20, "-a 6 -d 24 -c 7 -i 1 -k 3"),
+    "p16_a5_c3_b1": (16, "-a 5 -d 96 -c 3 -b 1 -p 4 -i 1 -k 2"),
+    "p16_a5_c4_b2": (16, "-a 5 -d 96 -c 4 -b 2 -p 2 -i 1 -k 2"),
 }
 
 
@@ -63,6 +68,15 @@ def idx_list(idxs):
         out.append(str(idxs[i]) if i == j else "%d-%d" % (idxs[i], idxs[j]))
         i = j + 1
     return ",".join(out)
+
+
+def tok(kind, rank, peer, cnt, tag, comm, path, line):
+    """s/i/r<peer>:<cnt>; on MPI_COMM_WORLD the tag is always rank+peer (checked), on any
+    other communicator the token carries @<comm>#<tag>."""
+    if comm == 0:
+        assert tag == rank + peer, (path, line)
+        return "%s%d:%d" % (kind, peer, cnt)
+    return "%s%d:%d@%d#%d" % (kind, peer, cnt, comm, tag)
 
 
 def parse_cap(path, rank):
@@ -80,18 +94,17 @@ def parse_cap(path, rank):
         if k == "B":
             cur["tokens"].append("B")
         elif k == "S":
-            idx, peer, cnt, tag = map(int, f[1:5])
+            idx, peer, cnt, tag, comm = map(int, f[1:6])
             assert idx == expect_idx, (path, line)
-            assert tag == rank + peer, (path, line)
             expect_idx += 1
-            cur["tokens"].append("s%d:%d" % (peer, cnt))
+            cur["tokens"].append(tok("i" if f[6] == "i" else "s", rank, peer, cnt, tag, comm, path, line))
         elif k == "R":
-            idx, peer, cnt, tag = map(int, f[1:5])
+            idx, peer, cnt, tag, comm = map(int, f[1:6])
             assert idx == expect_idx, (path, line)
-            assert tag == rank + peer, (path, line)
             expect_idx += 1
-            cur["tokens"].append("r%d:%d" % (peer, cnt))
-            cur["recv"].append((peer, cnt, 0 if f[5] == "(nil)" else int(f[5], 16)))
+            cur["tokens"].append(tok("r", rank, peer, cnt, tag, comm, path, line))
+            if comm == 0:
+                cur["recv"].append((peer, cnt, 0 if f[6] == "(nil)" else int(f[6], 16)))
         elif k == "W":
             cur["tokens"].append("w" + idx_list(map(int, f[1:])))
         elif k == "A":
@@ -155,12 +168,19 @@ def gen_config(name, P, args, work):
             "methods": {}}
     tables = {"a2m": {}, "m2a": {}}
     traces = []
-    for m in range(1, 13):
+    for m in METHODS:
         stdout, caps = run_one(P, args, m, work)
         if caps is None:
             meta["methods"][str(m)] = {"status": "timeout"}
             print(name, "m%d TIMEOUT" % m, flush=True)
             continue
+        if m == 13:   # save_all_timing (mpi_test.c:2008-2066): file names and shapes
+            shapes = {}
+            for fn in sorted(os.listdir(work)):
+                if fn.endswith(".csv") and fn != "results.csv":
+                    rows = [r.split(",") for r in open(os.path.join(work, fn)).read().splitlines()]
+                    shapes[fn] = [len(rows), len(rows[0]) if rows else 0, [int(r[0]) for r in rows]]
+            meta["m13_timing_files"] = shapes
         hdr = stdout.splitlines()
         if "aggregators" not in meta:
             meta["header"] = hdr[0]

@@ -25,11 +25,14 @@ def test_plans_deliver_every_byte(xg, case, G):
     if G > P:
         pytest.skip("more GPUs than ranks")
     rl = xg.aggregator_list(P, A, pn, t)
-    for m in range(1, 13):
-        s = xg.Schedule(m, P, A, d, c, rl, ntimes=k)
+    for m in O.METHODS:
+        s = xg.Schedule(m, P, A, d, c, rl, ntimes=k, proc_node=pn, barrier_type=(m * G) % 3)
         for pack in (0, 1 << 20):
             views, regs = simulate(s, G, it=1, mode=1, pack=pack)
             check_recv(s, G, regs, it=1, mode=1)
+            if G > 1 and m in (13, 17, 19):     # in-loop barriers become device-side barriers
+                assert all(v.sync_after == views[0].sync_after for v in views)
+                assert sum(views[0].sync_after) >= 1 or m == 13
 
 
 def test_pack_decision_and_volume(xg):

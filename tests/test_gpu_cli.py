@@ -16,18 +16,23 @@ def _mask(text):
     return re.sub(r"\d+(\.\d+)?", "#", text)
 
 
-@pytest.mark.parametrize("cfg", ["readme_p32_a14", "p16_a5_d1000_c3"])
+@pytest.mark.parametrize("cfg", ["readme_p32_a14", "p16_a5_d1000_c3", "p16_a5_c4_b2"])
 def test_cli_report_matches_reference(pkg, cfg, tmp_path):
     meta, _, _ = load_golden(cfg)
     exe = os.path.join(os.path.dirname(pkg.__file__), "bin", "test")
-    for m in range(1, 13):
+    for m in meta["method_list"]:
         args = [exe, "--procs", str(meta["P"])] + meta["args"].split() + ["-m", str(m)]
         out = subprocess.run(args, capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
         assert out.returncode == 0, out.stderr[-2000:]
         golden = open(os.path.join(GOLDEN, cfg, "report_m%d.txt" % m)).read()
         assert _mask(out.stdout) == golden, (cfg, m, out.stdout[:500])
+        if m == 13:   # save_all_timing files: same names, shapes and rank column as the reference's
+            for fn, (nrows, ncols, ranks) in meta["m13_timing_files"].items():
+                rows = [r.split(",") for r in open(str(tmp_path / fn)).read().splitlines()]
+                assert len(rows) == nrows and all(len(r) == ncols for r in rows), fn
+                assert [int(r[0]) for r in rows] == ranks
     rows = open(str(tmp_path / "results.csv")).read().splitlines()
-    assert rows[0].count(",") == 14 and len(rows) == 1 + 12 * meta["iters"]
+    assert rows[0].count(",") == 14 and len(rows) == 1 + len(meta["method_list"]) * meta["iters"]
 
 
 def test_cli_verify_all_methods(pkg, tmp_path):
@@ -37,7 +42,7 @@ def test_cli_verify_all_methods(pkg, tmp_path):
                          capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert out.returncode == 0, out.stderr[-2000:]
     verdicts = re.findall(r"verify = (\w+)", out.stdout)
-    assert len(verdicts) == 24 and set(verdicts) == {"OK"}, out.stdout[-3000:]
+    assert len(verdicts) == 36 and set(verdicts) == {"OK"}, out.stdout[-3000:]
 
 
 def test_cli_refuses_reference_deadlock(pkg, tmp_path):

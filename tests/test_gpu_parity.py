@@ -22,7 +22,8 @@ def ctx(xg):
 def _run(xg, ctx, meta, method, it, mode=0, pack=1 << 20):
     P, A, d, c, k = meta["P"], meta["A"], meta["d"], meta["c"], meta["ntimes"]
     rl = xg.aggregator_list(P, A, meta["proc_node"], meta["type"])
-    s = xg.Schedule(method, P, A, d, c, rl, ntimes=k)
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=meta["proc_node"],
+                    barrier_type=meta.get("barrier", 0))
     run = xg.MethodRun(ctx, s, it=it, mode=mode, pack_max_seg=pack)
     done, post, wall = run.run_timed()
     chk, bad, first = run.verify()
@@ -32,8 +33,9 @@ def _run(xg, ctx, meta, method, it, mode=0, pack=1 << 20):
 @pytest.mark.parametrize("cfg", golden_configs())
 def test_golden_all_methods(xg, ctx, cfg):
     meta, _traces, data = load_golden(cfg)
-    for method in range(1, 13):
-        direction = "a2m" if method in (1, 3, 6, 7, 8, 9, 12) else "m2a"
+    import xg_oracle as O
+    for method in meta["method_list"]:
+        direction = O.direction(method)
         for it in range(meta["iters"]):
             s, run, _t, chk, bad, first = _run(xg, ctx, meta, method, it)
             try:
@@ -46,11 +48,11 @@ def test_golden_all_methods(xg, ctx, cfg):
                 run.close()
 
 
-@pytest.mark.parametrize("method", list(range(1, 13)))
+@pytest.mark.parametrize("method", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 17, 18, 19, 20])
 def test_strong_fingerprint(xg, ctx, method):
     """Collision-free fingerprint: catches misroutes MAP_DATA cannot (equal rank+seed)."""
     import xg_oracle as O
-    meta = {"P": 20, "A": 6, "d": 1000, "c": 7, "ntimes": 2, "proc_node": 1, "type": 1}
+    meta = {"P": 20, "A": 6, "d": 1000, "c": 7, "ntimes": 2, "proc_node": 3, "type": 1, "barrier": 2}
     s, run, _t, chk, bad, _f = _run(xg, ctx, meta, method, it=3, mode=1)
     try:
         exp = O.expected_recv(method, 20, 6, 1000, s.rank_list, 3, mode=1)

@@ -15,8 +15,9 @@ def test_traces_match_reference(xg, cfg):
     meta, traces, _ = load_golden(cfg)
     rl = xg.aggregator_list(meta["P"], meta["A"], meta["proc_node"], meta["type"])
     assert rl == meta["aggregators"]
-    for m in range(1, 13):
-        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, ntimes=meta["ntimes"])
+    for m in meta["method_list"]:
+        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, ntimes=meta["ntimes"],
+                        proc_node=meta["proc_node"], barrier_type=meta["barrier"])
         for r in range(meta["P"]):
             assert s.trace(r) == traces[(m, r)], (cfg, m, r)
 
@@ -25,11 +26,15 @@ def test_traces_match_reference(xg, cfg):
 def test_steps_match_oracle(xg, cfg):
     meta, _, _ = load_golden(cfg)
     rl = meta["aggregators"]
-    for m in range(1, 13):
-        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, ntimes=meta["ntimes"])
-        progs = O.programs(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, meta["ntimes"])
+    for m in meta["method_list"]:
+        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, ntimes=meta["ntimes"],
+                        proc_node=meta["proc_node"], barrier_type=meta["barrier"])
+        progs = O.programs(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, meta["ntimes"], meta["proc_node"],
+                           meta["barrier"])
         om = O.match(progs)
-        ost, ons = O.asap_steps(progs, om)
+        info = {}
+        ost, ons = O.asap_steps(progs, om, info=info)
+        assert s.barrier_epochs()[1:] == info["barrier_epochs"][1:], (cfg, m)
         mine = sorted((a, b, c, d, n, st) for a, b, c, d, n, st, fl in s.messages() if not fl & 1)
         ref = sorted((a, b, c, d, n, st) for (a, b, c, d, n, _sp, _rp), st in zip(om, ost))
         assert mine == ref, (cfg, m)
@@ -52,7 +57,7 @@ def test_aggregator_types(xg, t):
 def test_labels(xg):
     for m, lab in O.LABELS.items():
         assert xg.method_label(m) == lab
-    assert xg.method_label(13) is None
+    assert xg.method_label(15) == "All to many TAM" and xg.method_label(21) is None
 
 
 def test_timer_semantics(xg):

@@ -28,8 +28,9 @@ def test_traces_match_reference(cfg):
     meta, traces, _ = load_golden(cfg)
     P = meta["P"]
     rl = meta["aggregators"]
-    for m in range(1, 13):
-        progs = O.programs(m, P, meta["A"], meta["d"], meta["c"], rl, meta["ntimes"])
+    for m in meta["method_list"]:
+        progs = O.programs(m, P, meta["A"], meta["d"], meta["c"], rl, meta["ntimes"], meta["proc_node"],
+                           meta["barrier"])
         for r in range(P):
             assert O.trace_tokens(progs[r]) == traces[(m, r)], (cfg, m, r)
 
@@ -40,9 +41,9 @@ def test_bytes_match_reference(cfg):
     P, A, d = meta["P"], meta["A"], meta["d"]
     rl = meta["aggregators"]
     aggidx = {g: i for i, g in enumerate(rl)}
-    for m in range(1, 13):
+    for m in meta["method_list"]:
         direction = O.direction(m)
-        progs = O.programs(m, P, A, d, meta["c"], rl, meta["ntimes"])
+        progs = O.programs(m, P, A, d, meta["c"], rl, meta["ntimes"], meta["proc_node"], meta["barrier"])
         for it in range(meta["iters"]):
             recv = O.execute(m, P, A, d, rl, progs, it)
             exp = O.expected_recv(m, P, A, d, rl, it)
@@ -64,14 +65,15 @@ def test_uncaptured_pairs_are_self_copies(cfg):
     for m, info in meta["methods"].items():
         assert info["status"] == "ok" and info["layout_ok"]
         for it, src, dst in info["uncaptured_pairs"]:
-            assert int(m) in (3, 4, 6) and src == dst and dst in rl
+            assert int(m) in (3, 4, 6, 18, 20) and src == dst and dst in rl
 
 
 def test_asap_schedules_exist_for_goldens():
     for cfg in CONFIGS:
         meta, _, _ = load_golden(cfg)
-        for m in range(1, 13):
-            progs = O.programs(m, meta["P"], meta["A"], meta["d"], meta["c"], meta["aggregators"], meta["ntimes"])
+        for m in meta["method_list"]:
+            progs = O.programs(m, meta["P"], meta["A"], meta["d"], meta["c"], meta["aggregators"], meta["ntimes"],
+                               meta["proc_node"], meta["barrier"])
             steps, n = O.asap_steps(progs)
             assert all(s is not None and 0 <= s < n for s in steps)
 
