@@ -64,9 +64,10 @@ int xg_device_info(xg_ctx *ctx, char *name, size_t namelen, int *cus, size_t *hb
 double xg_now(void);                                           /* host seconds (monotonic) */
 
 /* ------------------------------------------------------------------ HBM regions */
-/* region_bytes: XG_BUF_SEND, XG_BUF_RECV, XG_BUF_STAGE_SEND, XG_BUF_STAGE_RECV
- * (xg_devplan.region_bytes).  The RECV region is poisoned (0xA5). */
-int xg_regions_alloc(xg_ctx *ctx, const int64_t region_bytes[4], xg_regions **out);
+/* region_bytes: XG_BUF_SEND, XG_BUF_RECV, XG_BUF_STAGE_SEND, XG_BUF_STAGE_RECV,
+ * XG_BUF_SCRATCH (xg_devplan.region_bytes).  The RECV region is poisoned (0xA5),
+ * SCRATCH is zeroed. */
+int xg_regions_alloc(xg_ctx *ctx, const int64_t region_bytes[XG_NBUF], xg_regions **out);
 int xg_regions_free(xg_regions *r);
 int xg_regions_poison(xg_regions *r);
 /* Device pointer of a region (for tests that read buffers back). */
@@ -164,11 +165,17 @@ XG_METHOD_DECL(xg_many_to_all_scattered);       /* m14 :656  */
 XG_METHOD_DECL(xg_all_to_many_balanced_control);/* m18 :1229 */
 XG_METHOD_DECL(xg_all_to_many_scattered_isend); /* m19 :722  */
 XG_METHOD_DECL(xg_all_to_many_balanced_pre_send);/* m20 :1338 */
-/* m13 / m17 take the reference's extra arguments (:797, :1135) */
+/* m13 / m17 / m15 / m16 take the reference's extra arguments (:797, :1135, :366, :313) */
 int xg_all_to_many_scattered(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
                              int barrier_type, xg_timer *timers, xg_timer *rep_timers, int iter, int ntimes);
 int xg_all_to_many_node_robin(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
                               int proc_node, xg_timer *timers, int iter, int ntimes);
+/* TAM: collective_write over static_node_assignment type 0 nodes of procs_node ranks
+ * (lustre_driver_test.c:944-1309, :359-429) */
+int xg_all_to_many_tam(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
+                       int procs_node, xg_timer *timers, int iter, int ntimes);       /* m15 :366 */
+int xg_many_to_all_tam(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
+                       int procs_node, xg_timer *timers, int iter, int ntimes);       /* m16 :313 */
 
 #ifdef __cplusplus
 }

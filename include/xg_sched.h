@@ -15,7 +15,9 @@
  * Interfaces replaced (reference file:line):
  *   xg_aggregator_list  <- create_aggregator_list        mpi_test.c:1952-2006
  *   xg_sched_build      <- the body of each method       mpi_test.c:421-1950
- *                          (+ *_alltoall_translate :233-302)
+ *                          (+ *_alltoall_translate :233-302; TAM m15/m16
+ *                          :313-419 -> collective_write +
+ *                          static_node_assignment, lustre_driver_test.c:359-429, :944-1309)
  *   xg_sched_rank_timer <- the MPI_Wtime brackets filling Timer   :25-31
  *   xg_summarize_results<- summarize_results             mpi_test.c:2068-2118
  */
@@ -44,18 +46,24 @@ enum { XG_A2M = 0, XG_M2A = 1 };
 /* One matched message (one d-byte segment; zero-length for the pairwise
  * methods' non-participating pairs).  sseg: index of the segment in the
  * sender's send buffer; dslot: index of the slot in the receiver's receive
- * buffer.  step: the device-wide step it moves in.  Self memcpy's of
- * m3/m4/m6 (mpi_test.c:1473, :1646, :1714) are messages with src == dst and
- * XG_MSG_COPY. */
+ * buffer (-1 when the message lives elsewhere: TAM aggregation buffers).
+ * sbuf/soff and dbuf/doff: where its bytes are read and written, as a region
+ * (XG_BUF_SEND / RECV / SCRATCH) and a byte offset inside that rank's part of
+ * it.  step: the device-wide step it moves in.  Self memcpy's of m3/m4/m6
+ * (mpi_test.c:1473, :1646, :1714) and of TAM (lustre_driver_test.c:1069-1285)
+ * are messages with src == dst and XG_MSG_COPY. */
 typedef struct {
     int32_t src, sseg, dst, dslot;
     int64_t len;
     int32_t step;
     int32_t flags;
+    int32_t sbuf, dbuf;       /* -1: host-side control data (XG_MSG_CTRL) */
+    int64_t soff, doff;
 } xg_msg;
 
 #define XG_MSG_COPY 1
 #define XG_MSG_COLL 2   /* part of an MPI_Alltoallw */
+#define XG_MSG_CTRL 4   /* TAM size exchange (MPI_INT arrays): orders steps, moves no device bytes */
 
 #define XG_MPICH_EAGER_LIMIT 65424   /* see DESIGN.md "blocking-send semantics" */
 
@@ -67,12 +75,14 @@ int xg_aggregator_list(int procs, int cb_nodes, int proc_node, int type, int *ra
 
 /* Label printed by summarize_results for a method (mpi_test.c:2186-2337), NULL if not 1..20. */
 const char *xg_method_label(int method);
-/* XG_A2M or XG_M2A; -1 for a method this build does not run (15, 16, or not 1..20). */
+/* XG_A2M or XG_M2A (the buffer layout of the method); -1 if not 1..20. */
 int xg_method_direction(int method);
 
-/* Build the schedule of one method run (all `ntimes` repetitions).  Methods
- * 1..14 and 17..20 (15/16 = TAM are not part of this build).  proc_node (-p)
- * matters to m17 only (node_robin_map, :1116-1133); barrier_type (-b) to m13.
+/* Build the schedule of one method run (all `ntimes` repetitions), methods
+ * 1..20.  proc_node (-p) matters to m17 (node_robin_map, :1116-1133) and to
+ * m15/m16 (processes per node of static_node_assignment type 0); barrier_type
+ * (-b) to m13.  The schedule of m15/m16 depends on the iteration (its tags
+ * carry +100*iter): build it with xg_sched_build_iter.
  * eager_limit: blocking sends and Isends of <= eager_limit bytes complete
  * locally (XG_MPICH_EAGER_LIMIT reproduces the reference on the image's MPICH).
  * Returns NULL and writes a message into err on failure, e.g. when the
@@ -80,6 +90,9 @@ int xg_method_direction(int method);
 xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size, int comm_size,
                          const int *rank_list, int ntimes, int proc_node, int barrier_type,
                          int64_t eager_limit, char *err, size_t errlen);
+xg_sched *xg_sched_build_iter(int method, int procs, int cb_nodes, int64_t data_size, int comm_size,
+                              const int *rank_list, int ntimes, int proc_node, int barrier_type,
+                              int64_t eager_limit, int iter, char *err, size_t errlen);
 void xg_sched_free(xg_sched *s);
 
 int xg_sched_nmsg(const xg_sched *s);
@@ -121,8 +134,11 @@ int xg_sched_barrier_epochs(const xg_sched *s, int32_t *out);
  *   XG_BUF_RECV  receive slots (a2m: each local aggregator rank P slots;
  *                m2a: each local rank A slots), rank-major
  *   XG_BUF_STAGE_SEND / XG_BUF_STAGE_RECV  packed per-peer staging
+ *   XG_BUF_SCRATCH  TAM aggregation buffers of its ranks (aggregate_buf,
+ *                send_buf2, recv_buf of collective_write), rank-major
  */
-enum { XG_BUF_SEND = 0, XG_BUF_RECV = 1, XG_BUF_STAGE_SEND = 2, XG_BUF_STAGE_RECV = 3 };
+enum { XG_BUF_SEND = 0, XG_BUF_RECV = 1, XG_BUF_STAGE_SEND = 2, XG_BUF_STAGE_RECV = 3, XG_BUF_SCRATCH = 4,
+       XG_NBUF = 5 };
 
 typedef struct {
     int64_t src_off, dst_off, len;
@@ -140,12 +156,15 @@ typedef struct {
     int32_t pre_begin, pre_count;     /* local copies + packs   (before the exchange) */
     int32_t p2p_begin, p2p_count;     /* grouped RCCL send/recv                       */
     int32_t post_begin, post_count;   /* unpacks                (after the exchange)  */
-    int32_t sync_after, pad;          /* 1: device-side barrier of all GPUs after it  */
+    int32_t sync_after;               /* 1: device-side barrier of all GPUs after it  */
+    int32_t stage_count;              /* the first stage_count pre copies (rank-local
+                                         memcpy's through SCRATCH) run in a launch of
+                                         their own, ahead of the other pre copies     */
 } xg_stepplan;
 
 typedef struct {
     int32_t gpu, ngpus, nsteps, pad;
-    int64_t region_bytes[4];          /* send, recv, stage_send, stage_recv           */
+    int64_t region_bytes[XG_NBUF];    /* send, recv, stage_send, stage_recv, scratch  */
     int32_t ncopy, np2p;
     xg_copy *copies;
     xg_p2p *p2p;
@@ -161,6 +180,7 @@ int xg_gpu_of(int procs, int ngpus, int rank);
  * on that GPU). */
 int64_t xg_send_offset(const xg_sched *s, int ngpus, int rank);
 int64_t xg_recv_offset(const xg_sched *s, int ngpus, int rank);
+int64_t xg_scratch_offset(const xg_sched *s, int ngpus, int rank);
 int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf);
 
 /* Build GPU g's share of every step.  pack_max_seg: per (step, peer), pack the

@@ -12,8 +12,7 @@
  *  - Launch: single process, or any launcher that sets RANK/WORLD_SIZE
  *    (torchrun --no-python) or PMI_RANK/PMI_SIZE (mpiexec).  The RCCL unique
  *    id is handed over through a file in $XG_RDZV_DIR (default /tmp).
- *  - -m 0 runs methods 1..14 and 17..20; 15/16 (TAM, lustre_driver_test.c)
- *    are not part of this build and are reported as skipped on stderr.
+ *  - -m 0 runs methods 1..20 like the reference, TAM (15/16) included.
  *  - Extra, opt-in: --verify (or XG_VERIFY=1) checks every received byte on
  *    the GPU and prints one extra "| <label> verify ..." line per method;
  *    --fingerprint strong switches to the collision-free fingerprint.
@@ -88,6 +87,8 @@ static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
     xg_run_opts_default(&ro);
     ro.verify = o->verify; ro.fingerprint = o->fp_mode; ro.eager_limit = o->eager; ro.pack_max_seg = o->pack_max;
     ro.proc_node = o->proc_node; ro.barrier_type = o->barrier_type;
+    if ((method == 15 || method == 16) && g == 0)   /* static_node_assignment, lustre_driver_test.c:361-363 */
+        printf("static node assignment for %d node ( %d processes per node) of type %d\n", o->P, o->proc_node, 0);
     if (method == 13 && o->ntimes > 0)
         ro.rep_timers = reps = (xg_timer *)calloc((size_t)(hi - lo + 1) * o->ntimes, sizeof(xg_timer));
     t_wall = xg_now();
@@ -213,9 +214,6 @@ int main(int argc, char **argv)
         printf("aggregators = ");
         for (i = 0; i < cb_nodes; ++i) printf("%d, ", o.rank_list[i]);
         printf("\n");
-        if (method == 15 || method == 16)
-            fprintf(stderr, "method %d (TAM, lustre_driver_test.c) is not part of this build\n", method);
-        if (method == 0) fprintf(stderr, "-m 0: running methods 1..14, 17..20 (15/16 = TAM are not part of this build)\n");
     }
     for (i = 0; i < iter; ++i) {   /* :2181-2343 */
         int m;

@@ -44,8 +44,8 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
     if (!opts) { xg_run_opts_default(&dflt); opts = &dflt; }
     if (!err) { err = ebuf; errlen = sizeof ebuf; }
     if (bad_slots) *bad_slots = 0;
-    s = xg_sched_build(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, opts->proc_node,
-                       opts->barrier_type, opts->eager_limit, err, errlen);
+    s = xg_sched_build_iter(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, opts->proc_node,
+                            opts->barrier_type, opts->eager_limit, iter, err, errlen);
     if (!s) return XG_ESCHED;
     dp = xg_devplan_build(s, G, g, opts->pack_max_seg);
     TRY(xg_regions_alloc(ctx, dp->region_bytes, &reg));
@@ -129,16 +129,37 @@ int xg_all_to_many_scattered(xg_ctx *ctx, int procs, int cb_nodes, int data_size
     return rc;
 }
 
-int xg_all_to_many_node_robin(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
-                              int proc_node, xg_timer *timers, int iter, int ntimes)
+static int run_with_proc_node(xg_ctx *ctx, int method, const char *name, int procs, int cb_nodes, int data_size,
+                              int *rank_list, int comm_size, int proc_node, xg_timer *timers, int iter, int ntimes)
 {
     xg_run_opts o;
     char e[512];
     int rc;
     xg_run_opts_default(&o);
     o.proc_node = proc_node;
-    rc = xg_run_method(ctx, 17, procs, cb_nodes, data_size, rank_list, comm_size, timers, iter, ntimes, &o, NULL,
+    rc = xg_run_method(ctx, method, procs, cb_nodes, data_size, rank_list, comm_size, timers, iter, ntimes, &o, NULL,
                        e, sizeof e);
-    if (rc == XG_ESCHED) fprintf(stderr, "xg_all_to_many_node_robin: %s\n", e);
+    if (rc == XG_ESCHED) fprintf(stderr, "%s: %s\n", name, e);
     return rc;
+}
+
+int xg_all_to_many_node_robin(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
+                              int proc_node, xg_timer *timers, int iter, int ntimes)
+{
+    return run_with_proc_node(ctx, 17, "xg_all_to_many_node_robin", procs, cb_nodes, data_size, rank_list, comm_size,
+                              proc_node, timers, iter, ntimes);
+}
+
+int xg_many_to_all_tam(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
+                       int procs_node, xg_timer *timers, int iter, int ntimes)
+{
+    return run_with_proc_node(ctx, 16, "xg_many_to_all_tam", procs, cb_nodes, data_size, rank_list, comm_size,
+                              procs_node, timers, iter, ntimes);
+}
+
+int xg_all_to_many_tam(xg_ctx *ctx, int procs, int cb_nodes, int data_size, int *rank_list, int comm_size,
+                       int procs_node, xg_timer *timers, int iter, int ntimes)
+{
+    return run_with_proc_node(ctx, 15, "xg_all_to_many_tam", procs, cb_nodes, data_size, rank_list, comm_size,
+                              procs_node, timers, iter, ntimes);
 }

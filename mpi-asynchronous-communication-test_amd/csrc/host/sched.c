@@ -1,5 +1,5 @@
 /*
- * sched.c -- per-rank program restatement of methods 1..12, MPI matching, and
+ * sched.c -- per-rank program restatement of methods 1..20, MPI matching, and
  * the step compiler that turns the reference's per-process MPI schedules into
  * device-wide steps.  Plain C99, no HIP.  See include/xg_sched.h.
  *
@@ -10,6 +10,9 @@
  *   Send/Recv     -> post + OP_WAIT             Sendrecv -> 2 posts + OP_WAIT
  *   Alltoallw     -> OP_A2AW + collective posts + OP_WAIT
  *   memcpy (self) -> OP_COPY                    MPI_Wtime brackets -> OP_TMARK
+ * Messages and copies name a logical buffer of their rank (LB_*): the method's
+ * send segments / receive slots, or TAM's aggregation buffers, which live in
+ * the SCRATCH region; TAM's MPI_INT size arrays are LB_CTRL (host data).
  */
 #include "xg_sched.h"
 
@@ -22,6 +25,10 @@ enum { OP_BARRIER, OP_SEND, OP_RECV, OP_WAIT, OP_A2AW, OP_COPY, OP_TMARK,
        OP_REP, OP_MARK, OP_DELTA, OP_ACC, OP_COPYT, OP_ZERO };
 /* timer fields in xg_timer order */
 enum { F_POST = 0, F_SEND = 1, F_RECV = 2, F_BARRIER = 3, F_TOTAL = 4, NF = 5 };
+/* logical buffers of a rank: send segments, receive slots, TAM's aggregate_buf /
+ * send_buf2 / recv_buf (lustre_driver_test.c:1054-1068, :1116, :1150), size arrays */
+enum { LB_SEND = 0, LB_RECV = 1, LB_AGG = 2, LB_SBUF2 = 3, LB_RBUF = 4, LB_CTRL = 5, NLB = 6 };
+#define NSCR 3                  /* LB_AGG .. LB_RBUF live in SCRATCH */
 /* per-repetition timer DSL (m13's timers[m], mpi_test.c:829-874): targets and registers */
 enum { TG_G = 0, TG_R = 1 };
 enum { REG_S = 0, REG_T2 = 1, NREG = 2 };
@@ -36,7 +43,9 @@ typedef struct {
     int32_t idx2;           /* copy: slot; DSL: source field / mode               */
     int32_t post;           /* send/recv: post index; copy: message index; barrier: ordinal */
     int32_t wbeg, wcnt;     /* wait: range in the rank's pool                 */
-    int64_t cnt;
+    int64_t cnt;            /* elements (bytes unless esz > 1)                */
+    int8_t sb, db, esz;     /* logical buffers (LB_*) of source / destination */
+    int64_t off, off2;      /* byte offsets in sb / db when idx < 0 (TAM)     */
 } op_t;
 
 typedef struct {
@@ -45,6 +54,7 @@ typedef struct {
     int32_t *pool;
     int npool, poolcap;
     int nposts, ncoll, nbarrier, rank;
+    int64_t hi[NLB];        /* extent of every logical buffer the program touches */
 } prog_t;
 
 struct xg_sched {
@@ -63,6 +73,9 @@ struct xg_sched {
     int nsteps;
     int pc_ngpus;                /* posts per (gpu, step), cached for one ngpus    */
     int32_t *post_count;
+    int iter;                    /* TAM tags carry +100*iter                        */
+    int64_t *scr_base;           /* [rank][NSCR] offset of AGG/SBUF2/RBUF in the rank's scratch */
+    int64_t *scr_size;           /* [rank] scratch bytes                            */
 };
 
 /* ------------------------------------------------------------------ helpers */
@@ -83,6 +96,7 @@ static op_t *push(prog_t *p)
     op_t *o = &p->ops[p->nops++];
     memset(o, 0, sizeof *o);
     o->coll = -1;
+    o->sb = LB_SEND; o->db = LB_RECV; o->esz = 1;
     return o;
 }
 
@@ -179,6 +193,40 @@ static void copy_op(prog_t *p, int seg, int slot, int64_t cnt)
     o->kind = OP_COPY; o->idx = seg; o->idx2 = slot; o->cnt = cnt; o->post = -1;
 }
 
+static void extent(prog_t *p, int lb, int64_t end)
+{
+    if (end > p->hi[lb]) p->hi[lb] = end;
+}
+
+/* TAM point-to-point on (logical buffer, byte offset); cnt elements of esz bytes */
+static int buf_send(prog_t *p, int peer, int64_t cnt, int esz, int lb, int64_t off, int tag, int isend)
+{
+    int q = post_send_ex(p, peer, cnt, -1, 0, isend, 0, tag);
+    op_t *o = &p->ops[p->nops - 1];
+    o->sb = (int8_t)lb; o->off = off; o->esz = (int8_t)esz;
+    extent(p, lb, off + cnt * esz);
+    return q;
+}
+
+static int buf_recv(prog_t *p, int peer, int64_t cnt, int esz, int lb, int64_t off, int tag)
+{
+    int q = post_recv_ex(p, peer, cnt, -1, 0, tag);
+    op_t *o = &p->ops[p->nops - 1];
+    o->db = (int8_t)lb; o->off2 = off; o->esz = (int8_t)esz;
+    extent(p, lb, off + cnt * esz);
+    return q;
+}
+
+/* memcpy inside one rank: n bytes from (sb, soff) to (db, doff) */
+static void buf_copy(prog_t *p, int sb, int64_t soff, int db, int64_t doff, int64_t n)
+{
+    op_t *o = push(p);
+    o->kind = OP_COPY; o->idx = o->idx2 = -1; o->cnt = n; o->post = -1;
+    o->sb = (int8_t)sb; o->off = soff; o->db = (int8_t)db; o->off2 = doff;
+    extent(p, sb, soff + n);
+    extent(p, db, doff + n);
+}
+
 /* growable int list for request indices */
 typedef struct { int *v; int n, cap; } ilist;
 static void il_push(ilist *l, int x)
@@ -192,6 +240,9 @@ typedef struct {
     int rank, isagg, myindex, P, A, c, ntimes, proc_node, barrier_type;
     int64_t d;
     const int *rl;
+    int method, iter;
+    const int *isagg_all;   /* [P] */
+    const int *lastidx;     /* [P] last i with rl[i] == rank, -1 if none */
 } ctx_t;
 
 /* ------------------------------------------------------------------ methods */
@@ -822,6 +873,171 @@ static void m20_balanced_presend(ctx_t *x)
     free(sends.v);
 }
 
+/* ------------------------------------------------------------------ TAM (m15 / m16) */
+/* send_size[w] / recv_size[w] that all_to_many_tam / many_to_all_tam hand to
+ * collective_write (mpi_test.c:393 / :343; counts of *_alltoall_translate) */
+static int64_t tam_ss(const ctx_t *x, int r, int w)     /* bytes r sends to w */
+{
+    return x->method == 15 ? (x->isagg_all[w] ? x->d : 0) : (x->isagg_all[r] ? x->d : 0);
+}
+
+static int64_t tam_rs(const ctx_t *x, int r, int w)     /* bytes r receives from w */
+{
+    return x->method == 15 ? (x->isagg_all[r] ? x->d : 0) : (x->isagg_all[w] ? x->d : 0);
+}
+
+/* send_buf[w] / recv_buf[w] byte offsets: a2m send_buf2[rank_list[i]] = segment i
+ * (:388-391), recv slot w; m2a send segment w, recv_buf2[rank_list[i]] = slot i (:335-339) */
+static int64_t tam_sloc(const ctx_t *x, int w) { return (x->method == 15 ? x->lastidx[w] : w) * x->d; }
+static int64_t tam_rloc(const ctx_t *x, int w) { return (x->method == 15 ? w : x->lastidx[w]) * x->d; }
+
+/* collective_write, lustre_driver_test.c:944-1309, with static_node_assignment
+ * type 0 (:404-427): nodes of proc_node consecutive ranks, proxy = first rank
+ * of a node.  Tags are a + b + 100 * iter (:1006, :1012, :1094, ...). */
+static void tam_collective_write(ctx_t *x)
+{
+    prog_t *p = x->p;
+    const int P = x->P, pn = x->proc_node, rank = x->rank, it100 = 100 * x->iter;
+    const int nrecvs = (P + pn - 1) / pn, lr0 = (rank / pn) * pn;
+    const int npn = rank >= (nrecvs - 1) * pn ? P - pn * (nrecvs - 1) : pn;
+    const int proxy = rank == lr0;
+    int64_t total_send = 0, total_recv = 0, node_msg = 0, node_recv = 0, local = 0, off, ptr;
+    int64_t *s_lens = NULL, *r_lens = NULL, *gsl = NULL, *grl = NULL, *ptrs = NULL;
+    int i, w, v;
+    ilist idx = {0};
+    for (w = 0; w < P; ++w) { total_send += tam_ss(x, rank, w); total_recv += tam_rs(x, rank, w); }
+    /* intra-node gather of the send/recv size arrays (:996-1018) */
+    if (proxy)
+        for (i = 1; i < npn; ++i)
+            il_push(&idx, buf_recv(p, lr0 + i, 2 * P, 4, LB_CTRL, (int64_t)i * P * 8, lr0 + i + lr0 + it100));
+    else
+        il_push(&idx, buf_send(p, lr0, 2 * P, 4, LB_CTRL, 0, rank + lr0 + it100, 1));
+    if (idx.n) { tstart(p, F_RECV); wait_list(p, idx.v, idx.n); tstop(p, F_RECV); }
+    /* proxy: exclusive prefix sums over (local process i, target w) (:1027-1041) */
+    if (proxy) {
+        s_lens = (int64_t *)xmalloc(sizeof(int64_t) * npn * P);
+        r_lens = (int64_t *)xmalloc(sizeof(int64_t) * npn * P);
+        for (i = 0; i < npn; ++i)
+            for (w = 0; w < P; ++w) {
+                s_lens[i * P + w] = node_msg; node_msg += tam_ss(x, lr0 + i, w);
+                r_lens[i * P + w] = node_recv; node_recv += tam_rs(x, lr0 + i, w);
+            }
+        local = node_msg > node_recv ? node_msg : node_recv;   /* local_buf = aggregate_buf + temp (:1054-1068) */
+    }
+    /* pack this process's messages into local_buf (:1069-1077) */
+    off = 0;
+    for (w = 0; w < P; ++w) {
+        int64_t n = tam_ss(x, rank, w);
+        if (n) { buf_copy(p, LB_SEND, tam_sloc(x, w), LB_AGG, local + off, n); off += n; }
+    }
+    /* messages to the local proxy (:1078-1107) */
+    idx.n = 0;
+    if (proxy) {
+        if (total_send) buf_copy(p, LB_AGG, local, LB_AGG, 0, total_send);
+        ptr = total_send;
+        for (i = 1; i < npn; ++i) {
+            int64_t t = i == npn - 1 ? node_msg - s_lens[i * P] : s_lens[(i + 1) * P] - s_lens[i * P];
+            if (t) il_push(&idx, buf_recv(p, lr0 + i, t, 1, LB_AGG, ptr, lr0 + i + lr0 + it100));
+            ptr += t;
+        }
+    } else if (total_send) {
+        il_push(&idx, buf_send(p, lr0, total_send, 1, LB_AGG, local, rank + lr0 + it100, 0));
+    }
+    if (idx.n) { tstart(p, F_RECV); wait_list(p, idx.v, idx.n); tstop(p, F_RECV); }
+    if (proxy) {
+        /* inter-node exchange among the proxies (:1116-1197) */
+        int64_t rb = 0, ptr2 = 0;
+        gsl = (int64_t *)calloc(nrecvs, sizeof(int64_t));
+        grl = (int64_t *)calloc(nrecvs, sizeof(int64_t));
+        ptrs = (int64_t *)calloc(nrecvs, sizeof(int64_t));
+        idx.n = 0;
+        ptr = 0;
+        for (i = 0; i < nrecvs; ++i) {
+            int64_t temp2 = 0;
+            int vhi = (i + 1) * pn < P ? (i + 1) * pn : P;
+            for (v = i * pn; v < vhi; ++v)
+                for (w = 0; w < npn; ++w) {
+                    int t = w * P + v;
+                    int64_t n = t < P * npn - 1 ? s_lens[t + 1] - s_lens[t] : node_msg - s_lens[t];
+                    if (n) { buf_copy(p, LB_AGG, s_lens[t], LB_SBUF2, ptr + temp2, n); temp2 += n; }
+                }
+            ptr += temp2;
+            gsl[i] = temp2;
+            if (i * pn != rank) {
+                il_push(&idx, buf_recv(p, i * pn, 1, 4, LB_CTRL, (int64_t)i * 4, i * pn + rank + it100));
+                il_push(&idx, buf_send(p, i * pn, 1, 4, LB_CTRL, (int64_t)i * 4, i * pn + rank + it100, 0));
+            }
+        }
+        /* what proxy i sends here: everything its node's ranks send to this node's ranks */
+        for (i = 0; i < nrecvs; ++i) {
+            if (i * pn == rank) { grl[i] = gsl[i]; continue; }
+            {
+                int whi = (i + 1) * pn < P ? (i + 1) * pn : P, mhi = lr0 + npn;
+                for (w = i * pn; w < whi; ++w)
+                    for (v = lr0; v < mhi; ++v) grl[i] += tam_ss(x, w, v);
+            }
+        }
+        if (idx.n) { tstart(p, F_SEND); wait_list(p, idx.v, idx.n); tstop(p, F_SEND); }
+        idx.n = 0;
+        for (i = 0; i < nrecvs; ++i) {
+            int peer = i * pn;
+            if (i > 0) rb += grl[i - 1];
+            if (rank != peer) {
+                if (gsl[i]) il_push(&idx, buf_send(p, peer, gsl[i], 1, LB_SBUF2, ptr2, peer + rank + it100, 0));
+                if (grl[i]) il_push(&idx, buf_recv(p, peer, grl[i], 1, LB_RBUF, rb, peer + rank + it100));
+            } else if (grl[i]) {
+                buf_copy(p, LB_SBUF2, ptr2, LB_RBUF, rb, grl[i]);
+            }
+            ptr2 += gsl[i];
+            ptrs[i] = rb;
+        }
+        if (idx.n) { tstart(p, F_SEND); wait_list(p, idx.v, idx.n); tstop(p, F_SEND); }
+    }
+    /* local delivery (:1213-1285) */
+    idx.n = 0;
+    if (proxy) {
+        if (total_recv)
+            for (w = 0; w < P; ++w) {
+                int64_t n = tam_rs(x, rank, w);
+                if (n) buf_copy(p, LB_RBUF, ptrs[w / pn], LB_RECV, tam_rloc(x, w), n);
+                ptrs[w / pn] += n;
+            }
+        ptr = 0;
+        for (i = 1; i < npn; ++i) {
+            int64_t t = i == npn - 1 ? node_recv - r_lens[i * P] : r_lens[(i + 1) * P] - r_lens[i * P];
+            if (t) {
+                int64_t ptr2 = ptr;
+                for (w = 0; w < P; ++w) {
+                    int64_t n = (i == npn - 1 && w == P - 1) ? node_recv - r_lens[i * P + w]
+                                                             : r_lens[i * P + w + 1] - r_lens[i * P + w];
+                    if (n) buf_copy(p, LB_RBUF, ptrs[w / pn], LB_AGG, ptr, n);
+                    ptrs[w / pn] += n;
+                    ptr += n;
+                }
+                il_push(&idx, buf_send(p, lr0 + i, t, 1, LB_AGG, ptr2, lr0 + i + lr0 + it100, 0));
+            }
+        }
+    } else if (total_recv) {
+        il_push(&idx, buf_recv(p, lr0, total_recv, 1, LB_AGG, local, rank + lr0 + it100));
+    }
+    if (idx.n) { tstart(p, F_RECV); wait_list(p, idx.v, idx.n); tstop(p, F_RECV); }
+    if (!proxy && total_recv) {
+        off = local;
+        for (w = 0; w < P; ++w) {
+            int64_t n = tam_rs(x, rank, w);
+            if (n) { buf_copy(p, LB_AGG, off, LB_RECV, tam_rloc(x, w), n); off += n; }
+        }
+    }
+    free(idx.v); free(s_lens); free(r_lens); free(gsl); free(grl); free(ptrs);
+}
+
+/* all_to_many_tam :366-419 / many_to_all_tam :313-364 */
+static void m_tam(ctx_t *x)
+{
+    int m;
+    for (m = 0; m < x->ntimes; ++m) tam_collective_write(x);
+}
+
 /* ------------------------------------------------------------------ public: placement / labels */
 int xg_aggregator_list(int procs, int cb_nodes, int proc_node, int type, int *rl)
 {
@@ -867,15 +1083,19 @@ int xg_method_direction(int method)
     switch (method) {
     case 1: case 3: case 6: case 7: case 8: case 9: case 12: case 13: case 17: case 18: case 19: case 20:
         return XG_A2M;
+    case 15: return XG_A2M;  /* all_to_many_tam: prepare_all_to_many_data layout (:380) */
     case 2: case 4: case 5: case 10: case 11: case 14: return XG_M2A;
-    default: return -1;      /* 15/16 (TAM) are not part of this build */
+    case 16: return XG_M2A;  /* many_to_all_tam: prepare_many_to_all_data layout (:329) */
+    default: return -1;
     }
 }
 
 /* ------------------------------------------------------------------ matching */
 typedef struct {
     int32_t coll, comm, a, b, tag, rank, post, idx;
-    int64_t cnt;
+    int64_t cnt;            /* bytes */
+    int32_t lb, pad;        /* logical buffer of the data end (LB_*)  */
+    int64_t off;            /* byte offset in it                      */
 } pst_t;
 
 /* channel = (collective, communicator, src, dst, tag); FIFO inside a channel */
@@ -909,6 +1129,33 @@ static xg_msg *new_msg(xg_sched *s)
     return &s->msgs[s->nmsg++];
 }
 
+/* logical (buffer, offset) of rank r -> region + offset inside the rank's part of it */
+static void phys_loc(const xg_sched *s, int r, int lb, int64_t off, int32_t *buf, int64_t *o)
+{
+    switch (lb) {
+    case LB_SEND: *buf = XG_BUF_SEND; *o = off; break;
+    case LB_RECV: *buf = XG_BUF_RECV; *o = off; break;
+    case LB_CTRL: *buf = -1; *o = off; break;
+    default: *buf = XG_BUF_SCRATCH; *o = s->scr_base[(size_t)r * NSCR + (lb - LB_AGG)] + off; break;
+    }
+}
+
+/* TAM scratch of every rank: AGG | SBUF2 | RBUF, each 256-byte aligned */
+static void scratch_layout(xg_sched *s)
+{
+    int r, k;
+    s->scr_base = (int64_t *)xmalloc(sizeof(int64_t) * NSCR * s->P);
+    s->scr_size = (int64_t *)xmalloc(sizeof(int64_t) * s->P);
+    for (r = 0; r < s->P; ++r) {
+        int64_t o = 0;
+        for (k = 0; k < NSCR; ++k) {
+            s->scr_base[(size_t)r * NSCR + k] = o;
+            o += (s->progs[r].hi[LB_AGG + k] + 255) & ~(int64_t)255;
+        }
+        s->scr_size[r] = o;
+    }
+}
+
 static int do_match(xg_sched *s, char *err, size_t errlen)
 {
     int r, i, ns = 0, nr = 0, j;
@@ -926,10 +1173,12 @@ static int do_match(xg_sched *s, char *err, size_t errlen)
         for (i = 0; i < p->nops; ++i) {
             const op_t *o = &p->ops[i];
             if (o->kind == OP_SEND) {
-                pst_t t = { o->coll, o->comm, r, o->peer, o->coll >= 0 ? 0 : o->tag, r, o->post, o->idx, o->cnt };
+                pst_t t = { o->coll, o->comm, r, o->peer, o->coll >= 0 ? 0 : o->tag, r, o->post, o->idx,
+                            o->cnt * o->esz, o->sb, 0, o->idx >= 0 ? (int64_t)o->idx * s->d : o->off };
                 S[ns++] = t;
             } else if (o->kind == OP_RECV) {
-                pst_t t = { o->coll, o->comm, o->peer, r, o->coll >= 0 ? 0 : o->tag, r, o->post, o->idx, o->cnt };
+                pst_t t = { o->coll, o->comm, o->peer, r, o->coll >= 0 ? 0 : o->tag, r, o->post, o->idx,
+                            o->cnt * o->esz, o->db, 0, o->idx >= 0 ? (int64_t)o->idx * s->d : o->off2 };
                 R[nr++] = t;
             }
         }
@@ -949,10 +1198,17 @@ static int do_match(xg_sched *s, char *err, size_t errlen)
             free(S); free(R);
             return -1;
         }
+        if ((S[i].lb == LB_CTRL) != (R[j].lb == LB_CTRL)) {
+            snprintf(err, errlen, "size message matched with a data message %d -> %d", S[i].a, S[i].b);
+            free(S); free(R);
+            return -1;
+        }
         m = new_msg(s);
         m->src = S[i].a; m->sseg = S[i].idx; m->dst = S[i].b; m->dslot = R[j].idx;
         m->len = S[i].cnt; m->step = -1;
-        m->flags = S[i].coll >= 0 ? XG_MSG_COLL : 0;
+        m->flags = (S[i].coll >= 0 ? XG_MSG_COLL : 0) | (S[i].lb == LB_CTRL ? XG_MSG_CTRL : 0);
+        phys_loc(s, S[i].a, S[i].lb, S[i].off, &m->sbuf, &m->soff);
+        phys_loc(s, R[j].b, R[j].lb, R[j].off, &m->dbuf, &m->doff);
         s->msg_spost[s->nmsg - 1] = S[i].post;
         s->msg_rpost[s->nmsg - 1] = R[j].post;
         s->post_msg[S[i].rank][S[i].post] = s->nmsg - 1;
@@ -964,9 +1220,12 @@ static int do_match(xg_sched *s, char *err, size_t errlen)
         prog_t *p = &s->progs[r];
         for (i = 0; i < p->nops; ++i)
             if (p->ops[i].kind == OP_COPY) {
+                const op_t *o = &p->ops[i];
                 xg_msg *m = new_msg(s);
-                m->src = m->dst = r; m->sseg = p->ops[i].idx; m->dslot = p->ops[i].idx2;
-                m->len = p->ops[i].cnt; m->step = -1; m->flags = XG_MSG_COPY;
+                m->src = m->dst = r; m->sseg = o->idx; m->dslot = o->idx2;
+                m->len = o->cnt; m->step = -1; m->flags = XG_MSG_COPY;
+                phys_loc(s, r, o->sb, o->idx >= 0 ? (int64_t)o->idx * s->d : o->off, &m->sbuf, &m->soff);
+                phys_loc(s, r, o->db, o->idx2 >= 0 ? (int64_t)o->idx2 * s->d : o->off2, &m->dbuf, &m->doff);
                 p->ops[i].post = s->nmsg - 1;
             }
     }
@@ -981,10 +1240,12 @@ static int compile_steps(xg_sched *s, char *err, size_t errlen)
     int32_t **pe = (int32_t **)xmalloc(sizeof(int32_t *) * P);     /* post epoch */
     int nb = s->progs[0].nbarrier;
     int *arrived = (int *)calloc(nb + 1, sizeof(int)), *arr_epoch = (int *)xmalloc(sizeof(int) * (nb + 1));
+    int *lw = (int *)xmalloc(sizeof(int) * NLB * P), *lrd = (int *)xmalloc(sizeof(int) * NLB * P);
+    for (r = 0; r < NLB * P; ++r) lw[r] = lrd[r] = INT_MIN / 2;
     for (r = 1; r < P; ++r)
         if (s->progs[r].nbarrier != nb) {
             snprintf(err, errlen, "ranks disagree on the number of MPI_Barrier calls");
-            free(arrived); free(arr_epoch); free(pc); free(epoch); free(pe);
+            free(arrived); free(arr_epoch); free(pc); free(epoch); free(pe); free(lw); free(lrd);
             return -1;
         }
     s->nbarrier = nb;
@@ -1016,8 +1277,18 @@ static int compile_steps(xg_sched *s, char *err, size_t errlen)
                 } else if (o->kind == OP_SEND || o->kind == OP_RECV) {
                     pe[r][o->post] = epoch[r];
                 } else if (o->kind == OP_COPY) {
-                    s->msgs[o->post].step = epoch[r] + 1;
-                    if (epoch[r] + 1 > maxstep) maxstep = epoch[r] + 1;
+                    /* after everything the rank completed, after the last copy that wrote its
+                     * source, after the last copy that read its destination; what the rank
+                     * posts next moves no earlier than the copy (DESIGN.md "copy steps") */
+                    int *w = lw + (size_t)r * NLB, *rd = lrd + (size_t)r * NLB;
+                    int cs = epoch[r] + 1;
+                    if (w[o->sb] + 1 > cs) cs = w[o->sb] + 1;
+                    if (rd[o->db] + 1 > cs) cs = rd[o->db] + 1;
+                    if (cs > w[o->db]) w[o->db] = cs;
+                    if (cs > rd[o->sb]) rd[o->sb] = cs;
+                    if (cs - 1 > epoch[r]) epoch[r] = cs - 1;
+                    s->msgs[o->post].step = cs;
+                    if (cs > maxstep) maxstep = cs;
                 } else if (o->kind == OP_WAIT) {
                     int q, blocked = 0, e = epoch[r];
                     for (q = 0; q < o->wcnt; ++q) {
@@ -1058,7 +1329,7 @@ static int compile_steps(xg_sched *s, char *err, size_t errlen)
                 if (s->msgs[i].step > maxstep) maxstep = s->msgs[i].step;
             }
         for (r = 0; r < P; ++r) free(pe[r]);
-        free(pe); free(pc); free(epoch); free(arrived); free(arr_epoch);
+        free(pe); free(pc); free(epoch); free(arrived); free(arr_epoch); free(lw); free(lrd);
         s->nsteps = maxstep + 1;
         for (r = 0; r < P; ++r) {       /* reset the arrival marks used above */
             int i;
@@ -1080,7 +1351,7 @@ void xg_sched_free(xg_sched *s)
         for (r = 0; r < s->P; ++r) { free(s->post_msg[r]); free(s->post_eager[r]); }
     free(s->post_msg); free(s->post_eager);
     free(s->progs); free(s->msgs); free(s->msg_spost); free(s->msg_rpost); free(s->post_count);
-    free(s->barrier_epoch);
+    free(s->barrier_epoch); free(s->scr_base); free(s->scr_size);
     free(s->rank_list); free(s->isagg); free(s->agg_prefix);
     free(s);
 }
@@ -1089,13 +1360,21 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
                          const int *rank_list, int ntimes, int proc_node, int barrier_type,
                          int64_t eager_limit, char *err, size_t errlen)
 {
+    return xg_sched_build_iter(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, proc_node,
+                               barrier_type, eager_limit, 0, err, errlen);
+}
+
+xg_sched *xg_sched_build_iter(int method, int procs, int cb_nodes, int64_t data_size, int comm_size,
+                              const int *rank_list, int ntimes, int proc_node, int barrier_type,
+                              int64_t eager_limit, int iter, char *err, size_t errlen)
+{
     xg_sched *s;
-    int r, i;
+    int r, i, *lastidx;
     char dummy[8];
     if (!err) { err = dummy; errlen = sizeof dummy; }
     err[0] = 0;
     if (xg_method_direction(method) < 0) {
-        snprintf(err, errlen, "method %d is not part of this build (1..14, 17..20)", method);
+        snprintf(err, errlen, "method %d is not a method of the reference (1..20)", method);
         return NULL;
     }
     if (proc_node < 1) proc_node = 1;
@@ -1109,7 +1388,7 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
     s = (xg_sched *)calloc(1, sizeof *s);
     s->method = method; s->P = procs; s->A = cb_nodes; s->d = data_size; s->c = comm_size;
     s->ntimes = ntimes; s->eager = eager_limit; s->dir = xg_method_direction(method);
-    s->proc_node = proc_node; s->barrier_type = barrier_type;
+    s->proc_node = proc_node; s->barrier_type = barrier_type; s->iter = iter;
     s->rank_list = (int *)xmalloc(sizeof(int) * cb_nodes);
     memcpy(s->rank_list, rank_list, sizeof(int) * cb_nodes);
     s->isagg = (int *)calloc(procs, sizeof(int));
@@ -1118,12 +1397,16 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
     s->agg_prefix[0] = 0;
     for (r = 0; r < procs; ++r) s->agg_prefix[r + 1] = s->agg_prefix[r] + s->isagg[r];
     s->progs = (prog_t *)calloc(procs, sizeof(prog_t));
+    lastidx = (int *)xmalloc(sizeof(int) * procs);
+    for (r = 0; r < procs; ++r) lastidx[r] = -1;
+    for (i = 0; i < cb_nodes; ++i) lastidx[rank_list[i]] = i;
     for (r = 0; r < procs; ++r) {
         ctx_t x;
         prog_t *p = &s->progs[r];
         x.p = p; x.rank = r; x.isagg = s->isagg[r]; x.myindex = 0;
         x.P = procs; x.A = cb_nodes; x.c = comm_size; x.ntimes = ntimes; x.d = data_size; x.rl = rank_list;
         x.proc_node = proc_node; x.barrier_type = barrier_type;
+        x.method = method; x.iter = iter; x.isagg_all = s->isagg; x.lastidx = lastidx;
         p->rank = r;
         for (i = 0; i < cb_nodes; ++i)            /* last match, :111-115 / :183-187 */
             if (rank_list[i] == r) x.myindex = i;
@@ -1144,6 +1427,7 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
         case 12: m12_half_sync2(&x); break;
         case 13: m13_scattered(&x); break;
         case 14: m14_scattered(&x); break;
+        case 15: case 16: m_tam(&x); break;
         case 17: m17_node_robin(&x); break;
         case 18: m18_balanced_control(&x); break;
         case 19: m19_scattered_isend(&x); break;
@@ -1151,6 +1435,8 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
         }
         tstop(p, F_TOTAL);
     }
+    free(lastidx);
+    scratch_layout(s);
     s->post_msg = (int32_t **)calloc(procs, sizeof(int32_t *));
     s->post_eager = (uint8_t **)calloc(procs, sizeof(uint8_t *));
     for (r = 0; r < procs; ++r) {
@@ -1158,7 +1444,7 @@ xg_sched *xg_sched_build(int method, int procs, int cb_nodes, int64_t data_size,
         s->post_msg[r] = (int32_t *)xmalloc(sizeof(int32_t) * (p->nposts + 1));
         s->post_eager[r] = (uint8_t *)calloc(p->nposts + 1, 1);
         for (i = 0; i < p->nops; ++i)
-            if (p->ops[i].kind == OP_SEND && p->ops[i].eager_ok && p->ops[i].cnt <= eager_limit)
+            if (p->ops[i].kind == OP_SEND && p->ops[i].eager_ok && p->ops[i].cnt * p->ops[i].esz <= eager_limit)
                 s->post_eager[r][p->ops[i].post] = 1;
     }
     if (do_match(s, err, errlen) || compile_steps(s, err, errlen)) {
@@ -1201,7 +1487,8 @@ size_t xg_sched_trace(const xg_sched *s, int rank, char *buf, size_t buflen)
         else if (o->coll >= 0) continue;
         else if (o->kind == OP_SEND || o->kind == OP_RECV) {
             const char k = o->kind == OP_RECV ? 'r' : (o->isend ? 'i' : 's');
-            if (o->comm == 0) snprintf(tok, sizeof tok, "%c%d:%lld", k, o->peer, (long long)o->cnt);
+            if (o->comm == 0 && o->tag == rank + o->peer) snprintf(tok, sizeof tok, "%c%d:%lld", k, o->peer, (long long)o->cnt);
+            else if (o->comm == 0) snprintf(tok, sizeof tok, "%c%d:%lld#%d", k, o->peer, (long long)o->cnt, o->tag);
             else snprintf(tok, sizeof tok, "%c%d:%lld@%d#%d", k, o->peer, (long long)o->cnt, o->comm, o->tag);
         }
         else if (o->kind == OP_WAIT) {
@@ -1384,6 +1671,16 @@ static int64_t rank_offset(const xg_sched *s, int ngpus, int rank, int recv)
 int64_t xg_send_offset(const xg_sched *s, int ngpus, int rank) { return rank_offset(s, ngpus, rank, 0); }
 int64_t xg_recv_offset(const xg_sched *s, int ngpus, int rank) { return rank_offset(s, ngpus, rank, 1); }
 
+int64_t xg_scratch_offset(const xg_sched *s, int ngpus, int rank)
+{
+    int lo, hi, r;
+    int64_t o = 0;
+    xg_block_range(s->P, ngpus, xg_gpu_of(s->P, ngpus, rank), &lo, &hi);
+    if (!s->scr_size[rank]) return -1;
+    for (r = lo; r < rank; ++r) o += s->scr_size[r];
+    return o;
+}
+
 int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf)
 {
     int lo, hi, naggs;
@@ -1393,6 +1690,12 @@ int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf)
         return s->dir == XG_A2M ? (int64_t)(hi - lo) * s->A * s->d : (int64_t)naggs * s->P * s->d;
     if (buf == XG_BUF_RECV)
         return s->dir == XG_A2M ? (int64_t)naggs * s->P * s->d : (int64_t)(hi - lo) * s->A * s->d;
+    if (buf == XG_BUF_SCRATCH) {
+        int64_t t = 0;
+        int r;
+        for (r = lo; r < hi; ++r) t += s->scr_size[r];
+        return t;
+    }
     return 0;
 }
 
@@ -1424,6 +1727,50 @@ static int use_pack(int n, int64_t total, int64_t pack_max_seg)
     return pack_max_seg > 0 && n >= 2 && total / n < pack_max_seg;
 }
 
+/* region base of every rank hosted by the GPU the plan is for */
+typedef struct { int64_t *base[XG_NBUF]; } plan_bases;
+
+static void plan_bases_init(plan_bases *pb, const xg_sched *s, int G, int g)
+{
+    int lo, hi, r, k;
+    int64_t scr = 0;
+    (void)g;
+    for (k = 0; k < XG_NBUF; ++k) pb->base[k] = (int64_t *)calloc(s->P, sizeof(int64_t));
+    for (r = 0; r < s->P; ++r) {
+        pb->base[XG_BUF_SEND][r] = xg_send_offset(s, G, r);
+        pb->base[XG_BUF_RECV][r] = xg_recv_offset(s, G, r);
+    }
+    for (k = 0; k < G; ++k) {
+        xg_block_range(s->P, G, k, &lo, &hi);
+        for (scr = 0, r = lo; r < hi; ++r) { pb->base[XG_BUF_SCRATCH][r] = scr; scr += s->scr_size[r]; }
+    }
+}
+
+static void plan_bases_free(plan_bases *pb)
+{
+    int k;
+    for (k = 0; k < XG_NBUF; ++k) free(pb->base[k]);
+}
+
+static int64_t src_off(const plan_bases *pb, const xg_msg *m) { return pb->base[m->sbuf][m->src] + m->soff; }
+static int64_t dst_off(const plan_bases *pb, const xg_msg *m) { return pb->base[m->dbuf][m->dst] + m->doff; }
+
+/* a message that moves device bytes (not a size message, not empty) */
+static int moves(const xg_msg *m) { return m->len > 0 && !(m->flags & XG_MSG_CTRL); }
+
+/* a rank-local memcpy through a TAM aggregation buffer */
+static int is_stage(const xg_msg *m)
+{
+    return (m->flags & XG_MSG_COPY) && (m->sbuf == XG_BUF_SCRATCH || m->dbuf == XG_BUF_SCRATCH);
+}
+
+static void local_copy(xg_copy *c, const plan_bases *pb, const xg_msg *m)
+{
+    c->src_buf = m->sbuf; c->src_off = src_off(pb, m);
+    c->dst_buf = m->dbuf; c->dst_off = dst_off(pb, m);
+    c->len = m->len;
+}
+
 xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg)
 {
     xg_devplan *dp = (xg_devplan *)calloc(1, sizeof *dp);
@@ -1434,6 +1781,8 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
     int64_t stage_s_max = 0, stage_r_max = 0;
     int *bucket_n = (int *)calloc((size_t)G * 2, sizeof(int));
     int64_t *bucket_b = (int64_t *)calloc((size_t)G * 2, sizeof(int64_t));
+    plan_bases pb;
+    plan_bases_init(&pb, s, G, g);
     dp->gpu = g; dp->ngpus = G; dp->nsteps = nst;
     dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan));
     /* in-loop MPI_Barrier -> device-side barrier after the step it completes at (G > 1) */
@@ -1450,6 +1799,7 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
     }
     dp->region_bytes[XG_BUF_SEND] = xg_region_bytes(s, G, g, XG_BUF_SEND);
     dp->region_bytes[XG_BUF_RECV] = xg_region_bytes(s, G, g, XG_BUF_RECV);
+    dp->region_bytes[XG_BUF_SCRATCH] = xg_region_bytes(s, G, g, XG_BUF_SCRATCH);
     for (st = 0; st < nst; ++st) {
         int b = cnt[st], e = cnt[st + 1], k, p;
         int64_t sbase = 0, rbase = 0;
@@ -1458,15 +1808,21 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
         memset(bucket_n, 0, sizeof(int) * 2 * G);
         memset(bucket_b, 0, sizeof(int64_t) * 2 * G);
         sp->pre_begin = pre.n;
+        /* rank-local memcpy's through SCRATCH first, in a launch of their own: the
+         * local messages and packs below may read what they write in this step */
+        for (k = b; k < e; ++k) {
+            const xg_msg *m = &s->msgs[order[k]];
+            if (!moves(m) || !is_stage(m) || xg_gpu_of(s->P, G, m->src) != g) continue;
+            local_copy(cpush(&pre), &pb, m);
+            dp->local_bytes += m->len;
+        }
+        sp->stage_count = pre.n - sp->pre_begin;
         for (k = b; k < e; ++k) {
             const xg_msg *m = &s->msgs[order[k]];
             int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
-            if (m->len <= 0) continue;
+            if (!moves(m) || is_stage(m)) continue;
             if (gs == g && gd == g) {
-                xg_copy *c = cpush(&pre);
-                c->src_buf = XG_BUF_SEND; c->src_off = xg_send_offset(s, G, m->src) + (int64_t)m->sseg * s->d;
-                c->dst_buf = XG_BUF_RECV; c->dst_off = xg_recv_offset(s, G, m->dst) + (int64_t)m->dslot * s->d;
-                c->len = m->len;
+                local_copy(cpush(&pre), &pb, m);
                 dp->local_bytes += m->len;
             } else if (gs == g) {
                 bucket_n[gd]++; bucket_b[gd] += m->len;
@@ -1480,10 +1836,10 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
             if (p == g || !bucket_n[p] || !use_pack(bucket_n[p], bucket_b[p], pack_max_seg)) continue;
             for (k = b; k < e; ++k) {
                 const xg_msg *m = &s->msgs[order[k]];
-                if (m->len <= 0 || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
+                if (!moves(m) || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
                 {
                     xg_copy *c = cpush(&pre);
-                    c->src_buf = XG_BUF_SEND; c->src_off = xg_send_offset(s, G, m->src) + (int64_t)m->sseg * s->d;
+                    c->src_buf = m->sbuf; c->src_off = src_off(&pb, m);
                     c->dst_buf = XG_BUF_STAGE_SEND; c->dst_off = sbase + off;
                     c->len = m->len;
                     off += m->len;
@@ -1509,11 +1865,11 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
                     } else {
                         for (k = b; k < e; ++k) {
                             const xg_msg *m = &s->msgs[order[k]];
-                            if (m->len <= 0 || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
+                            if (!moves(m) || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
                             {
                                 xg_p2p *o = ppush(&pp);
-                                o->peer = p; o->is_send = 1; o->buf = XG_BUF_SEND;
-                                o->off = xg_send_offset(s, G, m->src) + (int64_t)m->sseg * s->d; o->len = m->len;
+                                o->peer = p; o->is_send = 1; o->buf = m->sbuf;
+                                o->off = src_off(&pb, m); o->len = m->len;
                             }
                         }
                     }
@@ -1527,11 +1883,11 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
                         o->peer = p; o->is_send = 0; o->buf = XG_BUF_STAGE_RECV; o->off = rbase; o->len = bucket_b[G + p];
                         for (k = b; k < e; ++k) {
                             const xg_msg *m = &s->msgs[order[k]];
-                            if (m->len <= 0 || xg_gpu_of(s->P, G, m->src) != p || xg_gpu_of(s->P, G, m->dst) != g) continue;
+                            if (!moves(m) || xg_gpu_of(s->P, G, m->src) != p || xg_gpu_of(s->P, G, m->dst) != g) continue;
                             {
                                 xg_copy *c = cpush(&post);
                                 c->src_buf = XG_BUF_STAGE_RECV; c->src_off = rbase + off;
-                                c->dst_buf = XG_BUF_RECV; c->dst_off = xg_recv_offset(s, G, m->dst) + (int64_t)m->dslot * s->d;
+                                c->dst_buf = m->dbuf; c->dst_off = dst_off(&pb, m);
                                 c->len = m->len;
                                 off += m->len;
                             }
@@ -1540,11 +1896,11 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
                     } else {
                         for (k = b; k < e; ++k) {
                             const xg_msg *m = &s->msgs[order[k]];
-                            if (m->len <= 0 || xg_gpu_of(s->P, G, m->src) != p || xg_gpu_of(s->P, G, m->dst) != g) continue;
+                            if (!moves(m) || xg_gpu_of(s->P, G, m->src) != p || xg_gpu_of(s->P, G, m->dst) != g) continue;
                             {
                                 xg_p2p *o = ppush(&pp);
-                                o->peer = p; o->is_send = 0; o->buf = XG_BUF_RECV;
-                                o->off = xg_recv_offset(s, G, m->dst) + (int64_t)m->dslot * s->d; o->len = m->len;
+                                o->peer = p; o->is_send = 0; o->buf = m->dbuf;
+                                o->off = dst_off(&pb, m); o->len = m->len;
                             }
                         }
                     }
@@ -1569,6 +1925,7 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
     dp->region_bytes[XG_BUF_STAGE_SEND] = stage_s_max;
     dp->region_bytes[XG_BUF_STAGE_RECV] = stage_r_max;
     free(pre.v); free(post.v); free(cnt); free(order); free(bucket_n); free(bucket_b);
+    plan_bases_free(&pb);
     return dp;
 }
 

@@ -59,13 +59,13 @@ struct xg_ctx {
 
 struct xg_regions {
     xg_ctx *ctx;
-    uint8_t *ptr[4];
-    int64_t bytes[4];
+    uint8_t *ptr[XG_NBUF];
+    int64_t bytes[XG_NBUF];
 };
 
 struct StepR {
-    int pre_b, pre_n, post_b, post_n, p2p_b, p2p_n, sync_after;
-    int64_t pre_bytes, post_bytes;   // bytes copied by each launch (read once + written once)
+    int stage_b, stage_n, pre_b, pre_n, post_b, post_n, p2p_b, p2p_n, sync_after;
+    int64_t stage_bytes, pre_bytes, post_bytes;   // bytes copied by each launch (read once + written once)
 };
 
 struct xg_plan {
@@ -198,12 +198,12 @@ extern "C" int xg_set_copy_params(xg_ctx *c, int64_t chunk, int variant)
 }
 
 // ------------------------------------------------------------------ regions
-extern "C" int xg_regions_alloc(xg_ctx *c, const int64_t bytes[4], xg_regions **out)
+extern "C" int xg_regions_alloc(xg_ctx *c, const int64_t bytes[XG_NBUF], xg_regions **out)
 {
     HIPCHK(hipSetDevice(c->device));
     xg_regions *r = new xg_regions();
     r->ctx = c;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < XG_NBUF; ++i) {
         r->bytes[i] = bytes[i];
         r->ptr[i] = nullptr;
         if (bytes[i] > 0) {
@@ -225,6 +225,8 @@ extern "C" int xg_regions_poison(xg_regions *r)
 {
     if (r->bytes[XG_BUF_RECV] > 0)
         HIPCHK(hipMemsetAsync(r->ptr[XG_BUF_RECV], 0xA5, (size_t)r->bytes[XG_BUF_RECV], r->ctx->stream));
+    if (r->bytes[XG_BUF_SCRATCH] > 0)   /* TAM aggregation buffers start zeroed (gaps stay deterministic) */
+        HIPCHK(hipMemsetAsync(r->ptr[XG_BUF_SCRATCH], 0, (size_t)r->bytes[XG_BUF_SCRATCH], r->ctx->stream));
     HIPCHK(hipStreamSynchronize(r->ctx->stream));
     return XG_OK;
 }
@@ -233,17 +235,17 @@ extern "C" int xg_regions_free(xg_regions *r)
 {
     if (!r) return XG_OK;
     HIPCHK(hipStreamSynchronize(r->ctx->stream));
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < XG_NBUF; ++i)
         if (r->ptr[i]) HIPCHK(hipFree(r->ptr[i]));
     delete r;
     return XG_OK;
 }
 
-extern "C" void *xg_regions_ptr(xg_regions *r, int buf) { return buf >= 0 && buf < 4 ? r->ptr[buf] : nullptr; }
+extern "C" void *xg_regions_ptr(xg_regions *r, int buf) { return buf >= 0 && buf < XG_NBUF ? r->ptr[buf] : nullptr; }
 
 extern "C" int xg_regions_read(xg_regions *r, int buf, int64_t off, void *host, int64_t len)
 {
-    if (buf < 0 || buf > 3 || off < 0 || len < 0 || off + len > r->bytes[buf]) return XG_EARG;
+    if (buf < 0 || buf >= XG_NBUF || off < 0 || len < 0 || off + len > r->bytes[buf]) return XG_EARG;
     HIPCHK(hipMemcpyAsync(host, r->ptr[buf] + off, (size_t)len, hipMemcpyDeviceToHost, r->ctx->stream));
     HIPCHK(hipStreamSynchronize(r->ctx->stream));
     return XG_OK;
@@ -329,7 +331,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
                 c->nranks);
         return XG_EARG;
     }
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < XG_NBUF; ++i)
         if (dp->region_bytes[i] > r->bytes[i]) {
             fprintf(stderr, "xg_plan_load: region %d too small (%lld < %lld)\n", i, (long long)r->bytes[i],
                     (long long)dp->region_bytes[i]);
@@ -342,6 +344,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     std::vector<xgk::DCopy> pieces;
     auto add = [&](const xg_copy &cp) -> bool {
         if (cp.len <= 0) return true;
+        if (cp.src_buf < 0 || cp.src_buf >= XG_NBUF || cp.dst_buf < 0 || cp.dst_buf >= XG_NBUF) return false;
         if (cp.src_off < 0 || cp.dst_off < 0 || cp.src_off + cp.len > r->bytes[cp.src_buf] ||
             cp.dst_off + cp.len > r->bytes[cp.dst_buf])
             return false;
@@ -358,8 +361,15 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     for (int s = 0; s < dp->nsteps; ++s) {
         const xg_stepplan &sp = dp->steps[s];
         StepR &st = p->steps[s];
+        if (sp.stage_count < 0 || sp.stage_count > sp.pre_count) goto bad;
+        st.stage_b = (int)pieces.size();
+        for (int i = 0; i < sp.stage_count; ++i)
+            if (!add(dp->copies[sp.pre_begin + i])) goto bad;
+        st.stage_n = (int)pieces.size() - st.stage_b;
+        st.stage_bytes = 0;
+        for (int i = st.stage_b; i < st.stage_b + st.stage_n; ++i) st.stage_bytes += pieces[i].len;
         st.pre_b = (int)pieces.size();
-        for (int i = 0; i < sp.pre_count; ++i)
+        for (int i = sp.stage_count; i < sp.pre_count; ++i)
             if (!add(dp->copies[sp.pre_begin + i])) goto bad;
         st.pre_n = (int)pieces.size() - st.pre_b;
         st.pre_bytes = 0;
@@ -373,7 +383,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.p2p_b = (int)p->p2p.size();
         for (int i = 0; i < sp.p2p_count; ++i) {
             const xg_p2p &o = dp->p2p[sp.p2p_begin + i];
-            if (o.peer < 0 || o.peer >= c->nranks || o.peer == c->rank || o.off < 0 ||
+            if (o.peer < 0 || o.peer >= c->nranks || o.peer == c->rank || o.buf < 0 || o.buf >= XG_NBUF || o.off < 0 ||
                 o.off + o.len > r->bytes[o.buf])
                 goto bad;
             p->p2p.push_back(o);
@@ -445,6 +455,7 @@ static int enqueue_step(xg_plan *p, int s)
         }
         return XG_OK;
     };
+    if (st.stage_n && (rc = timed(st.stage_b, st.stage_n, st.stage_bytes))) return rc;
     if (st.pre_n && (rc = timed(st.pre_b, st.pre_n, st.pre_bytes))) return rc;
     if (st.p2p_n) {
         NCCLCHK(ncclGroupStart());

@@ -27,9 +27,13 @@ class Timer(C.Structure):
                 self.barrier_time, self.total_time)
 
 
+NBUF = 5   # XG_NBUF
+
+
 class Msg(C.Structure):
     _fields_ = [("src", C.c_int32), ("sseg", C.c_int32), ("dst", C.c_int32), ("dslot", C.c_int32),
-                ("len", C.c_int64), ("step", C.c_int32), ("flags", C.c_int32)]
+                ("len", C.c_int64), ("step", C.c_int32), ("flags", C.c_int32),
+                ("sbuf", C.c_int32), ("dbuf", C.c_int32), ("soff", C.c_int64), ("doff", C.c_int64)]
 
 
 class Copy(C.Structure):
@@ -45,12 +49,12 @@ class P2P(C.Structure):
 class StepPlan(C.Structure):
     _fields_ = [("pre_begin", C.c_int32), ("pre_count", C.c_int32), ("p2p_begin", C.c_int32),
                 ("p2p_count", C.c_int32), ("post_begin", C.c_int32), ("post_count", C.c_int32),
-                ("sync_after", C.c_int32), ("pad", C.c_int32)]
+                ("sync_after", C.c_int32), ("stage_count", C.c_int32)]
 
 
 class DevPlan(C.Structure):
     _fields_ = [("gpu", C.c_int32), ("ngpus", C.c_int32), ("nsteps", C.c_int32), ("pad", C.c_int32),
-                ("region_bytes", C.c_int64 * 4), ("ncopy", C.c_int32), ("np2p", C.c_int32),
+                ("region_bytes", C.c_int64 * NBUF), ("ncopy", C.c_int32), ("np2p", C.c_int32),
                 ("copies", C.POINTER(Copy)), ("p2p", C.POINTER(P2P)), ("steps", C.POINTER(StepPlan)),
                 ("local_bytes", C.c_int64), ("remote_send_bytes", C.c_int64),
                 ("remote_recv_bytes", C.c_int64)]
@@ -67,7 +71,9 @@ class Slot(C.Structure):
 
 
 A2M, M2A = 0, 1
-BUF_SEND, BUF_RECV, BUF_STAGE_SEND, BUF_STAGE_RECV = 0, 1, 2, 3
+BUF_SEND, BUF_RECV, BUF_STAGE_SEND, BUF_STAGE_RECV, BUF_SCRATCH = 0, 1, 2, 3, 4
+MSG_COPY, MSG_COLL, MSG_CTRL = 1, 2, 4
+TAM_METHODS = (15, 16)
 MPICH_EAGER_LIMIT = 65424
 
 
@@ -93,6 +99,9 @@ def host():
         h.xg_sched_build.restype = C.c_void_p
         h.xg_sched_build.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_int),
                                      C.c_int, C.c_int, C.c_int, C.c_int64, C.c_char_p, C.c_size_t]
+        h.xg_sched_build_iter.restype = C.c_void_p
+        h.xg_sched_build_iter.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_int),
+                                          C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int, C.c_char_p, C.c_size_t]
         h.xg_sched_free.argtypes = [C.c_void_p]
         for fn in ("xg_sched_nmsg", "xg_sched_nsteps", "xg_sched_direction", "xg_sched_procs"):
             getattr(h, fn).argtypes = [C.c_void_p]
@@ -109,7 +118,7 @@ def host():
         h.xg_save_all_timing.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(Timer), C.c_char_p]
         h.xg_block_range.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         h.xg_gpu_of.argtypes = [C.c_int, C.c_int, C.c_int]
-        for fn in ("xg_send_offset", "xg_recv_offset"):
+        for fn in ("xg_send_offset", "xg_recv_offset", "xg_scratch_offset"):
             getattr(h, fn).restype = C.c_int64
             getattr(h, fn).argtypes = [C.c_void_p, C.c_int, C.c_int]
         h.xg_region_bytes.restype = C.c_int64
@@ -140,15 +149,15 @@ class Schedule:
     """One method run (all -k repetitions), compiled to device-wide steps."""
 
     def __init__(self, method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes=1,
-                 eager_limit=MPICH_EAGER_LIMIT, proc_node=1, barrier_type=0):
+                 eager_limit=MPICH_EAGER_LIMIT, proc_node=1, barrier_type=0, iteration=0):
         h = host()
         self.method, self.P, self.A, self.d, self.c = method, procs, cb_nodes, data_size, comm_size
         self.rank_list = list(rank_list)
         self.ntimes = ntimes
         err = C.create_string_buffer(512)
         rl = (C.c_int * cb_nodes)(*rank_list)
-        self._h = h.xg_sched_build(method, procs, cb_nodes, data_size, comm_size, rl, ntimes,
-                                   proc_node, barrier_type, eager_limit, err, 512)
+        self._h = h.xg_sched_build_iter(method, procs, cb_nodes, data_size, comm_size, rl, ntimes,
+                                        proc_node, barrier_type, eager_limit, iteration, err, 512)
         if not self._h:
             raise XGError(err.value.decode())
         self.nsteps = h.xg_sched_nsteps(self._h)
@@ -167,6 +176,12 @@ class Schedule:
         n = host().xg_sched_nmsg(self._h)
         ptr = host().xg_sched_msgs(self._h)
         return [(m.src, m.sseg, m.dst, m.dslot, m.len, m.step, m.flags) for m in ptr[:n]]
+
+    def locations(self):
+        """Per message: (sbuf, soff, dbuf, doff) -- region and offset inside the rank's part."""
+        n = host().xg_sched_nmsg(self._h)
+        ptr = host().xg_sched_msgs(self._h)
+        return [(m.sbuf, m.soff, m.dbuf, m.doff) for m in ptr[:n]]
 
     def trace(self, rank):
         n = host().xg_sched_trace(self._h, rank, None, 0)
@@ -211,6 +226,9 @@ class Schedule:
     def recv_offset(self, ngpus, rank):
         return host().xg_recv_offset(self._h, ngpus, rank)
 
+    def scratch_offset(self, ngpus, rank):
+        return host().xg_scratch_offset(self._h, ngpus, rank)
+
     def region_bytes(self, ngpus, g, buf):
         return host().xg_region_bytes(self._h, ngpus, g, buf)
 
@@ -244,6 +262,7 @@ class DevicePlanView:
         self.steps = [(s.pre_begin, s.pre_count, s.p2p_begin, s.p2p_count, s.post_begin, s.post_count)
                       for s in p.steps[:p.nsteps]]
         self.sync_after = [s.sync_after for s in p.steps[:p.nsteps]]
+        self.stage_count = [s.stage_count for s in p.steps[:p.nsteps]]
         self.local_bytes = p.local_bytes
         self.remote_send_bytes = p.remote_send_bytes
         self.remote_recv_bytes = p.remote_recv_bytes
@@ -384,7 +403,7 @@ class MethodRun:
         self.ctx, self.sched, self.it, self.mode = ctx, sched, it, mode
         G, g = ctx.nranks, ctx.rank
         self.view = sched.devplan(G, g, pack_max_seg)
-        rb = (C.c_int64 * 4)(*self.view.region_bytes)
+        rb = (C.c_int64 * NBUF)(*self.view.region_bytes)
         self._r = C.c_void_p()
         _check(d.xg_regions_alloc(ctx.handle, rb, C.byref(self._r)), "xg_regions_alloc")
         n = host().xg_fill_runs(sched.handle, G, g, None)

@@ -10,7 +10,7 @@ What it restates (every function cites the reference line it follows):
   * buffer layouts                  prepare_*_data           mpi_test.c:94-133, :162-202
   * alltoallw counts/displacements  *_alltoall_translate     mpi_test.c:233-302
   * the per-rank MPI programs of methods 1..14, 17..20         mpi_test.c:421-1950
-    (15/16 = TAM via lustre_driver_test.c are not part of this build)
+  * TAM (m15/m16): static_node_assignment + collective_write   lustre_driver_test.c:359-429, :944-1309
   * MPI point-to-point matching (non-overtaking per (src,dst,tag)) and
     collective matching for MPI_Alltoallw, executed with byte copies.
 
@@ -38,15 +38,17 @@ Post indices count 's' and 'r' ops (and the posts of an 'A') in program order.
 """
 import numpy as np
 
-A2M_METHODS = (1, 3, 6, 7, 8, 9, 12, 13, 17, 18, 19, 20)
-M2A_METHODS = (2, 4, 5, 10, 11, 14)
-METHODS = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 17, 18, 19, 20)
+A2M_METHODS = (1, 3, 6, 7, 8, 9, 12, 13, 15, 17, 18, 19, 20)
+M2A_METHODS = (2, 4, 5, 10, 11, 14, 16)
+METHODS = tuple(range(1, 21))
+TAM_METHODS = (15, 16)
 LABELS = {  # mpi_test.c:2186 ... :2337
     1: "All to many", 2: "Many to all", 3: "All to many balanced", 4: "Many to all balanced",
     5: "Many to all benchmark", 6: "All to many sync", 7: "All to many half sync",
     8: "All to many benchmark", 9: "All to many pairwise", 10: "Many to all pairwise",
     11: "Many to all half sync", 12: "All to many half sync 2", 13: "All to many scattered",
-    14: "Many to all scattered", 17: "All to many node robin", 18: "All to many balanced control",
+    14: "Many to all scattered", 15: "All to many TAM", 16: "Many to all TAM",
+    17: "All to many node robin", 18: "All to many balanced control",
     19: "All to many scattered isend", 20: "All to many balanced presend",
 }
 
@@ -165,15 +167,21 @@ class _Prog:
         self.ops = []
         self.nposts = 0
 
-    def s(self, peer, cnt, seg, eager_ok=False, comm=0, tag=None, isend=False):
-        self.ops.append(("s", peer, cnt, seg, eager_ok or isend, comm, tag, isend))
+    def s(self, peer, cnt, seg, eager_ok=False, comm=0, tag=None, isend=False, buf=None, off=0, esz=1):
+        """buf None: segment `seg` of the SEND buffer; otherwise bytes [off, off+cnt*esz) of the
+        rank's buffer `buf` ('AGG', 'SBUF2', 'RBUF', 'CTRL...')."""
+        self.ops.append(("s", peer, cnt, seg, eager_ok or isend, comm, tag, isend, buf, off, esz))
         self.nposts += 1
         return self.nposts - 1
 
-    def r(self, peer, cnt, slot, comm=0, tag=None):
-        self.ops.append(("r", peer, cnt, slot, comm, tag))
+    def r(self, peer, cnt, slot, comm=0, tag=None, buf=None, off=0, esz=1):
+        self.ops.append(("r", peer, cnt, slot, comm, tag, buf, off, esz))
         self.nposts += 1
         return self.nposts - 1
+
+    def cp(self, sbuf, soff, dbuf, doff, n):
+        """memcpy between (buffer, offset) locations of this rank; SEND/RECV offsets in bytes."""
+        self.ops.append(("C", sbuf, soff, dbuf, doff, n))
 
     def w(self, idxs):
         self.ops.append(("w", list(idxs)))
@@ -183,6 +191,10 @@ class _Prog:
 
     def recv(self, peer, cnt, slot, comm=0, tag=None):   # blocking MPI_Recv
         self.w([self.r(peer, cnt, slot, comm, tag)])
+
+    def ctrl(self, name, data):
+        """host-side int array whose bytes a size message carries (TAM)."""
+        self.ops.append(("K", name, np.asarray(data, dtype="<i4").view(np.uint8).copy()))
 
     def sendrecv(self, dst, scnt, seg, src, rcnt, slot):   # MPI_Sendrecv
         a = self.s(dst, scnt, seg, True)
@@ -212,7 +224,7 @@ def _in_window(rank, temp, cs, P):
     return rank >= temp or rank < (temp + cs) % P
 
 
-def programs(method, P, A, d, c, rank_list, ntimes, proc_node=1, barrier_type=0):
+def programs(method, P, A, d, c, rank_list, ntimes, proc_node=1, barrier_type=0, it=0):
     """Per-rank op lists of method `method` exactly as the reference issues them."""
     aggidx = {g: i for i, g in enumerate(rank_list)}
     progs = []
@@ -226,6 +238,8 @@ def programs(method, P, A, d, c, rank_list, ntimes, proc_node=1, barrier_type=0)
         fn = _METHODS[method]
         if method in (13, 17):
             fn(p, rank, isagg, myindex, P, A, d, c, rank_list, ntimes, proc_node, barrier_type)
+        elif method in (15, 16):
+            fn(p, rank, isagg, myindex, P, A, d, c, rank_list, ntimes, proc_node, it)
         else:
             fn(p, rank, isagg, myindex, P, A, d, c, rank_list, ntimes)
         p.t("total", -1)
@@ -752,10 +766,190 @@ def _m20(p, rank, isagg, myindex, P, A, d, c, rl, ntimes):
             p.t("send", +1); p.w(sends); p.t("send", -1)
 
 
+def static_node_assignment(rank, P, proc_node):
+    """static_node_assignment type 0 (lustre_driver_test.c:404-427) as called by the TAM methods
+    (mpi_test.c:341, :395): nodes of proc_node consecutive ranks; proxy = first rank of a node.
+    -> (nprocs_node of this rank, nrecvs, local_ranks, global_receivers, process_node_list)"""
+    nrecvs = (P + proc_node - 1) // proc_node
+    local_ranks = [(rank // proc_node) * proc_node + i for i in range(proc_node)]
+    receivers = [i * proc_node for i in range(nrecvs)]
+    node_of = [i // proc_node for i in range(P)]
+    npn = proc_node
+    if rank >= (nrecvs - 1) * proc_node:
+        npn = P - proc_node * (nrecvs - 1)
+    return npn, nrecvs, local_ranks, receivers, node_of
+
+
+def _tam_sizes(method, P, A, d, rl):
+    """send_size / recv_size per rank as handed to collective_write (mpi_test.c:343, :393)."""
+    ss, rs = {}, {}
+    for r in range(P):
+        isagg = r in rl
+        if method == 15:
+            sc, sd, rc, rd = _a2m_translate(r, isagg, P, A, d, rl)
+        else:
+            sc, sd, rc, rd = _m2a_translate(r, isagg, P, A, d, rl)
+        ss[r], rs[r] = sc, rc
+    return ss, rs
+
+
+def _tam_locs(method, rank, P, rl, d):
+    """send_buf[w] / recv_buf[w] locations (byte offsets in SEND / RECV): a2m send_buf2[rank_list[i]] =
+    segment i (:388-391), recv slot w; m2a send segment w, recv_buf2[rank_list[i]] = slot i (:335-339)."""
+    if method == 15:
+        sloc = {g: i * d for i, g in enumerate(rl)}
+        rloc = {w: w * d for w in range(P)}
+    else:
+        sloc = {w: w * d for w in range(P)}
+        rloc = {g: i * d for i, g in enumerate(rl)}
+    return sloc, rloc
+
+
+def _tam(method):
+    def run(p, rank, isagg, myindex, P, A, d, c, rl, ntimes, proc_node=1, it=0):
+        """all_to_many_tam :366-419 / many_to_all_tam :313-364 -> collective_write, lustre_driver_test.c:944-1309."""
+        ss_all, rs_all = _tam_sizes(method, P, A, d, rl)
+        sloc, rloc = _tam_locs(method, rank, P, rl, d)
+        for _ in range(ntimes):
+            _collective_write(p, rank, P, proc_node, ss_all, rs_all, sloc, rloc, it)
+    return run
+
+
+def _collective_write(p, rank, P, proc_node, ss_all, rs_all, sloc, rloc, it):
+    npn, nrecvs, lr, gr, node_of = static_node_assignment(rank, P, proc_node)
+    proxy = rank == lr[0]
+    ssz, rsz = ss_all[rank], rs_all[rank]
+    total_send, total_recv = sum(ssz), sum(rsz)
+    # tags of :1006, :1012, :1094, ...: a + b + 100*iter (None = the default rank + peer, iter 0)
+    tg = lambda a, b: None if it == 0 else a + b + 100 * it   # noqa: E731
+    # ---- intra-node gather of the send/recv sizes (:996-1018)
+    idx = []
+    if proxy:
+        for i in range(1, npn):
+            idx.append(p.r(lr[i], 2 * P, -1, tag=tg(lr[i], lr[0]), buf="CTRL_LL", off=i * P * 8, esz=4))
+    else:
+        p.ctrl("CTRL_MY", list(ssz) + list(rsz))
+        idx.append(p.s(lr[0], 2 * P, -1, isend=True, tag=tg(rank, lr[0]), buf="CTRL_MY", off=0, esz=4))
+    if idx:
+        p.t("recv", +1); p.w(idx); p.t("recv", -1)
+    # proxy: exclusive prefix sums over (local process i, target w) (:1027-1041)
+    if proxy:
+        s_lens, r_lens, node_msg, node_recv = [], [], 0, 0
+        for i in range(npn):
+            for w in range(P):
+                s_lens.append(node_msg); node_msg += ss_all[lr[i]][w]
+                r_lens.append(node_recv); node_recv += rs_all[lr[i]][w]
+        temp = max(node_msg, node_recv)
+    else:
+        temp = 0
+    local = temp                                     # local_buf = aggregate_buf + temp (:1054-1068)
+    # ---- pack this process's messages into local_buf (:1069-1077)
+    off = 0
+    for w in range(P):
+        if ssz[w]:
+            p.cp("SEND", sloc[w], "AGG", local + off, ssz[w])
+            off += ssz[w]
+    # ---- messages to the local proxy (:1078-1107)
+    idx = []
+    if proxy:
+        if total_send:
+            p.cp("AGG", local, "AGG", 0, total_send)
+        ptr = total_send
+        for i in range(1, npn):
+            t = (node_msg - s_lens[i * P]) if i == npn - 1 else (s_lens[(i + 1) * P] - s_lens[i * P])
+            if t:
+                idx.append(p.r(lr[i], t, -1, tag=tg(lr[i], lr[0]), buf="AGG", off=ptr))
+            ptr += t
+    elif total_send:
+        idx.append(p.s(lr[0], total_send, -1, tag=tg(rank, lr[0]), buf="AGG", off=local))
+    if idx:
+        p.t("recv", +1); p.w(idx); p.t("recv", -1)
+    if proxy:
+        # ---- inter-node exchange among proxies (:1116-1197)
+        idx, ptr, gsl, grl = [], 0, [0] * nrecvs, [0] * nrecvs
+        for i in range(nrecvs):
+            temp2 = 0
+            for v in range(P):
+                if node_of[v] != i:
+                    continue
+                for w in range(npn):
+                    t = w * P + v
+                    n = (s_lens[t + 1] - s_lens[t]) if t < P * npn - 1 else (node_msg - s_lens[t])
+                    if n:
+                        p.cp("AGG", s_lens[t], "SBUF2", ptr + temp2, n)
+                        temp2 += n
+            ptr += temp2
+            gsl[i] = temp2
+            r_rank = gr[i]
+            if r_rank != rank:
+                p.ctrl("CTRL_GS%d" % i, [temp2])
+                idx.append(p.r(r_rank, 1, -1, tag=tg(r_rank, rank), buf="CTRL_GR%d" % i, off=0, esz=4))
+                idx.append(p.s(r_rank, 1, -1, tag=tg(r_rank, rank), buf="CTRL_GS%d" % i, off=0, esz=4))
+        # what proxy i sends here: everything its node's ranks send to this node's ranks
+        for i in range(nrecvs):
+            if gr[i] == rank:
+                grl[i] = gsl[i]
+            else:
+                grl[i] = sum(ss_all[w][v] for w in range(P) if node_of[w] == i for v in range(P)
+                             if node_of[v] == node_of[rank])
+        if idx:
+            p.t("send", +1); p.w(idx); p.t("send", -1)
+        idx, ptr2, rb, ptrs = [], 0, 0, []
+        for i in range(nrecvs):
+            r_rank = gr[i]
+            if i > 0:
+                rb += grl[i - 1]
+            if rank != r_rank:
+                if gsl[i]:
+                    idx.append(p.s(r_rank, gsl[i], -1, tag=tg(r_rank, rank), buf="SBUF2", off=ptr2))
+                if grl[i]:
+                    idx.append(p.r(r_rank, grl[i], -1, tag=tg(r_rank, rank), buf="RBUF", off=rb))
+            elif grl[i]:
+                p.cp("SBUF2", ptr2, "RBUF", rb, grl[i])
+            ptr2 += gsl[i]
+            ptrs.append(rb)
+        if idx:
+            p.t("send", +1); p.w(idx); p.t("send", -1)
+    # ---- local delivery (:1213-1285)
+    idx = []
+    if proxy:
+        if total_recv:
+            for w in range(P):
+                if rsz[w]:
+                    p.cp("RBUF", ptrs[node_of[w]], "RECV", rloc[w], rsz[w])
+                ptrs[node_of[w]] += rsz[w]
+        ptr = 0
+        for i in range(1, npn):
+            t = (node_recv - r_lens[i * P]) if i == npn - 1 else (r_lens[(i + 1) * P] - r_lens[i * P])
+            if t:
+                ptr2 = ptr
+                for w in range(P):
+                    if i == npn - 1 and w == P - 1:
+                        n = node_recv - r_lens[i * P + w]
+                    else:
+                        n = r_lens[i * P + w + 1] - r_lens[i * P + w]
+                    if n:
+                        p.cp("RBUF", ptrs[node_of[w]], "AGG", ptr, n)
+                    ptrs[node_of[w]] += n
+                    ptr += n
+                idx.append(p.s(lr[i], t, -1, tag=tg(lr[i], lr[0]), buf="AGG", off=ptr2))
+    elif total_recv:
+        idx.append(p.r(lr[0], total_recv, -1, tag=tg(rank, lr[0]), buf="AGG", off=local))
+    if idx:
+        p.t("recv", +1); p.w(idx); p.t("recv", -1)
+    if not proxy and total_recv:
+        off = local
+        for i in range(P):
+            if rsz[i]:
+                p.cp("AGG", off, "RECV", rloc[i], rsz[i])
+                off += rsz[i]
+
+
 _METHODS = {
     1: _m1, 2: _m2, 3: _m3, 4: _m4, 5: _alltoallw(_m2a_translate), 6: _m6, 7: _m7,
     8: _alltoallw(_a2m_translate), 9: _pairwise(_a2m_translate), 10: _pairwise(_m2a_translate),
-    11: _m11, 12: _m12, 13: _m13, 14: _m14, 17: _m17, 18: _m18, 19: _m19, 20: _m20,
+    11: _m11, 12: _m12, 13: _m13, 14: _m14, 15: _tam(15), 16: _tam(16), 17: _m17, 18: _m18, 19: _m19,
+    20: _m20,
 }
 
 
@@ -772,6 +966,12 @@ def _idx_list(idxs):
     return ",".join(out)
 
 
+def _tok(kind, peer, cnt, comm, tag):
+    if comm == 0:
+        return "%s%d:%d" % (kind, peer, cnt) if tag is None else "%s%d:%d#%d" % (kind, peer, cnt, tag)
+    return "%s%d:%d@%d#%d" % (kind, peer, cnt, comm, tag)
+
+
 def trace_tokens(ops, ntimes_split=False):
     """Canonical token string, identical to the PMPI capture format (tests/golden/make_golden.py)."""
     toks = []
@@ -781,11 +981,9 @@ def trace_tokens(ops, ntimes_split=False):
             toks.append("B")
         elif k == "s":
             kind = "i" if op[7] else "s"
-            toks.append(("%s%d:%d" % (kind, op[1], op[2])) if op[5] == 0 else
-                        ("%s%d:%d@%d#%d" % (kind, op[1], op[2], op[5], op[6])))
+            toks.append(_tok(kind, op[1], op[2], op[5], op[6]))
         elif k == "r":
-            toks.append(("r%d:%d" % (op[1], op[2])) if op[4] == 0 else
-                        ("r%d:%d@%d#%d" % (op[1], op[2], op[4], op[5])))
+            toks.append(_tok("r", op[1], op[2], op[4], op[5]))
         elif k == "w":
             toks.append("w" + _idx_list(op[1]))
         elif k == "A":
@@ -795,7 +993,7 @@ def trace_tokens(ops, ntimes_split=False):
 
 # --------------------------------------------------------------------------- execution
 def match(progs):
-    """MPI matching.  Returns the message list [(src, seg, dst, slot, cnt, s_post, r_post)]
+    """MPI matching.  Returns the message list [(src, seg, dst, slot, bytes, s_post, r_post)]
     where s_post / r_post are the post indices at the sender / receiver.
     Point-to-point: FIFO per (communicator, src, dst, tag) (MPI non-overtaking); the
     reference's tag is src+dst on MPI_COMM_WORLD.  Alltoallw: the k-th call of every
@@ -810,10 +1008,10 @@ def match(progs):
         for op in ops:
             if op[0] == "s":
                 tag = r + op[1] if op[6] is None else op[6]
-                sends[(op[5], r, op[1], tag)].append((op[3], op[2], post)); post += 1
+                sends[(op[5], r, op[1], tag)].append((op[3], op[2] * op[10], post)); post += 1
             elif op[0] == "r":
                 tag = r + op[1] if op[5] is None else op[5]
-                recvs[(op[4], op[1], r, tag)].append((op[3], op[2], post)); post += 1
+                recvs[(op[4], op[1], r, tag)].append((op[3], op[2] * op[8], post)); post += 1
             elif op[0] == "A":
                 for q, cnt, seg in op[1]:
                     coll_s[ncoll][(r, q)] = (cnt, seg, post); post += 1
@@ -838,21 +1036,151 @@ def match(progs):
     return msgs
 
 
-def execute(method, P, A, d, rank_list, progs, it, mode=0):
-    """Run the matched programs with byte copies; returns {rank: recv buffer (uint8)}."""
+def execute(method, P, A, d, rank_list, progs, it, mode=0, record=None, eager_limit=None, buffers=None):
+    """Run the matched programs with MPI semantics on bytes; returns {rank: RECV buffer}.
+
+    Sends snapshot their bytes when posted (MPI forbids touching a send buffer before it
+    completes), receives land at the completion point that waits for them, copies and
+    size arrays run in program order, barriers are collective.  record (dict, optional)
+    gets, per rank, every received message as (src, count, chk64 of its first `count`
+    bytes) in completion order -- what oracle/pmpi_capture.c logs as D lines.  buffers (dict,
+    optional) gets every rank's final {buffer name: bytes}."""
+    if eager_limit is None:
+        eager_limit = MPICH_EAGER_LIMIT
     lay = layout(method, P, A, rank_list)
-    send = {r: np.concatenate([fingerprint(mode, r, seg_seed(method, r, s), it, d) for s in range(n)])
-            if n else np.zeros(0, np.uint8) for r, (n, _) in lay.items()}
-    recv = {r: np.full(m * d, 0xA5, np.uint8) for r, (_, m) in lay.items()}
-    for src, seg, dst, slot, cnt, _sp, _rp in match(progs):
-        if cnt > 0:
-            recv[dst][slot * d: slot * d + cnt] = send[src][seg * d: seg * d + cnt]
+    bufs = []
+    for r in range(P):
+        n_send, n_recv = lay[r]
+        bufs.append({
+            "SEND": np.concatenate([fingerprint(mode, r, seg_seed(method, r, q), it, d) for q in range(n_send)])
+            if n_send else np.zeros(0, np.uint8),
+            "RECV": np.full(n_recv * d, 0xA5, np.uint8)})
+
+    def region(r, name, lo, n):
+        b = bufs[r].get(name)
+        if b is None or b.size < lo + n:
+            nb = np.zeros(max(lo + n, 0), np.uint8)
+            if b is not None:
+                nb[:b.size] = b
+            bufs[r][name] = b = nb
+        return b[lo:lo + n]
+
+    def send_loc(r, op):       # ('s', peer, cnt, seg, eager_ok, comm, tag, isend, buf, off, esz)
+        n = op[2] * (op[10] if len(op) > 10 else 1)
+        if len(op) > 8 and op[8] is not None:
+            return op[8], op[9], n
+        return "SEND", max(op[3], 0) * d, n
+
+    def recv_loc(r, op):       # ('r', peer, cnt, slot, comm, tag, buf, off, esz)
+        n = op[2] * (op[8] if len(op) > 8 else 1)
+        if len(op) > 6 and op[6] is not None:
+            return op[6], op[7], n
+        return "RECV", max(op[3], 0) * d, n
+
+    msgs = match(progs)
+    by_post = {}
+    for mi, (src, _seg, dst, _slot, _cnt, sp, rp) in enumerate(msgs):
+        by_post[(src, sp)] = mi
+        by_post[(dst, rp)] = mi
+    post_op = {}
     for r, ops in enumerate(progs):
+        q = 0
         for op in ops:
-            if op[0] == "c":
-                _, seg, slot, cnt = op
-                recv[r][slot * d: slot * d + cnt] = send[r][seg * d: seg * d + cnt]
-    return recv
+            if op[0] in ("s", "r"):
+                post_op[(r, q)] = op
+                q += 1
+            elif op[0] == "A":
+                for peer, cnt, seg in op[1]:
+                    post_op[(r, q)] = ("s", peer, cnt, seg, False, 0, None, False)
+                    q += 1
+                for peer, cnt, slot in op[2]:
+                    post_op[(r, q)] = ("r", peer, cnt, slot, 0, None)
+                    q += 1
+    snap, posted = {}, set()
+    pc, npost, nbar = [0] * P, [0] * P, [0] * P
+    arrivals = {}
+    if record is not None:
+        for r in range(P):
+            record.setdefault(r, [])
+
+    def post(r, q):
+        op = post_op[(r, q)]
+        posted.add((r, q))
+        if op[0] == "s":
+            name, lo, n = send_loc(r, op)
+            snap[by_post[(r, q)]] = region(r, name, lo, n).copy()
+
+    def can_complete(r, q):
+        mi = by_post[(r, q)]
+        src, _s, dst, _sl, cnt, sp, rp = msgs[mi]
+        op = post_op[(r, q)]
+        if op[0] == "r":
+            return (src, sp) in posted
+        if op[4] and cnt <= eager_limit:               # eager send (bytes): completes locally
+            return True
+        return (dst, rp) in posted
+
+    def complete(r, qs):
+        for q in qs:
+            op = post_op[(r, q)]
+            if op[0] != "r":
+                continue
+            mi = by_post[(r, q)]
+            name, lo, n = recv_loc(r, op)
+            data = snap[mi]
+            region(r, name, lo, n)[:data.size] = data
+            if record is not None and op[2] > 0:
+                b = bufs[r][name]
+                record[r].append((msgs[mi][0], op[2], chk64(b[lo:lo + op[2]])))
+
+    progress = True
+    while progress:
+        progress = False
+        for r in range(P):
+            ops = progs[r]
+            while pc[r] < len(ops):
+                op = ops[pc[r]]
+                k = op[0]
+                if k == "B":
+                    arr = arrivals.setdefault(nbar[r], set())
+                    arr.add(r)
+                    if len(arr) < P:
+                        break
+                    nbar[r] += 1
+                elif k in ("s", "r"):
+                    post(r, npost[r])
+                    npost[r] += 1
+                elif k == "A":
+                    first = npost[r]
+                    n = len(op[1]) + len(op[2])
+                    if (r, first) not in posted:
+                        for q in range(first, first + n):
+                            post(r, q)
+                    qs = list(range(first, first + n))
+                    if not all(can_complete(r, q) for q in qs):
+                        break
+                    complete(r, qs)
+                    npost[r] += n
+                elif k == "w":
+                    if not all(can_complete(r, q) for q in op[1]):
+                        break
+                    complete(r, op[1])
+                elif k == "c":
+                    _, seg, slot, cnt = op
+                    region(r, "RECV", slot * d, cnt)[:] = region(r, "SEND", seg * d, cnt)
+                elif k == "C":
+                    _, sb, so, db, do, n = op
+                    src = region(r, sb, so, n).copy()
+                    region(r, db, do, n)[:] = src
+                elif k == "K":
+                    region(r, op[1], 0, op[2].size)[:] = op[2]
+                pc[r] += 1
+                progress = True
+    if any(pc[r] < len(progs[r]) for r in range(P)):
+        raise RuntimeError("deadlock while executing")
+    if buffers is not None:
+        buffers.update({r: bufs[r] for r in range(P)})
+    return {r: bufs[r]["RECV"][:lay[r][1] * d] for r in range(P)}
 
 
 MPICH_EAGER_LIMIT = 65424   # measured on the image's MPICH 3.3.2 ch3:nemesis (DESIGN.md)
@@ -874,7 +1202,7 @@ def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT, info=None):
         post = 0
         for op in ops:
             if op[0] == "s":
-                if op[4] and op[2] <= eager_limit:      # blocking send / Isend of <= eager limit
+                if op[4] and op[2] * op[10] <= eager_limit:   # blocking send / Isend of <= eager limit
                     eager.add((r, post))
                 post += 1
             elif op[0] == "r":
@@ -894,6 +1222,10 @@ def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT, info=None):
     nbar = [0] * P                  # barriers passed per rank
     arrivals = {}                   # barrier k -> {rank: epoch at arrival}
     barrier_epochs = []             # epoch at which barrier k completes (global)
+    NEG = -(1 << 40)
+    last_w = [dict() for _ in range(P)]     # rank -> buffer -> last step a copy wrote it
+    last_r = [dict() for _ in range(P)]     # rank -> buffer -> last step a copy read it
+    copy_steps = []
     progress = True
     while progress:
         progress = False
@@ -931,15 +1263,26 @@ def asap_steps(progs, msgs=None, eager_limit=MPICH_EAGER_LIMIT, info=None):
                     if not _try_wait(r, [q for q in op[1] if (r, q) not in eager],
                                      by_post, msgs, post_epoch, step, epoch):
                         break
+                elif k in ("c", "C"):
+                    # memcpy: after everything the rank completed (epoch), after the last copy
+                    # that wrote its source, after the last copy that read its destination; what
+                    # the rank posts next moves no earlier than the copy (DESIGN.md "copy steps")
+                    sb, db = ("SEND", "RECV") if k == "c" else (op[1], op[3])
+                    cs = max(epoch[r] + 1, last_w[r].get(sb, NEG) + 1, last_r[r].get(db, NEG) + 1)
+                    last_w[r][db] = max(last_w[r].get(db, NEG), cs)
+                    last_r[r][sb] = max(last_r[r].get(sb, NEG), cs)
+                    epoch[r] = max(epoch[r], cs - 1)
+                    copy_steps.append((r, cs))
                 pc[r] += 1
                 progress = True
             if pc[r] == len(ops):
                 done[r] = True
     if not all(done):
         raise RuntimeError("deadlock: ranks %s blocked" % [r for r in range(P) if not done[r]])
-    nsteps = max([s for s in step if s is not None] + [-1]) + 1
+    nsteps = max([s for s in step if s is not None] + [c for _, c in copy_steps] + [-1]) + 1
     if info is not None:
         info["barrier_epochs"] = barrier_epochs
+        info["copy_steps"] = copy_steps
     return step, nsteps
 
 

@@ -46,4 +46,12 @@ def load_golden(name):
         rows = gzip.open(os.path.join(p, "data_%s.csv.gz" % direction), "rt").read().split("\n")[1:]
         data[direction] = {tuple(map(int, r.split(",")[:3])): (int(r.split(",")[3]), int(r.split(",")[4], 16))
                            for r in rows if r}
+    # m15/m16 (TAM): per (method, iter, rank) the received messages in completion order
+    data["tam"] = {}
+    tp = os.path.join(p, "data_tam.csv.gz")
+    if os.path.exists(tp):
+        for r in gzip.open(tp, "rt").read().split("\n")[1:]:
+            if r:
+                m, it, rank, _k, src, cnt, chk = r.split(",")
+                data["tam"].setdefault((int(m), int(it), int(rank)), []).append((int(src), int(cnt), int(chk, 16)))
     return meta, traces, data

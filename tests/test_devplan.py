@@ -15,6 +15,7 @@ CASES = [  # P, A, d, c, ntimes, type, proc_node
     (24, 7, 16, 1, 1, 3, 4),       # unsorted aggregator list
     (16, 16, 8, 5, 1, 0, 1),       # every rank an aggregator
     (13, 4, 33, 200000000, 2, 1, 1),
+    (18, 5, 20, 4, 2, 1, 5),       # TAM nodes of 5, 5, 5, 3 ranks
 ]
 
 

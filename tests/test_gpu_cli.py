@@ -42,7 +42,7 @@ def test_cli_verify_all_methods(pkg, tmp_path):
                          capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert out.returncode == 0, out.stderr[-2000:]
     verdicts = re.findall(r"verify = (\w+)", out.stdout)
-    assert len(verdicts) == 36 and set(verdicts) == {"OK"}, out.stdout[-3000:]
+    assert len(verdicts) == 40 and set(verdicts) == {"OK"}, out.stdout[-3000:]
 
 
 def test_cli_refuses_reference_deadlock(pkg, tmp_path):

@@ -48,7 +48,7 @@ def test_golden_all_methods(xg, ctx, cfg):
                 run.close()
 
 
-@pytest.mark.parametrize("method", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 17, 18, 19, 20])
+@pytest.mark.parametrize("method", list(range(1, 21)))
 def test_strong_fingerprint(xg, ctx, method):
     """Collision-free fingerprint: catches misroutes MAP_DATA cannot (equal rank+seed)."""
     import xg_oracle as O
@@ -84,3 +84,34 @@ def test_readback_matches_oracle_bytes(xg, ctx):
                 assert (got == buf).all(), (method, r)
         finally:
             run.close()
+
+
+@pytest.mark.parametrize("method", [15, 16])
+def test_tam_aggregation_buffers_match_oracle(xg, ctx, method):
+    """TAM (collective_write): besides the receive slots, the intermediate aggregation
+    buffers of every rank (aggregate_buf | send_buf2 | recv_buf in SCRATCH) hold exactly
+    what the oracle's MPI execution leaves in them -- the same bytes the PMPI capture of
+    the reference checksums message by message (tests/test_oracle.py)."""
+    import numpy as np
+    import xg_oracle as O
+    P, A, d, c, k, pn, it = 18, 5, 1000, 3, 2, 5, 1
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=pn, iteration=it)
+    run = xg.MethodRun(ctx, s, it=it, mode=1)
+    try:
+        run.run_timed()
+        _chk, bad, _f = run.verify()
+        assert all(b == 0 for b in bad)
+        bufs = {}
+        O.execute(method, P, A, d, rl, O.programs(method, P, A, d, c, rl, k, pn, it=it), it, mode=1, buffers=bufs)
+        for r in range(P):
+            base = s.scratch_offset(1, r)
+            off = 0
+            for name in ("AGG", "SBUF2", "RBUF"):
+                ref = bufs[r].get(name, np.zeros(0, np.uint8))
+                if ref.size:
+                    got = np.frombuffer(run.read(xg.BUF_SCRATCH, base + off, ref.size), dtype=np.uint8)
+                    assert (got == ref).all(), (method, r, name)
+                off += (ref.size + 255) // 256 * 256
+    finally:
+        run.close()

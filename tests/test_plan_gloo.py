@@ -37,15 +37,17 @@ def _worker(rank, world, port, results):
                                    (16, 4, 32, 200000000, 1, 5), (12, 5, 48, 2, 1, 6), (16, 6, 40, 3, 1, 9),
                                    (12, 5, 16, 2, 2, 11), (16, 5, 56, 3, 1, 12), (12, 5, 32, 3, 2, 13),
                                    (12, 4, 24, 5, 1, 14), (16, 5, 40, 3, 1, 17), (12, 5, 48, 4, 2, 18),
-                                   (12, 5, 16, 3, 1, 19), (16, 6, 40, 5, 1, 20)]:
+                                   (12, 5, 16, 3, 1, 19), (16, 6, 40, 5, 1, 20), (12, 5, 40, 3, 2, 15),
+                                   (16, 5, 24, 3, 1, 16)]:
             rl = xg.aggregator_list(P, A)
-            s = xg.Schedule(m, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2)
+            s = xg.Schedule(m, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2, iteration=2)
             for pack in (0, 1 << 20):
                 v = s.devplan(world, rank, pack)
                 reg = make_regions(s, v, world, rank, 2, 1)
                 seq = {}
                 for st in range(v.nsteps):
-                    pre, p2p, post = step_parts(v, st)
+                    stage, pre, p2p, post = step_parts(v, st)
+                    copies(reg, stage)
                     copies(reg, pre)
                     reqs, bufs = [], []
                     for peer, is_send, buf, off, ln in p2p:
