@@ -52,6 +52,12 @@ int xg_get_unique_id(void *uid /* XG_UNIQUE_ID_BYTES */);
 /* rank/nranks: this process in the job (one per GPU).  device: HIP ordinal.
  * uid: from rank 0's xg_get_unique_id (ignored when nranks == 1). */
 int xg_init(xg_ctx **out, int rank, int nranks, int device, const void *uid);
+/* Test hook: GPU `rank` of an `nranks`-GPU job emulated on physical `device`
+ * in this process (no RCCL).  Its plans run only via xg_vplans_run, which
+ * executes every GPU of the job on one device and moves each RCCL send/recv
+ * pair (xg_p2p) as a device-to-device copy -- the multi-GPU device plans,
+ * packing and unpacking exercised on one MI355X.  Barrier / MAX are local. */
+int xg_init_virtual(xg_ctx **out, int rank, int nranks, int device);
 int xg_finalize(xg_ctx *ctx);
 int xg_rank(const xg_ctx *ctx);
 int xg_nranks(const xg_ctx *ctx);
@@ -92,6 +98,9 @@ int xg_plan_nsteps(const xg_plan *p);
 int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall);
 /* Enqueue all steps once without events or synchronisation (bench loops). */
 int xg_plan_enqueue(xg_plan *p);
+/* plans[g] = GPU g's plan of one virtual job (xg_init_virtual, g = 0..n-1, same
+ * schedule); step_done[nsteps]: device seconds from start to the end of each step. */
+int xg_vplans_run(xg_plan *const *plans, int n, double *step_done);
 /* Kernel timing session: while active, every copy_kernel launch of any plan
  * on this context is bracketed by HIP events on the stream it runs on.
  * xg_ktime_end waits for the stream and returns the summed kernel time (ms),

@@ -173,7 +173,22 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_cu4;
 typedef __attribute__((address_space(1))) u32x4 g_u4;
 
-template <int U>
+// LP / SP: load / store cache policy, 0 = default, 1 = nontemporal (`nt` bit)
+template <int LP>
+__device__ __forceinline__ u32x4 ld16(g_cu4 *p)
+{
+    if constexpr (LP == 1) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int SP>
+__device__ __forceinline__ void st16g(g_u4 *p, u32x4 v)
+{
+    if constexpr (SP == 1) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int U, int LP = 0, int SP = 0>
 __device__ __forceinline__ void pipelined_copy16(g_cu4 *__restrict__ s4, g_u4 *__restrict__ t4, int64_t n4)
 {
     int64_t i = threadIdx.x;
@@ -181,30 +196,30 @@ __device__ __forceinline__ void pipelined_copy16(g_cu4 *__restrict__ s4, g_u4 *_
     if (i + (U - 1) * (int64_t)kThreads < n4) {
         u32x4 cur[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = s4[i + u * kThreads];
+        for (int u = 0; u < U; ++u) cur[u] = ld16<LP>(s4 + i + u * kThreads);
         for (; i + step + (U - 1) * (int64_t)kThreads < n4; i += step) {
             u32x4 nxt[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) nxt[u] = s4[i + step + u * kThreads];
+            for (int u = 0; u < U; ++u) nxt[u] = ld16<LP>(s4 + i + step + u * kThreads);
 #pragma unroll
-            for (int u = 0; u < U; ++u) t4[i + u * kThreads] = cur[u];
+            for (int u = 0; u < U; ++u) st16g<SP>(t4 + i + u * kThreads, cur[u]);
 #pragma unroll
             for (int u = 0; u < U; ++u) cur[u] = nxt[u];
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) t4[i + u * kThreads] = cur[u];
+        for (int u = 0; u < U; ++u) st16g<SP>(t4 + i + u * kThreads, cur[u]);
         i += step;
     }
-    for (; i < n4; i += kThreads) t4[i] = s4[i];
+    for (; i < n4; i += kThreads) st16g<SP>(t4 + i, ld16<LP>(s4 + i));
 }
 
-template <int U>
+template <int U, int LP = 0, int SP = 0>
 __global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restrict__ pieces)
 {
     const DCopy c = pieces[blockIdx.x];
     const int64_t n = c.len;
     if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)n) & 15) == 0) {
-        pipelined_copy16<U>((g_cu4 *)c.src, (g_u4 *)c.dst, n >> 4);
+        pipelined_copy16<U, LP, SP>((g_cu4 *)c.src, (g_u4 *)c.dst, n >> 4);
     } else {
         for (int64_t i = threadIdx.x; i < n; i += kThreads) c.dst[i] = c.src[i];
     }

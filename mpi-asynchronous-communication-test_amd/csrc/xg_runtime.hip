@@ -45,6 +45,7 @@
 
 struct xg_ctx {
     int rank, nranks, device;
+    bool virt;              // xg_init_virtual: one of nranks GPUs emulated on one device, no RCCL
     hipStream_t stream;
     ncclComm_t comm;
     double *d_red;          // device scratch for barrier / MAX reductions
@@ -109,7 +110,7 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     }
     HIPCHK(hipSetDevice(device));
     xg_ctx *c = new xg_ctx();
-    c->rank = rank; c->nranks = nranks; c->device = device; c->comm = nullptr;
+    c->rank = rank; c->nranks = nranks; c->device = device; c->comm = nullptr; c->virt = false;
     c->chunk = 32768; c->variant = 5; c->kt_on = false; c->nk = 0;   // measured best: profiles/r01_copy_ab.txt
     const char *env = getenv("XG_COPY_CHUNK");
     if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
@@ -124,6 +125,25 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
         NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
     }
     *out = c;
+    return XG_OK;
+}
+
+// GPU `rank` of an `nranks`-GPU job, emulated on physical `device` inside this
+// process: same regions, plans and kernels as a real rank, no communicator.
+// Its cross-GPU ops are executed only by xg_vplans_run (all GPUs of the job
+// together), which moves each RCCL send/recv pair as a device copy.
+extern "C" int xg_init_virtual(xg_ctx **out, int rank, int nranks, int device)
+{
+    int rc = xg_init(out, 0, 1, device, nullptr);
+    if (rc) return rc;
+    if (nranks < 1 || rank < 0 || rank >= nranks) {
+        xg_finalize(*out);
+        *out = nullptr;
+        return XG_EARG;
+    }
+    (*out)->rank = rank;
+    (*out)->nranks = nranks;
+    (*out)->virt = true;
     return XG_OK;
 }
 
@@ -159,7 +179,7 @@ extern "C" int xg_device_sync(xg_ctx *c)
 extern "C" int xg_allreduce_max(xg_ctx *c, double *vals, int n)
 {
     if (n < 0) return XG_EARG;
-    if (c->nranks == 1 || n == 0) return XG_OK;
+    if (c->nranks == 1 || n == 0 || c->virt) return XG_OK;   // virtual: one process holds every GPU
     double *buf = c->d_red;
     if (n > 64) HIPCHK(hipMalloc(&buf, sizeof(double) * n));
     HIPCHK(hipMemcpyAsync(buf, vals, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
@@ -173,7 +193,7 @@ extern "C" int xg_allreduce_max(xg_ctx *c, double *vals, int n)
 extern "C" int xg_barrier(xg_ctx *c)
 {
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->nranks > 1) {
+    if (c->nranks > 1 && !c->virt) {
         NCCLCHK(ncclAllReduce(c->d_red, c->d_red, 1, ncclFloat64, ncclMax, c->comm, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
     }
@@ -421,9 +441,8 @@ extern "C" int xg_plan_free(xg_plan *p)
 
 extern "C" int xg_plan_nsteps(const xg_plan *p) { return p->nsteps; }
 
-static int launch_copy(xg_plan *p, int b, int n)
+static int launch_copy(xg_plan *p, int b, int n, hipStream_t st)
 {
-    hipStream_t st = p->ctx->stream;
     const xgk::DCopy *pc = p->d_pieces + b;
     switch (p->variant) {
     case 1: hipLaunchKernelGGL((xgk::copy_kernel<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
@@ -432,6 +451,11 @@ static int launch_copy(xg_plan *p, int b, int n)
     case 4: hipLaunchKernelGGL((xgk::copy_kernel<2, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 5: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 6: hipLaunchKernelGGL((xgk::copy_kernel_g<2>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 7: hipLaunchKernelGGL((xgk::copy_kernel_g<4, 1, 0>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 8: hipLaunchKernelGGL((xgk::copy_kernel_g<4, 1, 1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 9: hipLaunchKernelGGL((xgk::copy_kernel_g<4, 0, 1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 10: hipLaunchKernelGGL((xgk::copy_kernel_g<8>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 11: hipLaunchKernelGGL((xgk::copy_kernel_g<8, 1, 1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 0: hipLaunchKernelGGL((xgk::copy_kernel<4, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     }
@@ -439,24 +463,48 @@ static int launch_copy(xg_plan *p, int b, int n)
     return XG_OK;
 }
 
+// one copy launch, bracketed by kernel-timing events when a session is on
+static int timed_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t stream)
+{
+    xg_ctx *c = p->ctx;
+    int rc;
+    const bool kt = c->kt_on && 2 * (size_t)c->nk + 1 < c->kev.size();
+    if (kt) HIPCHK(hipEventRecord(c->kev[2 * c->nk], stream));
+    if ((rc = launch_copy(p, b, n, stream))) return rc;
+    if (kt) {
+        HIPCHK(hipEventRecord(c->kev[2 * c->nk + 1], stream));
+        c->kbytes[c->nk] = 2 * bytes;      // algorithmic HBM bytes: read + write
+        c->nk++;
+    }
+    return XG_OK;
+}
+
+// step parts 1 (stage + pre copies) and 3 (post copies)
+static int enqueue_pre(xg_plan *p, int s, hipStream_t stream)
+{
+    const StepR &st = p->steps[s];
+    int rc;
+    if (st.stage_n && (rc = timed_copy(p, st.stage_b, st.stage_n, st.stage_bytes, stream))) return rc;
+    if (st.pre_n && (rc = timed_copy(p, st.pre_b, st.pre_n, st.pre_bytes, stream))) return rc;
+    return XG_OK;
+}
+
+static int enqueue_post(xg_plan *p, int s, hipStream_t stream)
+{
+    const StepR &st = p->steps[s];
+    return st.post_n ? timed_copy(p, st.post_b, st.post_n, st.post_bytes, stream) : XG_OK;
+}
+
 static int enqueue_step(xg_plan *p, int s)
 {
     xg_ctx *c = p->ctx;
     const StepR &st = p->steps[s];
     int rc;
-    auto timed = [&](int b, int n, int64_t bytes) -> int {
-        const bool kt = c->kt_on && 2 * (size_t)c->nk + 1 < c->kev.size();
-        if (kt) HIPCHK(hipEventRecord(c->kev[2 * c->nk], c->stream));
-        if ((rc = launch_copy(p, b, n))) return rc;
-        if (kt) {
-            HIPCHK(hipEventRecord(c->kev[2 * c->nk + 1], c->stream));
-            c->kbytes[c->nk] = 2 * bytes;      // algorithmic HBM bytes: read + write
-            c->nk++;
-        }
-        return XG_OK;
-    };
-    if (st.stage_n && (rc = timed(st.stage_b, st.stage_n, st.stage_bytes))) return rc;
-    if (st.pre_n && (rc = timed(st.pre_b, st.pre_n, st.pre_bytes))) return rc;
+    if (c->virt && (st.p2p_n || st.sync_after)) {
+        fprintf(stderr, "xg: a virtual GPU's cross-GPU step runs only through xg_vplans_run\n");
+        return XG_EARG;
+    }
+    if ((rc = enqueue_pre(p, s, c->stream))) return rc;
     if (st.p2p_n) {
         NCCLCHK(ncclGroupStart());
         for (int i = 0; i < st.p2p_n; ++i) {
@@ -469,7 +517,7 @@ static int enqueue_step(xg_plan *p, int s)
         }
         NCCLCHK(ncclGroupEnd());
     }
-    if (st.post_n && (rc = timed(st.post_b, st.post_n, st.post_bytes))) return rc;
+    if ((rc = enqueue_post(p, s, c->stream))) return rc;
     if (st.sync_after)   /* in-loop MPI_Barrier: every GPU finishes this step before any goes on */
         NCCLCHK(ncclAllReduce(c->d_red, c->d_red, 1, ncclFloat64, ncclMax, c->comm, c->stream));
     return XG_OK;
@@ -504,6 +552,76 @@ extern "C" int xg_plan_enqueue(xg_plan *p)
     int rc;
     for (int s = 0; s < p->nsteps; ++s)
         if ((rc = enqueue_step(p, s))) return rc;
+    return XG_OK;
+}
+
+// Every GPU of a virtual job (xg_init_virtual), step by step on plans[0]'s
+// stream: all pre copies, then each RCCL send/recv pair as one device copy
+// (sends of g to h matched in order with h's receives from g -- RCCL's
+// per-peer FIFO inside a group), then all post copies, then the step event.
+// step_done[s] = device seconds from the start to the end of step s.
+extern "C" int xg_vplans_run(xg_plan *const *plans, int n, double *step_done)
+{
+    if (!plans || n < 1) return XG_EARG;
+    xg_ctx *c0 = plans[0]->ctx;
+    const int nst = plans[0]->nsteps;
+    for (int g = 0; g < n; ++g) {
+        const xg_ctx *c = plans[g]->ctx;
+        if (!c->virt || c->nranks != n || c->rank != g || c->device != c0->device || plans[g]->nsteps != nst) {
+            fprintf(stderr, "xg_vplans_run: plan %d is not GPU %d of one %d-GPU virtual job\n", g, g, n);
+            return XG_EARG;
+        }
+    }
+    int rc;
+    hipStream_t st = c0->stream;
+    HIPCHK(hipSetDevice(c0->device));
+    for (int g = 0; g < n; ++g) HIPCHK(hipStreamSynchronize(plans[g]->ctx->stream));
+    HIPCHK(hipEventRecord(plans[0]->ev0, st));
+    std::vector<std::vector<const xg_p2p *>> sends((size_t)n * n), recvs((size_t)n * n);
+    for (int s = 0; s < nst; ++s) {
+        for (int g = 0; g < n; ++g)
+            if ((rc = enqueue_pre(plans[g], s, st))) return rc;
+        for (auto &v : sends) v.clear();
+        for (auto &v : recvs) v.clear();
+        for (int g = 0; g < n; ++g) {
+            const StepR &sr = plans[g]->steps[s];
+            for (int i = 0; i < sr.p2p_n; ++i) {
+                const xg_p2p &o = plans[g]->p2p[sr.p2p_b + i];
+                if (o.is_send) sends[(size_t)g * n + o.peer].push_back(&o);
+                else recvs[(size_t)o.peer * n + g].push_back(&o);
+            }
+        }
+        for (int g = 0; g < n; ++g)
+            for (int h = 0; h < n; ++h) {
+                const auto &sv = sends[(size_t)g * n + h], &rv = recvs[(size_t)g * n + h];
+                if (sv.size() != rv.size()) {
+                    fprintf(stderr, "xg_vplans_run: step %d: GPU %d posts %zu sends to %d, which posts %zu receives\n",
+                            s, g, sv.size(), h, rv.size());
+                    return XG_EARG;
+                }
+                for (size_t k = 0; k < sv.size(); ++k) {
+                    if (sv[k]->len != rv[k]->len) {
+                        fprintf(stderr, "xg_vplans_run: step %d: %d->%d op %zu: send %lld B, receive %lld B\n", s,
+                                g, h, k, (long long)sv[k]->len, (long long)rv[k]->len);
+                        return XG_EARG;
+                    }
+                    if (sv[k]->len)
+                        HIPCHK(hipMemcpyAsync(plans[h]->reg->ptr[rv[k]->buf] + rv[k]->off,
+                                              plans[g]->reg->ptr[sv[k]->buf] + sv[k]->off, (size_t)sv[k]->len,
+                                              hipMemcpyDeviceToDevice, st));
+                }
+            }
+        for (int g = 0; g < n; ++g)
+            if ((rc = enqueue_post(plans[g], s, st))) return rc;
+        HIPCHK(hipEventRecord(plans[0]->ev[s], st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    if (step_done)
+        for (int s = 0; s < nst; ++s) {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, plans[0]->ev0, plans[0]->ev[s]));
+            step_done[s] = ms * 1e-3;
+        }
     return XG_OK;
 }
 

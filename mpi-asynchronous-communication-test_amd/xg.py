@@ -288,6 +288,8 @@ def device():
         d.xg_get_unique_id.argtypes = [vp]
         d.xg_init.argtypes = [C.POINTER(vp), ip, ip, ip, vp]
         d.xg_finalize.argtypes = [vp]
+        d.xg_init_virtual.argtypes = [C.POINTER(vp), ip, ip, ip]
+        d.xg_vplans_run.argtypes = [C.POINTER(vp), ip, C.POINTER(C.c_double)]
         d.xg_barrier.argtypes = [vp]
         d.xg_sync.argtypes = [vp]
         d.xg_device_sync.argtypes = [vp]
@@ -338,6 +340,16 @@ class Context:
         ub = C.create_string_buffer(uid, 128) if uid else None
         _check(d.xg_init(C.byref(self._c), rank, nranks, dev, ub), "xg_init")
         self.rank, self.nranks = rank, nranks
+
+    @classmethod
+    def virtual(cls, rank, nranks, device=0):
+        """GPU `rank` of an `nranks`-GPU job emulated on one physical device (test hook,
+        xg_init_virtual); run the job's plans together with run_virtual()."""
+        self = cls.__new__(cls)
+        self._c = C.c_void_p()
+        _check(globals()["device"]().xg_init_virtual(C.byref(self._c), rank, nranks, device), "xg_init_virtual")
+        self.rank, self.nranks = rank, nranks
+        return self
 
     @property
     def handle(self):
@@ -392,6 +404,17 @@ class Context:
 
 def now():
     return device().xg_now()
+
+
+def run_virtual(runs):
+    """Execute the MethodRuns of every GPU of one virtual job (runs[g] on Context.virtual(g, n))
+    step by step on one device; returns step_done[] (device seconds)."""
+    n = len(runs)
+    arr = (C.c_void_p * n)(*[r._p for r in runs])
+    nst = max(1, runs[0].nsteps)
+    done = (C.c_double * nst)()
+    _check(device().xg_vplans_run(arr, n, done), "xg_vplans_run")
+    return list(done)[:runs[0].nsteps]
 
 
 class MethodRun:

@@ -1,0 +1,84 @@
+"""Multi-GPU device plans on one MI355X: every GPU of a G-GPU job is emulated on
+the one device (xg_init_virtual), each with its own regions, fill, plan and
+copy-kernel launches; the RCCL send/recv pairs of each step are moved as device
+copies in RCCL's per-peer order (xg_vplans_run).  This runs the exact per-GPU
+plans the driver's 2/4/8-GPU bench executes (local gather/scatter, packing
+into per-peer staging, unpacking) on the hardware, and checks every received
+segment against the checksums captured from the real reference.
+
+What it does not exercise is RCCL itself (the box has one GPU, and RCCL refuses
+two ranks on one device); tests/test_plan_gloo.py runs the same plans across
+two processes on CPU.
+"""
+import pytest
+
+from conftest import golden_configs, load_golden
+
+pytestmark = pytest.mark.gpu
+
+GPUS = (2, 3, 8)
+
+
+@pytest.fixture(scope="module")
+def worlds(xg):
+    w = {G: [xg.Context.virtual(g, G, device=0) for g in range(G)] for G in GPUS}
+    yield w
+    for ctxs in w.values():
+        for c in ctxs:
+            c.close()
+
+
+def _run_job(xg, ctxs, s, it, mode, pack):
+    runs = [xg.MethodRun(c, s, it=it, mode=mode, pack_max_seg=pack) for c in ctxs]
+    try:
+        done = xg.run_virtual(runs)
+        assert all(b >= a for a, b in zip(done, done[1:]))
+        out = []
+        for r in runs:
+            chk, bad, first = r.verify()
+            out += list(zip(r.slots, chk, bad, first))
+        return out
+    finally:
+        for r in runs:
+            r.close()
+
+
+@pytest.mark.parametrize("G", GPUS)
+@pytest.mark.parametrize("cfg", golden_configs())
+def test_golden_multi_gpu(xg, worlds, cfg, G):
+    meta, _traces, data = load_golden(cfg)
+    import xg_oracle as O
+    P, A, d, c, k = meta["P"], meta["A"], meta["d"], meta["c"], meta["ntimes"]
+    if G > P:
+        pytest.skip("more GPUs than ranks")
+    rl = xg.aggregator_list(P, A, meta["proc_node"], meta["type"])
+    it = meta["iters"] - 1
+    for method in meta["method_list"]:
+        direction = O.direction(method)
+        s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=meta["proc_node"],
+                        barrier_type=meta.get("barrier", 0), iteration=it)
+        for pack in (0, 1 << 30):          # never pack / pack every multi-segment peer transfer
+            res = _run_job(xg, worlds[G], s, it, 0, pack)
+            assert len(res) == sum(1 for key in data[direction] if key[0] == it), (cfg, method, G)
+            for (src, seed, dst, off), ck, nb, fb in res:
+                assert nb == 0, "%s G%d m%d pack%d %d->%d: %d bad bytes from %d" % (cfg, G, method, pack, src, dst,
+                                                                                     nb, fb)
+                glen, gchk = data[direction][(it, src, dst)]
+                assert ck == gchk, (cfg, G, method, pack, src, dst, hex(ck), hex(gchk))
+
+
+@pytest.mark.parametrize("G", GPUS)
+@pytest.mark.parametrize("method", list(range(1, 21)))
+def test_strong_fingerprint_multi_gpu(xg, worlds, G, method):
+    """Collision-free fingerprint across GPU boundaries (unaligned d, packed staging)."""
+    import xg_oracle as O
+    P, A, d, c, k, it = 20, 6, 1000, 7, 2, 3
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2, iteration=it)
+    exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
+    res = _run_job(xg, worlds[G], s, it, 1, 1 << 20)
+    assert res
+    for (src, seed, dst, off), ck, nb, _fb in res:
+        assert nb == 0, (method, G, src, dst)
+        local = off - s.recv_offset(G, dst)
+        assert ck == O.chk64(exp[dst][local: local + d]), (method, G, src, dst)
