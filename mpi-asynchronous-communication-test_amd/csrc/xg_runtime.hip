@@ -47,6 +47,7 @@ struct xg_ctx {
     int rank, nranks, device;
     bool virt;              // xg_init_virtual: one of nranks GPUs emulated on one device, no RCCL
     hipStream_t stream;
+    hipStream_t side;       // local gather/scatter of a step that also talks to other GPUs (overlaps RCCL)
     ncclComm_t comm;
     double *d_red;          // device scratch for barrier / MAX reductions
     int64_t chunk;          // bytes per copy workgroup
@@ -65,8 +66,12 @@ struct xg_regions {
 };
 
 struct StepR {
-    int stage_b, stage_n, pre_b, pre_n, post_b, post_n, p2p_b, p2p_n, sync_after;
-    int64_t stage_bytes, pre_bytes, post_bytes;   // bytes copied by each launch (read once + written once)
+    // pre = [local gather/scatter pieces | pack-into-staging pieces], one launch
+    // unless the step also has cross-GPU ops: then the local part runs on the side
+    // stream beside the RCCL group and only the packs precede it (split).
+    int stage_b, stage_n, pre_b, pre_n, local_n, post_b, post_n, p2p_b, p2p_n, sync_after;
+    int64_t stage_bytes, local_bytes, pack_bytes, post_bytes;   // bytes copied by each launch (read + written once)
+    bool split;
 };
 
 struct xg_plan {
@@ -78,6 +83,7 @@ struct xg_plan {
     std::vector<StepR> steps;
     std::vector<xg_p2p> p2p;
     std::vector<hipEvent_t> ev;
+    std::vector<hipEvent_t> fork, join;   // per split step: main -> side, side -> main
     hipEvent_t ev0;
     int variant;
 };
@@ -117,6 +123,7 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     env = getenv("XG_COPY_VARIANT");
     if (env) c->variant = atoi(env);
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_red, 64 * sizeof(double)));
     if (nranks > 1) {
         ncclUniqueId id;
@@ -155,6 +162,8 @@ extern "C" int xg_finalize(xg_ctx *c)
     if (c->comm) NCCLCHK(ncclCommDestroy(c->comm));
     for (auto &e : c->kev) HIPCHK(hipEventDestroy(e));
     HIPCHK(hipFree(c->d_red));
+    HIPCHK(hipStreamSynchronize(c->side));
+    HIPCHK(hipStreamDestroy(c->side));
     HIPCHK(hipStreamDestroy(c->stream));
     delete c;
     return XG_OK;
@@ -389,11 +398,18 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.stage_bytes = 0;
         for (int i = st.stage_b; i < st.stage_b + st.stage_n; ++i) st.stage_bytes += pieces[i].len;
         st.pre_b = (int)pieces.size();
-        for (int i = sp.stage_count; i < sp.pre_count; ++i)
-            if (!add(dp->copies[sp.pre_begin + i])) goto bad;
+        st.local_bytes = st.pack_bytes = 0;
+        for (int i = sp.stage_count; i < sp.pre_count; ++i) {
+            const xg_copy &cp = dp->copies[sp.pre_begin + i];
+            const bool pack = cp.dst_buf == XG_BUF_STAGE_SEND;   // the plan lists local copies, then packs
+            const int before = (int)pieces.size();
+            if (!pack && st.pack_bytes) goto bad;
+            if (!add(cp)) goto bad;
+            for (int k = before; k < (int)pieces.size(); ++k) (pack ? st.pack_bytes : st.local_bytes) += pieces[k].len;
+            if (!pack) st.local_n = (int)pieces.size() - st.pre_b;
+        }
         st.pre_n = (int)pieces.size() - st.pre_b;
-        st.pre_bytes = 0;
-        for (int i = st.pre_b; i < st.pre_b + st.pre_n; ++i) st.pre_bytes += pieces[i].len;
+        if (!st.local_bytes) st.local_n = 0;
         st.post_b = (int)pieces.size();
         for (int i = 0; i < sp.post_count; ++i)
             if (!add(dp->copies[sp.post_begin + i])) goto bad;
@@ -410,6 +426,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         }
         st.p2p_n = (int)p->p2p.size() - st.p2p_b;
         st.sync_after = sp.sync_after && c->nranks > 1;
+        st.split = st.p2p_n > 0 && st.local_n > 0;
     }
     p->npieces = (int)pieces.size();
     p->d_pieces = nullptr;
@@ -419,6 +436,13 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     }
     p->ev.resize(dp->nsteps);
     for (auto &e : p->ev) HIPCHK(hipEventCreate(&e));
+    p->fork.assign(dp->nsteps, nullptr);
+    p->join.assign(dp->nsteps, nullptr);
+    for (int s = 0; s < dp->nsteps; ++s)
+        if (p->steps[s].split) {
+            HIPCHK(hipEventCreateWithFlags(&p->fork[s], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&p->join[s], hipEventDisableTiming));
+        }
     HIPCHK(hipEventCreate(&p->ev0));
     *out = p;
     return XG_OK;
@@ -433,7 +457,10 @@ extern "C" int xg_plan_free(xg_plan *p)
     if (!p) return XG_OK;
     HIPCHK(hipStreamSynchronize(p->ctx->stream));
     if (p->d_pieces) HIPCHK(hipFree(p->d_pieces));
+    HIPCHK(hipStreamSynchronize(p->ctx->side));
     for (auto &e : p->ev) HIPCHK(hipEventDestroy(e));
+    for (auto &e : p->fork) if (e) HIPCHK(hipEventDestroy(e));
+    for (auto &e : p->join) if (e) HIPCHK(hipEventDestroy(e));
     HIPCHK(hipEventDestroy(p->ev0));
     delete p;
     return XG_OK;
@@ -479,20 +506,36 @@ static int timed_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t strea
     return XG_OK;
 }
 
-// step parts 1 (stage + pre copies) and 3 (post copies)
-static int enqueue_pre(xg_plan *p, int s, hipStream_t stream)
+// step part 1: stage copies, then local gather/scatter + packs.  A split step
+// forks its local part onto `side`, where it runs beside the packs and the RCCL
+// group on `stream`; enqueue_post joins it back before the step ends.
+static int enqueue_pre(xg_plan *p, int s, hipStream_t stream, hipStream_t side)
 {
     const StepR &st = p->steps[s];
     int rc;
     if (st.stage_n && (rc = timed_copy(p, st.stage_b, st.stage_n, st.stage_bytes, stream))) return rc;
-    if (st.pre_n && (rc = timed_copy(p, st.pre_b, st.pre_n, st.pre_bytes, stream))) return rc;
+    if (st.split) {
+        HIPCHK(hipEventRecord(p->fork[s], stream));
+        HIPCHK(hipStreamWaitEvent(side, p->fork[s], 0));
+        if ((rc = timed_copy(p, st.pre_b, st.local_n, st.local_bytes, side))) return rc;
+        HIPCHK(hipEventRecord(p->join[s], side));
+        if (st.pre_n > st.local_n &&
+            (rc = timed_copy(p, st.pre_b + st.local_n, st.pre_n - st.local_n, st.pack_bytes, stream)))
+            return rc;
+    } else if (st.pre_n && (rc = timed_copy(p, st.pre_b, st.pre_n, st.local_bytes + st.pack_bytes, stream))) {
+        return rc;
+    }
     return XG_OK;
 }
 
+// step part 3: unpack out of staging, then wait for the forked local part
 static int enqueue_post(xg_plan *p, int s, hipStream_t stream)
 {
     const StepR &st = p->steps[s];
-    return st.post_n ? timed_copy(p, st.post_b, st.post_n, st.post_bytes, stream) : XG_OK;
+    int rc;
+    if (st.post_n && (rc = timed_copy(p, st.post_b, st.post_n, st.post_bytes, stream))) return rc;
+    if (st.split) HIPCHK(hipStreamWaitEvent(stream, p->join[s], 0));
+    return XG_OK;
 }
 
 static int enqueue_step(xg_plan *p, int s)
@@ -504,7 +547,7 @@ static int enqueue_step(xg_plan *p, int s)
         fprintf(stderr, "xg: a virtual GPU's cross-GPU step runs only through xg_vplans_run\n");
         return XG_EARG;
     }
-    if ((rc = enqueue_pre(p, s, c->stream))) return rc;
+    if ((rc = enqueue_pre(p, s, c->stream, c->side))) return rc;
     if (st.p2p_n) {
         NCCLCHK(ncclGroupStart());
         for (int i = 0; i < st.p2p_n; ++i) {
@@ -580,7 +623,7 @@ extern "C" int xg_vplans_run(xg_plan *const *plans, int n, double *step_done)
     std::vector<std::vector<const xg_p2p *>> sends((size_t)n * n), recvs((size_t)n * n);
     for (int s = 0; s < nst; ++s) {
         for (int g = 0; g < n; ++g)
-            if ((rc = enqueue_pre(plans[g], s, st))) return rc;
+            if ((rc = enqueue_pre(plans[g], s, st, plans[g]->ctx->side))) return rc;
         for (auto &v : sends) v.clear();
         for (auto &v : recvs) v.clear();
         for (int g = 0; g < n; ++g) {
