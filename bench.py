@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--comm-size", type=int, default=200000000)
     ap.add_argument("--methods", default="1,2,3,4")
     ap.add_argument("--pack-max-seg", type=int, default=4 << 20)
+    ap.add_argument("--tune-pack", type=int, default=-1,
+                    help="1/0: time direct vs packed cross-GPU plans per method and keep the faster "
+                         "(default: on when N > 1 and --pack-max-seg is left at its default)")
     ap.add_argument("--copy-variant", type=int, default=-1)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -165,22 +168,51 @@ def main():
     arch, cus, hbm = ctx.info()
 
     rl = xg.aggregator_list(a.procs, a.aggs)
-    runs, max_total = [], {}
+    runs, max_total, tune = [], {}, {}
+
+    def timed_reps(r, reps):
+        """device time of `reps` back-to-back runs of one method, MAX over GPUs"""
+        ctx.barrier()
+        ctx.device_sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r.enqueue()
+        ctx.device_sync()
+        return ctx.allreduce_max([time.perf_counter() - t0])[0] / reps
+
+    # N > 1: per method, pick by measurement whether cross-GPU segments go to RCCL
+    # one op per segment (direct) or packed into one staging buffer per peer
+    # (pack + unpack launches).  Every GPU sees the same MAX times -> same choice.
+    tune_on = a.tune_pack == 1 or (a.tune_pack < 0 and world > 1 and a.pack_max_seg == 4 << 20)
+    cands = [0, 4 << 20] if tune_on else [a.pack_max_seg]
     for m in methods:
         s = xg.Schedule(m, a.procs, a.aggs, a.size, a.comm_size, rl, ntimes=1)
-        r = xg.MethodRun(ctx, s, it=0, mode=0, pack_max_seg=a.pack_max_seg)
-        # parity gate + the reference's own timing report for this method
-        ctx.barrier()
-        done, post, _wall = r.run_timed()
-        lo, hi = s.block_range(world, rank)
-        tmax = max(s.rank_timer(q, done, post, world).total_time for q in range(lo, hi)) if hi > lo else 0.0
-        _chk, bad, _first = r.verify()
-        nbad = float(sum(1 for b in bad if b))
-        tmax, nbad = ctx.allreduce_max([tmax, nbad])
-        if nbad:
-            raise SystemExit("bench: method %d delivered wrong bytes on some GPU; refusing to time it" % m)
-        max_total[str(m)] = tmax
-        runs.append(r)
+        best = None
+        for pk in cands:
+            r = xg.MethodRun(ctx, s, it=0, mode=0, pack_max_seg=pk)
+            # parity gate + the reference's own timing report for this method
+            ctx.barrier()
+            done, post, _wall = r.run_timed()
+            lo, hi = s.block_range(world, rank)
+            tmax = max(s.rank_timer(q, done, post, world).total_time for q in range(lo, hi)) if hi > lo else 0.0
+            _chk, bad, _first = r.verify()
+            nbad = float(sum(1 for b in bad if b))
+            tmax, nbad = ctx.allreduce_max([tmax, nbad])
+            if nbad:
+                raise SystemExit("bench: method %d delivered wrong bytes on some GPU; refusing to time it" % m)
+            t = timed_reps(r, 5) if len(cands) > 1 else 0.0
+            if len(cands) > 1:
+                tune.setdefault(str(m), {})["packed_ms" if pk else "direct_ms"] = round(t * 1e3, 4)
+            if best is None or t < best[0]:
+                if best is not None:
+                    best[1].close()
+                best = (t, r, tmax, pk)
+            else:
+                r.close()
+        if len(cands) > 1:
+            tune[str(m)]["chosen"] = "packed" if best[3] else "direct"
+        max_total[str(m)] = best[2]
+        runs.append(best[1])
 
     def step():
         for r in runs:
@@ -190,7 +222,7 @@ def main():
         step()
     ctx.device_sync()
 
-    launches_per_step = sum(sum((st[1] > 0) + (st[5] > 0) for st in r.view.steps) for r in runs)
+    launches_per_step = sum(4 * len(r.view.steps) for r in runs)   # <= stage, local, pack, post per step
     ctx.barrier()
     ctx.device_sync()
     ctx.ktime_begin(max(1, launches_per_step * a.steps))
@@ -212,7 +244,7 @@ def main():
         cross_step = 0      # every rank derives every GPU's plan (deterministic, cheap)
         for r in runs:
             for g in range(world):
-                cross_step += r.sched.devplan(world, g, a.pack_max_seg).remote_send_bytes
+                cross_step += r.sched.devplan(world, g, r.pack_max_seg).remote_send_bytes
         per_pair = max(65536, (cross_step // max(1, len(methods) * world * (world - 1)) + 4095) & ~4095)
         ceil_gbps, _ = ctx.p2p_bench(per_pair, mode=0, reps=20)
         ceil_min = -ctx.allreduce_max([-ceil_gbps])[0]          # slowest GPU's egress
@@ -255,6 +287,7 @@ def main():
         "max_total_time_s": max_total,
         "roofline": roof,
         "xgmi": xgmi,
+        "pack_autotune_ms_per_run": tune or None,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out))

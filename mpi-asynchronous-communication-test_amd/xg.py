@@ -423,7 +423,7 @@ class MethodRun:
 
     def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20):
         d = device()
-        self.ctx, self.sched, self.it, self.mode = ctx, sched, it, mode
+        self.ctx, self.sched, self.it, self.mode, self.pack_max_seg = ctx, sched, it, mode, pack_max_seg
         G, g = ctx.nranks, ctx.rank
         self.view = sched.devplan(G, g, pack_max_seg)
         rb = (C.c_int64 * NBUF)(*self.view.region_bytes)
