@@ -115,7 +115,9 @@ def cpu_baseline_port(a, methods, note=""):
 def rendezvous_uid(xg, rank, world):
     port = os.environ.get("MASTER_PORT", "0")
     run = os.environ.get("TORCHELASTIC_RUN_ID", "")
-    path = "/tmp/xg_bench_rdzv_%s_%s.bin" % (port, re.sub(r"[^A-Za-z0-9_-]", "_", run))
+    # the launcher (torchrun agent) is the parent of every local rank: its pid keeps a
+    # stale file of an earlier launch on the same port from matching
+    path = "/tmp/xg_bench_rdzv_%s_%s_pp%d.bin" % (port, re.sub(r"[^A-Za-z0-9_-]", "_", run), os.getppid())
     t_start = time.time()
     if rank == 0:
         uid = xg.unique_id()

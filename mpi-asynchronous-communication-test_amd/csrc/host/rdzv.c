@@ -31,7 +31,9 @@ int xg_rendezvous(int rank, int nranks, unsigned char uid[XG_UNIQUE_ID_BYTES], c
     if (!dir) dir = "/tmp";
     if (!key) {
         const char *port = getenv("MASTER_PORT"), *run = getenv("TORCHELASTIC_RUN_ID");
-        if (port) snprintf(kbuf, sizeof kbuf, "p%s_%s", port, run ? run : "");
+        /* the launcher (torchrun agent / mpiexec proxy) is every local rank's parent:
+         * its pid keeps a stale file of an earlier launch on the same port from matching */
+        if (port) snprintf(kbuf, sizeof kbuf, "p%s_%s_pp%ld", port, run ? run : "", (long)getppid());
         else snprintf(kbuf, sizeof kbuf, "pp%ld", (long)getppid());
         key = kbuf;
     }
