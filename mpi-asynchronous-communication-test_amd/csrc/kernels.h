@@ -225,6 +225,70 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restric
     }
 }
 
+// ---------------------------------------------------------------- step engine
+// A GPU-local plan of many small steps (sync / pairwise / throttled schedules
+// at small -d) is bound by the per-step kernel boundary + timing event, not by
+// HBM.  The engine runs the whole plan in ONE launch of W co-resident
+// workgroups: step s = pieces [step_begin[s], step_begin[s+1]) strided over the
+// workgroups, then a grid barrier whose last arriver stamps the step's
+// completion time (wall clock).  No workgroup reads bytes another writes in
+// this launch (every piece reads SEND and writes RECV), so the barrier orders
+// and times steps but publishes no data: each workgroup drains its stores
+// (vmcnt(0)) before its arrival ticket, and the kernel end makes them visible.
+// State (cumulative ticket counter + timeout word) is zeroed by a memset before
+// every launch; spins are bounded, and a timed-out workgroup sets *tmo and
+// leaves, so a broken residency assumption ends the launch instead of hanging.
+struct EngineState {
+    unsigned count;     // arrival tickets, cumulative over the launch
+    unsigned tmo;       // != 0: some workgroup gave up waiting
+    unsigned pad[2];
+};
+
+typedef __attribute__((address_space(1))) unsigned g_u32;
+
+__global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__restrict__ pieces,
+                                                               const int *__restrict__ step_begin, int nsteps,
+                                                               EngineState *st, unsigned long long *stamps)
+{
+    const unsigned W = gridDim.x;
+    g_u32 *count = (g_u32 *)&st->count;
+    g_u32 *tmo = (g_u32 *)&st->tmo;
+    __shared__ int give_up;
+    if (threadIdx.x == 0) give_up = 0;
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const int e = step_begin[s + 1];
+        for (int i = step_begin[s] + (int)blockIdx.x; i < e; i += (int)W) {
+            const DCopy c = pieces[i];
+            if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
+                pipelined_copy16<4>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
+            else
+                for (int64_t k = threadIdx.x; k < c.len; k += kThreads) c.dst[k] = c.src[k];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores of step s performed
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned target = (unsigned)(s + 1) * W;
+            const unsigned t = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+            if (t == target) {
+                stamps[s] = (unsigned long long)wall_clock64();
+            } else {
+                unsigned spins = 0;
+                while (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 22) || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        give_up = 1;
+                        break;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (give_up) return;
+    }
+}
+
 // ---------------------------------------------------------------- balanced byte-range copy
 // The launch's copies form one virtual byte space [0, total) (prefix[k] =
 // start of copy k, an exclusive scan of the lengths).  Workgroup b streams the

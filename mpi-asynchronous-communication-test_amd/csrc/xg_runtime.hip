@@ -51,6 +51,9 @@ struct xg_ctx {
     ncclComm_t comm;
     double *d_red;          // device scratch for barrier / MAX reductions
     int64_t chunk;          // bytes per copy workgroup
+    int64_t engine_max_step;   // GPU-local plans whose largest step moves <= this many bytes use the step engine
+    int engine_wmax;           // at most this many (co-resident) engine workgroups
+    double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant
     // kernel timing session (xg_ktime_begin/end)
     bool kt_on;
@@ -86,6 +89,12 @@ struct xg_plan {
     std::vector<hipEvent_t> fork, join;   // per split step: main -> side, side -> main
     hipEvent_t ev0;
     int variant;
+    // step engine (one persistent launch for the whole plan), or engine_w == 0
+    int engine_w;
+    int *d_step_begin;
+    xgk::DCopy *d_epieces;         // the engine's work units, step-major
+    xgk::EngineState *d_engine;    // state (16 B, zeroed per launch) followed by nsteps stamps
+    int64_t engine_bytes;          // bytes copied per run
 };
 
 extern "C" double xg_now(void)
@@ -122,6 +131,17 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
     env = getenv("XG_COPY_VARIANT");
     if (env) c->variant = atoi(env);
+    c->engine_max_step = 4 << 20;     // crossover vs one launch per step: profiles/r01_engine_sweep.txt
+    env = getenv("XG_ENGINE_MAX_STEP");      // 0: never use the step engine
+    if (env) c->engine_max_step = atol(env);
+    env = getenv("XG_ENGINE_WG");
+    c->engine_wmax = env && atoi(env) > 0 ? atoi(env) : 256;    // one per CU
+    if (c->engine_wmax > 1024) c->engine_wmax = 1024;
+    {
+        int khz = 0;
+        HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+        c->wall_hz = khz > 0 ? khz * 1e3 : 1e8;
+    }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_red, 64 * sizeof(double)));
@@ -444,6 +464,41 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             HIPCHK(hipEventCreateWithFlags(&p->join[s], hipEventDisableTiming));
         }
     HIPCHK(hipEventCreate(&p->ev0));
+    p->engine_w = 0; p->d_step_begin = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->engine_bytes = 0;
+    {
+        bool ok = !c->virt && c->engine_max_step > 0 && p->nsteps >= 2;
+        for (const StepR &st : p->steps)
+            ok = ok && !st.p2p_n && !st.sync_after && !st.stage_n && !st.post_n &&
+                 st.local_bytes + st.pack_bytes <= c->engine_max_step;
+        if (ok) {
+            // the engine's work units: the step's pieces (<= chunk bytes), one per workgroup
+            // visit; smaller units and more than 256 workgroups measured slower
+            // (profiles/r01_engine_sweep.txt)
+            const int64_t unit = c->chunk;
+            std::vector<xgk::DCopy> ep;
+            std::vector<int> sb(p->nsteps + 1);
+            int maxu = 0;
+            for (int s = 0; s < p->nsteps; ++s) {
+                const StepR &st = p->steps[s];
+                sb[s] = (int)ep.size();
+                for (int i = st.pre_b; i < st.pre_b + st.pre_n; ++i)
+                    for (int64_t o = 0; o < pieces[i].len; o += unit)
+                        ep.push_back({pieces[i].src + o, pieces[i].dst + o,
+                                      pieces[i].len - o < unit ? pieces[i].len - o : unit});
+                if ((int)ep.size() - sb[s] > maxu) maxu = (int)ep.size() - sb[s];
+                p->engine_bytes += st.local_bytes + st.pack_bytes;
+            }
+            sb[p->nsteps] = (int)ep.size();
+            p->engine_w = maxu < 1 ? 1 : (maxu > c->engine_wmax ? c->engine_wmax : maxu);
+            HIPCHK(hipMalloc(&p->d_step_begin, sizeof(int) * sb.size()));
+            HIPCHK(hipMemcpy(p->d_step_begin, sb.data(), sizeof(int) * sb.size(), hipMemcpyHostToDevice));
+            if (!ep.empty()) {
+                HIPCHK(hipMalloc(&p->d_epieces, sizeof(xgk::DCopy) * ep.size()));
+                HIPCHK(hipMemcpy(p->d_epieces, ep.data(), sizeof(xgk::DCopy) * ep.size(), hipMemcpyHostToDevice));
+            }
+            HIPCHK(hipMalloc(&p->d_engine, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps));
+        }
+    }
     *out = p;
     return XG_OK;
 bad:
@@ -458,6 +513,9 @@ extern "C" int xg_plan_free(xg_plan *p)
     HIPCHK(hipStreamSynchronize(p->ctx->stream));
     if (p->d_pieces) HIPCHK(hipFree(p->d_pieces));
     HIPCHK(hipStreamSynchronize(p->ctx->side));
+    if (p->d_step_begin) HIPCHK(hipFree(p->d_step_begin));
+    if (p->d_epieces) HIPCHK(hipFree(p->d_epieces));
+    if (p->d_engine) HIPCHK(hipFree(p->d_engine));
     for (auto &e : p->ev) HIPCHK(hipEventDestroy(e));
     for (auto &e : p->fork) if (e) HIPCHK(hipEventDestroy(e));
     for (auto &e : p->join) if (e) HIPCHK(hipEventDestroy(e));
@@ -467,6 +525,7 @@ extern "C" int xg_plan_free(xg_plan *p)
 }
 
 extern "C" int xg_plan_nsteps(const xg_plan *p) { return p->nsteps; }
+extern "C" int xg_plan_engine(const xg_plan *p) { return p->engine_w; }
 
 static int launch_copy(xg_plan *p, int b, int n, hipStream_t st)
 {
@@ -566,11 +625,67 @@ static int enqueue_step(xg_plan *p, int s)
     return XG_OK;
 }
 
+// one launch of the step engine (state zeroed first); timed as one copy launch
+static int launch_engine(xg_plan *p)
+{
+    xg_ctx *c = p->ctx;
+    HIPCHK(hipMemsetAsync(p->d_engine, 0, sizeof(xgk::EngineState), c->stream));
+    const bool kt = c->kt_on && 2 * (size_t)c->nk + 1 < c->kev.size();
+    if (kt) HIPCHK(hipEventRecord(c->kev[2 * c->nk], c->stream));
+    hipLaunchKernelGGL(xgk::step_engine_kernel, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream, p->d_epieces,
+                       p->d_step_begin, p->nsteps, p->d_engine,
+                       reinterpret_cast<unsigned long long *>(p->d_engine + 1));
+    HIPCHK(hipGetLastError());
+    if (kt) {
+        HIPCHK(hipEventRecord(c->kev[2 * c->nk + 1], c->stream));
+        c->kbytes[c->nk] = 2 * p->engine_bytes;
+        c->nk++;
+    }
+    return XG_OK;
+}
+
+// after a synchronised engine run: per-step completion times from the wall-clock
+// stamps, anchored at the stream events around the launch
+static int engine_times(xg_plan *p, double *step_done)
+{
+    std::vector<unsigned long long> h(2 + (size_t)p->nsteps);
+    HIPCHK(hipMemcpy(h.data(), p->d_engine, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
+    const xgk::EngineState *es = reinterpret_cast<const xgk::EngineState *>(h.data());
+    if (es->tmo) {
+        fprintf(stderr, "xg: step engine: a workgroup timed out at a grid barrier (workgroups not co-resident?)\n");
+        return XG_EHIP;
+    }
+    if (step_done) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[p->nsteps - 1]));
+        const unsigned long long *st = h.data() + 2;
+        const double total = ms * 1e-3, last = (double)st[p->nsteps - 1];
+        for (int s = 0; s < p->nsteps; ++s) {
+            const double t = total - (last - (double)st[s]) / p->ctx->wall_hz;
+            step_done[s] = t > 0 ? t : 0;
+        }
+    }
+    return XG_OK;
+}
+
 extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
 {
     xg_ctx *c = p->ctx;
     int rc;
     HIPCHK(hipSetDevice(c->device));
+    if (p->engine_w) {
+        const double t0 = xg_now();
+        HIPCHK(hipEventRecord(p->ev0, c->stream));
+        if ((rc = launch_engine(p))) return rc;
+        HIPCHK(hipEventRecord(p->ev[p->nsteps - 1], c->stream));
+        if (step_post) {               // one launch posts every step
+            step_post[0] = xg_now() - t0;
+            for (int s = 1; s < p->nsteps; ++s) step_post[s] = 0;
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (wall) *wall = xg_now() - t0;
+        return engine_times(p, step_done);
+    }
     const double t0 = xg_now();
     HIPCHK(hipEventRecord(p->ev0, c->stream));
     for (int s = 0; s < p->nsteps; ++s) {
@@ -593,6 +708,7 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
 extern "C" int xg_plan_enqueue(xg_plan *p)
 {
     int rc;
+    if (p->engine_w) return launch_engine(p);
     for (int s = 0; s < p->nsteps; ++s)
         if ((rc = enqueue_step(p, s))) return rc;
     return XG_OK;

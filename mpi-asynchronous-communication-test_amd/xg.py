@@ -310,6 +310,7 @@ def device():
         d.xg_plan_nsteps.argtypes = [vp]
         d.xg_plan_run.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
         d.xg_plan_enqueue.argtypes = [vp]
+        d.xg_plan_engine.argtypes = [vp]
         d.xg_ktime_begin.argtypes = [vp, ip]
         d.xg_ktime_end.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(ip), C.POINTER(i64)]
         d.xg_set_copy_params.argtypes = [vp, i64, ip]
@@ -441,6 +442,7 @@ class MethodRun:
         self._p = C.c_void_p()
         _check(d.xg_plan_load(ctx.handle, self._r, self.view.ptr, C.byref(self._p)), "xg_plan_load")
         self.nsteps = d.xg_plan_nsteps(self._p)
+        self.engine_workgroups = d.xg_plan_engine(self._p)   # 0: one launch per step
 
     def run_timed(self):
         """barrier-free timed run; returns (step_done[], step_post[], wall)."""

@@ -115,3 +115,42 @@ def test_tam_aggregation_buffers_match_oracle(xg, ctx, method):
                 off += (ref.size + 255) // 256 * 256
     finally:
         run.close()
+
+
+@pytest.mark.parametrize("method", [1, 6, 9, 10, 11, 12, 13, 18])
+def test_step_engine_matches_per_step_launches(xg, ctx, method):
+    """GPU-local plans of small steps run as ONE persistent launch (step engine: grid
+    barrier + wall-clock stamp per step).  Same bytes as one launch per step, every slot
+    checked against the oracle with the strong fingerprint; step times ordered and
+    inside the run's wall time."""
+    import os
+    import xg_oracle as O
+    P, A, d, c, k, it = 20, 6, 1000, 3, 2, 1
+    rl = xg.aggregator_list(P, A)
+    os.environ["XG_ENGINE_MAX_STEP"] = "0"
+    try:
+        ctx_eager = xg.Context(rank=0, nranks=1, device=0)
+    finally:
+        del os.environ["XG_ENGINE_MAX_STEP"]
+    try:
+        s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=1, iteration=it)
+        exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
+        res = {}
+        for name, cx in (("engine", ctx), ("eager", ctx_eager)):
+            run = xg.MethodRun(cx, s, it=it, mode=1)
+            try:
+                assert (run.engine_workgroups > 0) == (name == "engine" and run.nsteps >= 2), (name, run.nsteps)
+                done, post, wall = run.run_timed()
+                assert all(0 <= a <= b for a, b in zip(done, done[1:])), done
+                assert done[-1] <= wall + 1e-4
+                chk, bad, _f = run.verify()
+                assert all(b == 0 for b in bad), name
+                for (src, seed, dst, off), ck in zip(run.slots, chk):
+                    local = off - s.recv_offset(1, dst)
+                    assert ck == O.chk64(exp[dst][local: local + d]), (name, method, src, dst)
+                res[name] = chk
+            finally:
+                run.close()
+        assert res["engine"] == res["eager"]
+    finally:
+        ctx_eager.close()
