@@ -256,9 +256,21 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
     __shared__ int give_up;
     if (threadIdx.x == 0) give_up = 0;
     __syncthreads();
+    // next step's first unit of this workgroup, loaded while the barrier is pending
+    // (<= 4 KiB, 16-B aligned: one 16-B register per lane); pf is workgroup-uniform
+    bool pf = false;
+    DCopy nc = {nullptr, nullptr, 0};
+    u32x4 nv = {0u, 0u, 0u, 0u};
+    const int lane16 = (int)threadIdx.x * 16;
     for (int s = 0; s < nsteps; ++s) {
         const int e = step_begin[s + 1];
-        for (int i = step_begin[s] + (int)blockIdx.x; i < e; i += (int)W) {
+        int i = step_begin[s] + (int)blockIdx.x;
+        if (pf) {
+            if (lane16 < nc.len) *(g_u4 *)(nc.dst + lane16) = nv;
+            i += (int)W;
+            pf = false;
+        }
+        for (; i < e; i += (int)W) {
             const DCopy c = pieces[i];
             if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
                 pipelined_copy16<4>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
@@ -267,20 +279,29 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores of step s performed
         __syncthreads();
+        const unsigned target = (unsigned)(s + 1) * W;
+        bool last = false;
         if (threadIdx.x == 0) {
-            const unsigned target = (unsigned)(s + 1) * W;
             const unsigned t = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-            if (t == target) {
-                stamps[s] = (unsigned long long)wall_clock64();
-            } else {
-                unsigned spins = 0;
-                while (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 22) || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        give_up = 1;
-                        break;
-                    }
+            last = t == target;
+            if (last) stamps[s] = (unsigned long long)wall_clock64();
+        }
+        if (s + 1 < nsteps) {              // no step reads what another writes: safe to load early
+            const int j = step_begin[s + 1] + (int)blockIdx.x;
+            if (j < step_begin[s + 2]) {
+                nc = pieces[j];
+                pf = nc.len <= kThreads * 16 && ((((uintptr_t)nc.src | (uintptr_t)nc.dst | (uint64_t)nc.len) & 15) == 0);
+                if (pf && lane16 < nc.len) nv = *(g_cu4 *)(nc.src + lane16);
+            }
+        }
+        if (threadIdx.x == 0 && !last) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 22) || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    give_up = 1;
+                    break;
                 }
             }
         }

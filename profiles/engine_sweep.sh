@@ -5,7 +5,7 @@
 out=${1:-gpurun_out/engine_sweep.txt}; : > $out
 B=$PWD/mpi-asynchronous-communication-test_amd/bin/test
 run() { (cd /tmp && env "$@" timeout -k 5 60 $B --procs 32 -a 14 -d $d -c 3 -m $m -i 1 -k 3 | grep "max total" | sed 's/.*= //'); }
-for m in 1 6 9 11 12; do for d in 2048 16384 65536 262144 1048576; do
+for m in ${METHODS:-1 6 9 11 12}; do for d in ${SIZES:-2048 16384 65536 262144 1048576}; do
   [ $m = 6 ] && [ $d -gt 65424 ] && continue      # the reference deadlocks there (refused)
   e=$(run XG_ENGINE_MAX_STEP=1073741824) || exit 1
   e2=$(run XG_ENGINE_MAX_STEP=1073741824 XG_ENGINE_WG=256) || exit 1
