@@ -225,6 +225,22 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restric
     }
 }
 
+// One workgroup moves up to B*4 KiB in one burst: every lane issues its (up to)
+// B 16-B loads, then its B stores -- B*4 KiB in flight per workgroup, so a few
+// hundred resident workgroups keep enough bytes in flight to stream HBM.
+template <int B>
+__device__ __forceinline__ void burst_copy16(g_cu4 *__restrict__ s4, g_u4 *__restrict__ t4, int64_t n4)
+{
+    u32x4 v[B];
+    const int64_t i0 = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < B; ++k)
+        if (i0 + k * kThreads < n4) v[k] = s4[i0 + k * kThreads];
+#pragma unroll
+    for (int k = 0; k < B; ++k)
+        if (i0 + k * kThreads < n4) t4[i0 + k * kThreads] = v[k];
+}
+
 // ---------------------------------------------------------------- step engine
 // A GPU-local plan of many small steps (sync / pairwise / throttled schedules
 // at small -d) is bound by the per-step kernel boundary + timing event, not by
@@ -246,6 +262,9 @@ struct EngineState {
 
 typedef __attribute__((address_space(1))) unsigned g_u32;
 
+// B: 16-B loads per lane per unit -> units of B * 4 KiB (the host cuts the step's
+// transfers to that size and picks B so that a step has enough units to spread).
+template <int B>
 __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__restrict__ pieces,
                                                                const int *__restrict__ step_begin, int nsteps,
                                                                EngineState *st, unsigned long long *stamps)
@@ -256,24 +275,29 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
     __shared__ int give_up;
     if (threadIdx.x == 0) give_up = 0;
     __syncthreads();
-    // next step's first unit of this workgroup, loaded while the barrier is pending
-    // (<= 4 KiB, 16-B aligned: one 16-B register per lane); pf is workgroup-uniform
+    // This workgroup's first unit of the next step is LOADED while the barrier is
+    // pending (into v[]) and stored once it opens: the load latency of each step
+    // (HBM + address translation of fresh pages) overlaps the barrier.  pf is
+    // workgroup-uniform.
     bool pf = false;
     DCopy nc = {nullptr, nullptr, 0};
-    u32x4 nv = {0u, 0u, 0u, 0u};
-    const int lane16 = (int)threadIdx.x * 16;
+    u32x4 v[B];
+    const int64_t i0 = threadIdx.x;
     for (int s = 0; s < nsteps; ++s) {
         const int e = step_begin[s + 1];
         int i = step_begin[s] + (int)blockIdx.x;
         if (pf) {
-            if (lane16 < nc.len) *(g_u4 *)(nc.dst + lane16) = nv;
+            const int64_t n4 = nc.len >> 4;
+#pragma unroll
+            for (int k = 0; k < B; ++k)
+                if (i0 + k * kThreads < n4) ((g_u4 *)nc.dst)[i0 + k * kThreads] = v[k];
             i += (int)W;
             pf = false;
         }
         for (; i < e; i += (int)W) {
-            const DCopy c = pieces[i];
+            const DCopy c = pieces[i];       // <= B * 4 KiB
             if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
-                pipelined_copy16<4>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
+                burst_copy16<B>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
             else
                 for (int64_t k = threadIdx.x; k < c.len; k += kThreads) c.dst[k] = c.src[k];
         }
@@ -290,8 +314,13 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
             const int j = step_begin[s + 1] + (int)blockIdx.x;
             if (j < step_begin[s + 2]) {
                 nc = pieces[j];
-                pf = nc.len <= kThreads * 16 && ((((uintptr_t)nc.src | (uintptr_t)nc.dst | (uint64_t)nc.len) & 15) == 0);
-                if (pf && lane16 < nc.len) nv = *(g_cu4 *)(nc.src + lane16);
+                pf = (((uintptr_t)nc.src | (uintptr_t)nc.dst | (uint64_t)nc.len) & 15) == 0;
+                if (pf) {
+                    const int64_t n4 = nc.len >> 4;
+#pragma unroll
+                    for (int k = 0; k < B; ++k)
+                        if (i0 + k * kThreads < n4) v[k] = ((g_cu4 *)nc.src)[i0 + k * kThreads];
+                }
             }
         }
         if (threadIdx.x == 0 && !last) {

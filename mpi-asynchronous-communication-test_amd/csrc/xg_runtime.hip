@@ -91,6 +91,7 @@ struct xg_plan {
     int variant;
     // step engine (one persistent launch for the whole plan), or engine_w == 0
     int engine_w;
+    int engine_b;                  // 16-B loads per lane per unit (1, 4, 16)
     int *d_step_begin;
     xgk::DCopy *d_epieces;         // the engine's work units, step-major
     xgk::EngineState *d_engine;    // state (16 B, zeroed per launch) followed by nsteps stamps
@@ -131,7 +132,7 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
     env = getenv("XG_COPY_VARIANT");
     if (env) c->variant = atoi(env);
-    c->engine_max_step = 4 << 20;     // crossover vs one launch per step: profiles/r01_engine_sweep.txt
+    c->engine_max_step = 16 << 20;    // crossover vs one launch per step: profiles/r01_engine_sweep.txt
     env = getenv("XG_ENGINE_MAX_STEP");      // 0: never use the step engine
     if (env) c->engine_max_step = atol(env);
     env = getenv("XG_ENGINE_WG");
@@ -471,20 +472,32 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             ok = ok && !st.p2p_n && !st.sync_after && !st.stage_n && !st.post_n &&
                  st.local_bytes + st.pack_bytes <= c->engine_max_step;
         if (ok) {
-            // the engine's work units: the step's pieces (<= chunk bytes), one per workgroup
-            // visit; smaller units and more than 256 workgroups measured slower
-            // (profiles/r01_engine_sweep.txt)
-            const int64_t unit = c->chunk;
+            // the engine's work units: the step's transfers cut to B * 4 KiB, one burst of B
+            // 16-B loads per lane per workgroup visit.  B grows with the largest step so a
+            // step spreads over up to ~256 workgroups with bytes enough in flight
+            // (profiles/r01_engine_sweep.txt: small units starve big steps, big units leave
+            // small steps on a handful of workgroups)
+            int64_t maxstep = 0;
+            for (const StepR &st : p->steps)
+                if (st.local_bytes + st.pack_bytes > maxstep) maxstep = st.local_bytes + st.pack_bytes;
+            p->engine_b = maxstep <= (1 << 20) ? 1 : (maxstep <= (4 << 20) ? 4 : 16);
+            const int64_t unit = (int64_t)p->engine_b * xgk::kThreads * 16;
             std::vector<xgk::DCopy> ep;
             std::vector<int> sb(p->nsteps + 1);
             int maxu = 0;
             for (int s = 0; s < p->nsteps; ++s) {
                 const StepR &st = p->steps[s];
                 sb[s] = (int)ep.size();
-                for (int i = st.pre_b; i < st.pre_b + st.pre_n; ++i)
-                    for (int64_t o = 0; o < pieces[i].len; o += unit)
-                        ep.push_back({pieces[i].src + o, pieces[i].dst + o,
-                                      pieces[i].len - o < unit ? pieces[i].len - o : unit});
+                for (int i = st.pre_b; i < st.pre_b + st.pre_n;) {
+                    // re-join the chunk-sized pieces of one transfer, then cut it into units
+                    const uint8_t *src = pieces[i].src;
+                    uint8_t *dst = pieces[i].dst;
+                    int64_t len = pieces[i].len;
+                    for (++i; i < st.pre_b + st.pre_n && pieces[i].src == src + len && pieces[i].dst == dst + len; ++i)
+                        len += pieces[i].len;
+                    for (int64_t o = 0; o < len; o += unit)
+                        ep.push_back({src + o, dst + o, len - o < unit ? len - o : unit});
+                }
                 if ((int)ep.size() - sb[s] > maxu) maxu = (int)ep.size() - sb[s];
                 p->engine_bytes += st.local_bytes + st.pack_bytes;
             }
@@ -632,9 +645,16 @@ static int launch_engine(xg_plan *p)
     HIPCHK(hipMemsetAsync(p->d_engine, 0, sizeof(xgk::EngineState), c->stream));
     const bool kt = c->kt_on && 2 * (size_t)c->nk + 1 < c->kev.size();
     if (kt) HIPCHK(hipEventRecord(c->kev[2 * c->nk], c->stream));
-    hipLaunchKernelGGL(xgk::step_engine_kernel, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream, p->d_epieces,
-                       p->d_step_begin, p->nsteps, p->d_engine,
-                       reinterpret_cast<unsigned long long *>(p->d_engine + 1));
+    unsigned long long *stamps = reinterpret_cast<unsigned long long *>(p->d_engine + 1);
+    if (p->engine_b == 1)
+        hipLaunchKernelGGL(xgk::step_engine_kernel<1>, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream,
+                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps);
+    else if (p->engine_b == 4)
+        hipLaunchKernelGGL(xgk::step_engine_kernel<4>, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream,
+                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps);
+    else
+        hipLaunchKernelGGL(xgk::step_engine_kernel<16>, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream,
+                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps);
     HIPCHK(hipGetLastError());
     if (kt) {
         HIPCHK(hipEventRecord(c->kev[2 * c->nk + 1], c->stream));
