@@ -255,7 +255,7 @@ __device__ __forceinline__ void burst_copy16(g_cu4 *__restrict__ s4, g_u4 *__res
 // every launch; spins are bounded, and a timed-out workgroup sets *tmo and
 // leaves, so a broken residency assumption ends the launch instead of hanging.
 struct EngineState {
-    unsigned count;     // arrival tickets, cumulative over the launch
+    unsigned count;     // arrival tickets, cumulative over every launch of the plan
     unsigned tmo;       // != 0: some workgroup gave up waiting
     unsigned pad[2];
 };
@@ -267,8 +267,12 @@ typedef __attribute__((address_space(1))) unsigned g_u32;
 template <int B>
 __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__restrict__ pieces,
                                                                const int *__restrict__ step_begin, int nsteps,
-                                                               EngineState *st, unsigned long long *stamps)
+                                                               EngineState *st, unsigned long long *stamps,
+                                                               unsigned base)
 {
+    // base: tickets taken by this plan's earlier launches (count is never reset
+    // between launches, so no memset precedes a launch); compare by difference,
+    // which is wrap-safe
     const unsigned W = gridDim.x;
     g_u32 *count = (g_u32 *)&st->count;
     g_u32 *tmo = (g_u32 *)&st->tmo;
@@ -303,7 +307,7 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores of step s performed
         __syncthreads();
-        const unsigned target = (unsigned)(s + 1) * W;
+        const unsigned target = base + (unsigned)(s + 1) * W;
         bool last = false;
         if (threadIdx.x == 0) {
             const unsigned t = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
@@ -325,7 +329,7 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
         }
         if (threadIdx.x == 0 && !last) {
             unsigned spins = 0;
-            while (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            while ((int)(__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 22) || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                     __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

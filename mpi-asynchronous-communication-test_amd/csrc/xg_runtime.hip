@@ -94,7 +94,9 @@ struct xg_plan {
     int engine_b;                  // 16-B loads per lane per unit (1, 4, 16)
     int *d_step_begin;
     xgk::DCopy *d_epieces;         // the engine's work units, step-major
-    xgk::EngineState *d_engine;    // state (16 B, zeroed per launch) followed by nsteps stamps
+    xgk::EngineState *d_engine;    // state (16 B, zeroed at load) followed by nsteps stamps
+    unsigned engine_base;          // barrier tickets taken by earlier launches (wraps)
+    bool engine_reset;             // zero the state before the next launch
     int64_t engine_bytes;          // bytes copied per run
 };
 
@@ -510,6 +512,9 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
                 HIPCHK(hipMemcpy(p->d_epieces, ep.data(), sizeof(xgk::DCopy) * ep.size(), hipMemcpyHostToDevice));
             }
             HIPCHK(hipMalloc(&p->d_engine, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps));
+            HIPCHK(hipMemset(p->d_engine, 0, sizeof(xgk::EngineState)));
+            p->engine_base = 0;
+            p->engine_reset = false;
         }
     }
     *out = p;
@@ -642,19 +647,24 @@ static int enqueue_step(xg_plan *p, int s)
 static int launch_engine(xg_plan *p)
 {
     xg_ctx *c = p->ctx;
-    HIPCHK(hipMemsetAsync(p->d_engine, 0, sizeof(xgk::EngineState), c->stream));
+    if (p->engine_reset) {
+        HIPCHK(hipMemsetAsync(p->d_engine, 0, sizeof(xgk::EngineState), c->stream));
+        p->engine_base = 0;
+    }
+    const unsigned base = p->engine_base;
+    p->engine_base += (unsigned)p->nsteps * (unsigned)p->engine_w;
     const bool kt = c->kt_on && 2 * (size_t)c->nk + 1 < c->kev.size();
     if (kt) HIPCHK(hipEventRecord(c->kev[2 * c->nk], c->stream));
     unsigned long long *stamps = reinterpret_cast<unsigned long long *>(p->d_engine + 1);
     if (p->engine_b == 1)
         hipLaunchKernelGGL(xgk::step_engine_kernel<1>, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream,
-                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps);
+                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps, base);
     else if (p->engine_b == 4)
         hipLaunchKernelGGL(xgk::step_engine_kernel<4>, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream,
-                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps);
+                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps, base);
     else
         hipLaunchKernelGGL(xgk::step_engine_kernel<16>, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream,
-                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps);
+                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps, base);
     HIPCHK(hipGetLastError());
     if (kt) {
         HIPCHK(hipEventRecord(c->kev[2 * c->nk + 1], c->stream));
@@ -672,6 +682,7 @@ static int engine_times(xg_plan *p, double *step_done)
     HIPCHK(hipMemcpy(h.data(), p->d_engine, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
     const xgk::EngineState *es = reinterpret_cast<const xgk::EngineState *>(h.data());
     if (es->tmo) {
+        p->engine_reset = true;        // the tickets are inconsistent now: zero before every launch
         fprintf(stderr, "xg: step engine: a workgroup timed out at a grid barrier (workgroups not co-resident?)\n");
         return XG_EHIP;
     }
