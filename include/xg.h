@@ -106,6 +106,11 @@ int xg_plan_engine(const xg_plan *p);
 /* plans[g] = GPU g's plan of one virtual job (xg_init_virtual, g = 0..n-1, same
  * schedule); step_done[nsteps]: device seconds from start to the end of each step. */
 int xg_vplans_run(xg_plan *const *plans, int n, double *step_done);
+/* Same, with every send/recv pair moved by RCCL: a 1-rank communicator on the
+ * device, one ncclGroupStart/End of self ncclSend + ncclRecv per step (matched
+ * in issue order) and ncclAllReduce for the in-loop barriers -- RCCL's calls on
+ * the real plan buffers with one GPU. */
+int xg_vplans_run_rccl(xg_plan *const *plans, int n, double *step_done);
 /* Kernel timing session: while active, every copy_kernel launch of any plan
  * on this context is bracketed by HIP events on the stream it runs on.
  * xg_ktime_end waits for the stream and returns the summed kernel time (ms),

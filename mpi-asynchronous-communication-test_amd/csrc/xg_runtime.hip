@@ -750,7 +750,12 @@ extern "C" int xg_plan_enqueue(xg_plan *p)
 // (sends of g to h matched in order with h's receives from g -- RCCL's
 // per-peer FIFO inside a group), then all post copies, then the step event.
 // step_done[s] = device seconds from the start to the end of step s.
-extern "C" int xg_vplans_run(xg_plan *const *plans, int n, double *step_done)
+// rccl = true: the same pairs go through RCCL instead -- a 1-rank communicator
+// on the device (created once, held by plans[0]'s context), each step's pairs as
+// one ncclGroupStart/End of self ncclSend + ncclRecv (matched in issue order),
+// and the in-loop barriers as ncclAllReduce: RCCL's p2p and collective calls on
+// the real plan buffers, on a box with one GPU.
+static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl)
 {
     if (!plans || n < 1) return XG_EARG;
     xg_ctx *c0 = plans[0]->ctx;
@@ -766,6 +771,11 @@ extern "C" int xg_vplans_run(xg_plan *const *plans, int n, double *step_done)
     hipStream_t st = c0->stream;
     HIPCHK(hipSetDevice(c0->device));
     for (int g = 0; g < n; ++g) HIPCHK(hipStreamSynchronize(plans[g]->ctx->stream));
+    if (rccl && !c0->comm) {
+        ncclUniqueId id;
+        NCCLCHK(ncclGetUniqueId(&id));
+        NCCLCHK(ncclCommInitRank(&c0->comm, 1, id, 0));
+    }
     HIPCHK(hipEventRecord(plans[0]->ev0, st));
     std::vector<std::vector<const xg_p2p *>> sends((size_t)n * n), recvs((size_t)n * n);
     for (int s = 0; s < nst; ++s) {
@@ -781,6 +791,7 @@ extern "C" int xg_vplans_run(xg_plan *const *plans, int n, double *step_done)
                 else recvs[(size_t)o.peer * n + g].push_back(&o);
             }
         }
+        bool grouped = false;
         for (int g = 0; g < n; ++g)
             for (int h = 0; h < n; ++h) {
                 const auto &sv = sends[(size_t)g * n + h], &rv = recvs[(size_t)g * n + h];
@@ -795,14 +806,26 @@ extern "C" int xg_vplans_run(xg_plan *const *plans, int n, double *step_done)
                                 g, h, k, (long long)sv[k]->len, (long long)rv[k]->len);
                         return XG_EARG;
                     }
-                    if (sv[k]->len)
-                        HIPCHK(hipMemcpyAsync(plans[h]->reg->ptr[rv[k]->buf] + rv[k]->off,
-                                              plans[g]->reg->ptr[sv[k]->buf] + sv[k]->off, (size_t)sv[k]->len,
-                                              hipMemcpyDeviceToDevice, st));
+                    if (!sv[k]->len) continue;
+                    uint8_t *dst = plans[h]->reg->ptr[rv[k]->buf] + rv[k]->off;
+                    uint8_t *src = plans[g]->reg->ptr[sv[k]->buf] + sv[k]->off;
+                    if (!rccl) {
+                        HIPCHK(hipMemcpyAsync(dst, src, (size_t)sv[k]->len, hipMemcpyDeviceToDevice, st));
+                        continue;
+                    }
+                    if (!grouped) {
+                        NCCLCHK(ncclGroupStart());
+                        grouped = true;
+                    }
+                    NCCLCHK(ncclSend(src, (size_t)sv[k]->len, ncclUint8, 0, c0->comm, st));
+                    NCCLCHK(ncclRecv(dst, (size_t)rv[k]->len, ncclUint8, 0, c0->comm, st));
                 }
             }
+        if (grouped) NCCLCHK(ncclGroupEnd());
         for (int g = 0; g < n; ++g)
             if ((rc = enqueue_post(plans[g], s, st))) return rc;
+        if (rccl && plans[0]->steps[s].sync_after)
+            NCCLCHK(ncclAllReduce(c0->d_red, c0->d_red, 1, ncclFloat64, ncclMax, c0->comm, st));
         HIPCHK(hipEventRecord(plans[0]->ev[s], st));
     }
     HIPCHK(hipStreamSynchronize(st));
@@ -813,6 +836,16 @@ extern "C" int xg_vplans_run(xg_plan *const *plans, int n, double *step_done)
             step_done[s] = ms * 1e-3;
         }
     return XG_OK;
+}
+
+extern "C" int xg_vplans_run(xg_plan *const *plans, int n, double *step_done)
+{
+    return vplans_run(plans, n, step_done, false);
+}
+
+extern "C" int xg_vplans_run_rccl(xg_plan *const *plans, int n, double *step_done)
+{
+    return vplans_run(plans, n, step_done, true);
 }
 
 extern "C" int xg_ktime_begin(xg_ctx *c, int max_launches)

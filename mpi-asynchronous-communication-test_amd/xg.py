@@ -290,6 +290,7 @@ def device():
         d.xg_finalize.argtypes = [vp]
         d.xg_init_virtual.argtypes = [C.POINTER(vp), ip, ip, ip]
         d.xg_vplans_run.argtypes = [C.POINTER(vp), ip, C.POINTER(C.c_double)]
+        d.xg_vplans_run_rccl.argtypes = [C.POINTER(vp), ip, C.POINTER(C.c_double)]
         d.xg_barrier.argtypes = [vp]
         d.xg_sync.argtypes = [vp]
         d.xg_device_sync.argtypes = [vp]
@@ -407,14 +408,16 @@ def now():
     return device().xg_now()
 
 
-def run_virtual(runs):
+def run_virtual(runs, rccl=False):
     """Execute the MethodRuns of every GPU of one virtual job (runs[g] on Context.virtual(g, n))
-    step by step on one device; returns step_done[] (device seconds)."""
+    step by step on one device; returns step_done[] (device seconds).  rccl: move the
+    cross-GPU pairs through RCCL (1-rank communicator, self send/recv) instead of copies."""
     n = len(runs)
     arr = (C.c_void_p * n)(*[r._p for r in runs])
     nst = max(1, runs[0].nsteps)
     done = (C.c_double * nst)()
-    _check(device().xg_vplans_run(arr, n, done), "xg_vplans_run")
+    fn = "xg_vplans_run_rccl" if rccl else "xg_vplans_run"
+    _check(getattr(device(), fn)(arr, n, done), fn)
     return list(done)[:runs[0].nsteps]
 
 

@@ -6,9 +6,12 @@ plans the driver's 2/4/8-GPU bench executes (local gather/scatter, packing
 into per-peer staging, unpacking) on the hardware, and checks every received
 segment against the checksums captured from the real reference.
 
-What it does not exercise is RCCL itself (the box has one GPU, and RCCL refuses
-two ranks on one device); tests/test_plan_gloo.py runs the same plans across
-two processes on CPU.
+RCCL refuses two ranks on one device, so the box cannot run a 2-rank
+communicator; test_golden_multi_gpu_rccl instead moves the same pairs through
+RCCL on a 1-rank communicator (self ncclSend/ncclRecv in one group per step,
+ncclAllReduce for the in-loop barriers): RCCL's p2p calls with the plans' real
+buffers, offsets and lengths.  tests/test_plan_gloo.py runs the same plans
+across two processes on CPU.
 """
 import pytest
 
@@ -28,10 +31,10 @@ def worlds(xg):
             c.close()
 
 
-def _run_job(xg, ctxs, s, it, mode, pack):
+def _run_job(xg, ctxs, s, it, mode, pack, rccl=False):
     runs = [xg.MethodRun(c, s, it=it, mode=mode, pack_max_seg=pack) for c in ctxs]
     try:
-        done = xg.run_virtual(runs)
+        done = xg.run_virtual(runs, rccl=rccl)
         assert all(b >= a for a, b in zip(done, done[1:]))
         out = []
         for r in runs:
@@ -46,6 +49,16 @@ def _run_job(xg, ctxs, s, it, mode, pack):
 @pytest.mark.parametrize("G", GPUS)
 @pytest.mark.parametrize("cfg", golden_configs())
 def test_golden_multi_gpu(xg, worlds, cfg, G):
+    _golden_job(xg, worlds, cfg, G, rccl=False)
+
+
+@pytest.mark.parametrize("G", (2, 8))
+@pytest.mark.parametrize("cfg", golden_configs())
+def test_golden_multi_gpu_rccl(xg, worlds, cfg, G):
+    _golden_job(xg, worlds, cfg, G, rccl=True)
+
+
+def _golden_job(xg, worlds, cfg, G, rccl):
     meta, _traces, data = load_golden(cfg)
     import xg_oracle as O
     P, A, d, c, k = meta["P"], meta["A"], meta["d"], meta["c"], meta["ntimes"]
@@ -58,7 +71,7 @@ def test_golden_multi_gpu(xg, worlds, cfg, G):
         s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=meta["proc_node"],
                         barrier_type=meta.get("barrier", 0), iteration=it)
         for pack in (0, 1 << 30):          # never pack / pack every multi-segment peer transfer
-            res = _run_job(xg, worlds[G], s, it, 0, pack)
+            res = _run_job(xg, worlds[G], s, it, 0, pack, rccl)
             assert len(res) == sum(1 for key in data[direction] if key[0] == it), (cfg, method, G)
             for (src, seed, dst, off), ck, nb, fb in res:
                 assert nb == 0, "%s G%d m%d pack%d %d->%d: %d bad bytes from %d" % (cfg, G, method, pack, src, dst,
