@@ -58,6 +58,7 @@ CONFIGS = {
     "p20_a6_c7": (20, "-a 6 -d 24 -c 7 -i 1 -k 3"),
     "p16_a5_c3_b1": (16, "-a 5 -d 96 -c 3 -b 1 -p 4 -i 1 -k 2"),
     "p16_a5_c4_b2": (16, "-a 5 -d 96 -c 4 -b 2 -p 2 -i 1 -k 2"),
+    "p8_a3_d0_c3": (8, "-a 3 -d 0 -c 3 -p 2 -i 1 -k 2"),        # empty segments (every message 0 bytes)
 }
 
 

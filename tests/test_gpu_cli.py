@@ -16,7 +16,7 @@ def _mask(text):
     return re.sub(r"\d+(\.\d+)?", "#", text)
 
 
-@pytest.mark.parametrize("cfg", ["readme_p32_a14", "p16_a5_d1000_c3", "p16_a5_c4_b2"])
+@pytest.mark.parametrize("cfg", ["readme_p32_a14", "p16_a5_d1000_c3", "p16_a5_c4_b2", "p8_a3_d0_c3"])
 def test_cli_report_matches_reference(pkg, cfg, tmp_path):
     meta, _, _ = load_golden(cfg)
     exe = os.path.join(os.path.dirname(pkg.__file__), "bin", "test")

@@ -83,11 +83,14 @@ def test_tam_messages_match_reference(cfg):
 
 @pytest.mark.parametrize("cfg", CONFIGS)
 def test_uncaptured_pairs_are_self_copies(cfg):
-    """The only pairs PMPI could not see are the aggregator self-memcpys of m3/m4/m6."""
+    """The only pairs PMPI could not see are the aggregator self-memcpys of m3/m4/m6
+    (and, at -d 0, every pair: a 0-byte segment has nothing to checksum)."""
     meta, _, _ = load_golden(cfg)
     rl = meta["aggregators"]
     for m, info in meta["methods"].items():
         assert info["status"] == "ok" and info["layout_ok"]
+        if meta["d"] == 0:
+            continue
         for it, src, dst in info["uncaptured_pairs"]:
             assert int(m) in (3, 4, 6, 18, 20) and src == dst and dst in rl
 
