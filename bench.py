@@ -296,6 +296,10 @@ def main():
                 traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None
+        # the committed PMC figure is per launch of THIS workload at N = 1 (profiles/bench_rocprof.sh);
+        # any other launch size has not been counted
+        if traffic and (world != 1 or abs(traffic - per_launch) > 0.05 * per_launch):
+            traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "copy_kernel (intra-GPU gather/scatter)", "launches": nlaunch,
