@@ -225,20 +225,72 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restric
     }
 }
 
-// One workgroup moves up to B*4 KiB in one burst: every lane issues its (up to)
-// B 16-B loads, then its B stores -- B*4 KiB in flight per workgroup, so a few
-// hundred resident workgroups keep enough bytes in flight to stream HBM.
+// Raw buffer access (gfx9 buffer resource, stride 0, num_records = bytes): a load
+// past num_records returns 0 and a store past it is dropped, so the partial tail
+// of a transfer needs no per-lane branch.  Branch-free code matters here: with a
+// branch around every load and store the compiler's waitcnt pass can no longer
+// count, and puts vmcnt(0) before EVERY store (each store then waits for the
+// previous one to be acknowledged).
+typedef __amdgpu_buffer_rsrc_t brsrc;
+// s_waitcnt immediate (gfx9 encoding): vmcnt(0), expcnt(7) and lgkmcnt(15) = no wait on those
+constexpr int kVmcnt0 = 0x0F70;
+constexpr int kRsrcWord3 = 0x00020000;     // gfx9 (gfx950) raw buffer, as composable_kernel
+
+__device__ __forceinline__ brsrc make_rsrc(const void *p, int64_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, kRsrcWord3);
+}
+
+__device__ __forceinline__ u32x4 bload16(brsrc r, int off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+
+__device__ __forceinline__ void bstore16(brsrc r, int off, u32x4 v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+
+// One workgroup moves up to B*4 KiB (len, 16-B aligned) in one burst: every lane
+// issues its B 16-B loads, then its B stores -- B*4 KiB in flight per workgroup, so
+// a few hundred resident workgroups keep enough bytes in flight to stream HBM.
 template <int B>
-__device__ __forceinline__ void burst_copy16(g_cu4 *__restrict__ s4, g_u4 *__restrict__ t4, int64_t n4)
+__device__ __forceinline__ void burst_load16(const uint8_t *src, int64_t len, u32x4 *v)
+{
+    const brsrc r = make_rsrc(src, len);
+#pragma unroll
+    for (int k = 0; k < B; ++k) v[k] = bload16(r, ((int)threadIdx.x + k * kThreads) * 16);
+}
+
+template <int B>
+__device__ __forceinline__ void burst_store16(uint8_t *dst, int64_t len, const u32x4 *v)
+{
+    const brsrc r = make_rsrc(dst, len);
+#pragma unroll
+    for (int k = 0; k < B; ++k) bstore16(r, ((int)threadIdx.x + k * kThreads) * 16, v[k]);
+}
+
+template <int B>
+__device__ __forceinline__ void burst_copy16(const uint8_t *src, uint8_t *dst, int64_t len)
 {
     u32x4 v[B];
-    const int64_t i0 = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < B; ++k)
-        if (i0 + k * kThreads < n4) v[k] = s4[i0 + k * kThreads];
-#pragma unroll
-    for (int k = 0; k < B; ++k)
-        if (i0 + k * kThreads < n4) t4[i0 + k * kThreads] = v[k];
+    burst_load16<B>(src, len, v);
+    burst_store16<B>(dst, len, v);
+}
+
+// Piece copy in bursts (copy variant 12): one workgroup per DCopy piece, B*4 KiB per
+// burst, every load of a burst issued before its first store.
+template <int B>
+__global__ __launch_bounds__(kThreads) void copy_kernel_b(const DCopy *__restrict__ pieces)
+{
+    const DCopy c = pieces[blockIdx.x];
+    if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0) {
+        constexpr int64_t step = (int64_t)B * kThreads * 16;
+        for (int64_t o = 0; o < c.len; o += step)
+            burst_copy16<B>(c.src + o, c.dst + o, c.len - o < step ? c.len - o : step);
+    } else {
+        for (int64_t i = threadIdx.x; i < c.len; i += kThreads) c.dst[i] = c.src[i];
+    }
 }
 
 // ---------------------------------------------------------------- step engine
@@ -286,26 +338,22 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
     bool pf = false;
     DCopy nc = {nullptr, nullptr, 0};
     u32x4 v[B];
-    const int64_t i0 = threadIdx.x;
     for (int s = 0; s < nsteps; ++s) {
         const int e = step_begin[s + 1];
         int i = step_begin[s] + (int)blockIdx.x;
         if (pf) {
-            const int64_t n4 = nc.len >> 4;
-#pragma unroll
-            for (int k = 0; k < B; ++k)
-                if (i0 + k * kThreads < n4) ((g_u4 *)nc.dst)[i0 + k * kThreads] = v[k];
+            burst_store16<B>(nc.dst, nc.len, v);
             i += (int)W;
             pf = false;
         }
         for (; i < e; i += (int)W) {
             const DCopy c = pieces[i];       // <= B * 4 KiB
             if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
-                burst_copy16<B>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
+                burst_copy16<B>(c.src, c.dst, c.len);
             else
                 for (int64_t k = threadIdx.x; k < c.len; k += kThreads) c.dst[k] = c.src[k];
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores of step s performed
+        __builtin_amdgcn_s_waitcnt(kVmcnt0);                // this wave's stores of step s performed
         __syncthreads();
         const unsigned target = base + (unsigned)(s + 1) * W;
         bool last = false;
@@ -319,12 +367,7 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
             if (j < step_begin[s + 2]) {
                 nc = pieces[j];
                 pf = (((uintptr_t)nc.src | (uintptr_t)nc.dst | (uint64_t)nc.len) & 15) == 0;
-                if (pf) {
-                    const int64_t n4 = nc.len >> 4;
-#pragma unroll
-                    for (int k = 0; k < B; ++k)
-                        if (i0 + k * kThreads < n4) v[k] = ((g_cu4 *)nc.src)[i0 + k * kThreads];
-                }
+                if (pf) burst_load16<B>(nc.src, nc.len, v);
             }
         }
         if (threadIdx.x == 0 && !last) {

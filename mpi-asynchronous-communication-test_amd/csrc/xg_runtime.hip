@@ -474,36 +474,47 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             ok = ok && !st.p2p_n && !st.sync_after && !st.stage_n && !st.post_n &&
                  st.local_bytes + st.pack_bytes <= c->engine_max_step;
         if (ok) {
-            // the engine's work units: the step's transfers cut to B * 4 KiB, one burst of B
-            // 16-B loads per lane per workgroup visit.  B grows with the largest step so a
-            // step spreads over up to ~256 workgroups with bytes enough in flight
-            // (profiles/r01_engine_sweep.txt: small units starve big steps, big units leave
-            // small steps on a handful of workgroups)
+            // the engine's work units: the step's transfers (chunk-sized pieces re-joined) cut
+            // to B * 4 KiB, one burst of B 16-B loads per lane per workgroup visit.  B grows
+            // with the largest step so a step spreads over up to ~256 workgroups with bytes
+            // enough in flight (profiles/r01_engine_sweep.txt: small units starve big steps,
+            // big units leave small steps on a handful of workgroups).  One workgroup for a
+            // whole plan of tiny steps (workgroup barrier instead of the grid barrier) was
+            // measured 2x slower per step: profiles/r01_engine_wg_probe.txt, r01_engine_sweep.txt
             int64_t maxstep = 0;
             for (const StepR &st : p->steps)
                 if (st.local_bytes + st.pack_bytes > maxstep) maxstep = st.local_bytes + st.pack_bytes;
-            p->engine_b = maxstep <= (1 << 20) ? 1 : (maxstep <= (4 << 20) ? 4 : 16);
-            const int64_t unit = (int64_t)p->engine_b * xgk::kThreads * 16;
-            std::vector<xgk::DCopy> ep;
-            std::vector<int> sb(p->nsteps + 1);
-            int maxu = 0;
+            std::vector<std::vector<xgk::DCopy>> xfer(p->nsteps);
             for (int s = 0; s < p->nsteps; ++s) {
                 const StepR &st = p->steps[s];
-                sb[s] = (int)ep.size();
                 for (int i = st.pre_b; i < st.pre_b + st.pre_n;) {
-                    // re-join the chunk-sized pieces of one transfer, then cut it into units
                     const uint8_t *src = pieces[i].src;
                     uint8_t *dst = pieces[i].dst;
                     int64_t len = pieces[i].len;
                     for (++i; i < st.pre_b + st.pre_n && pieces[i].src == src + len && pieces[i].dst == dst + len; ++i)
                         len += pieces[i].len;
-                    for (int64_t o = 0; o < len; o += unit)
-                        ep.push_back({src + o, dst + o, len - o < unit ? len - o : unit});
+                    xfer[s].push_back({src, dst, len});
                 }
-                if ((int)ep.size() - sb[s] > maxu) maxu = (int)ep.size() - sb[s];
                 p->engine_bytes += st.local_bytes + st.pack_bytes;
             }
-            sb[p->nsteps] = (int)ep.size();
+            auto cut = [&](int64_t unit, std::vector<xgk::DCopy> &ep, std::vector<int> &sb) -> int {
+                int maxu = 0;
+                ep.clear();
+                sb.assign(p->nsteps + 1, 0);
+                for (int s = 0; s < p->nsteps; ++s) {
+                    sb[s] = (int)ep.size();
+                    for (const xgk::DCopy &x : xfer[s])
+                        for (int64_t o = 0; o < x.len; o += unit)
+                            ep.push_back({x.src + o, x.dst + o, x.len - o < unit ? x.len - o : unit});
+                    if ((int)ep.size() - sb[s] > maxu) maxu = (int)ep.size() - sb[s];
+                }
+                sb[p->nsteps] = (int)ep.size();
+                return maxu;
+            };
+            std::vector<xgk::DCopy> ep;
+            std::vector<int> sb;
+            p->engine_b = maxstep <= (1 << 20) ? 1 : (maxstep <= (4 << 20) ? 4 : 16);
+            const int maxu = cut((int64_t)p->engine_b * xgk::kThreads * 16, ep, sb);
             p->engine_w = maxu < 1 ? 1 : (maxu > c->engine_wmax ? c->engine_wmax : maxu);
             HIPCHK(hipMalloc(&p->d_step_begin, sizeof(int) * sb.size()));
             HIPCHK(hipMemcpy(p->d_step_begin, sb.data(), sizeof(int) * sb.size(), hipMemcpyHostToDevice));
@@ -560,6 +571,8 @@ static int launch_copy(xg_plan *p, int b, int n, hipStream_t st)
     case 9: hipLaunchKernelGGL((xgk::copy_kernel_g<4, 0, 1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 10: hipLaunchKernelGGL((xgk::copy_kernel_g<8>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 11: hipLaunchKernelGGL((xgk::copy_kernel_g<8, 1, 1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 12: hipLaunchKernelGGL((xgk::copy_kernel_b<8>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 13: hipLaunchKernelGGL((xgk::copy_kernel_b<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 0: hipLaunchKernelGGL((xgk::copy_kernel<4, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     }

@@ -117,15 +117,17 @@ def test_tam_aggregation_buffers_match_oracle(xg, ctx, method):
         run.close()
 
 
+@pytest.mark.parametrize("d", [1000, 2048])
 @pytest.mark.parametrize("method", [1, 6, 9, 10, 11, 12, 13, 18])
-def test_step_engine_matches_per_step_launches(xg, ctx, method):
+def test_step_engine_matches_per_step_launches(xg, ctx, method, d):
     """GPU-local plans of small steps run as ONE persistent launch (step engine: grid
-    barrier + wall-clock stamp per step).  Same bytes as one launch per step, every slot
+    barrier + wall-clock stamp per step; d = 1000: byte path, d = 2048: 16-B buffer
+    loads/stores with partial units).  Same bytes as one launch per step, every slot
     checked against the oracle with the strong fingerprint; step times ordered and
     inside the run's wall time."""
     import os
     import xg_oracle as O
-    P, A, d, c, k, it = 20, 6, 1000, 3, 2, 1
+    P, A, c, k, it = 20, 6, 3, 2, 1
     rl = xg.aggregator_list(P, A)
     os.environ["XG_ENGINE_MAX_STEP"] = "0"
     try:
@@ -139,7 +141,7 @@ def test_step_engine_matches_per_step_launches(xg, ctx, method):
         for name, cx in (("engine", ctx), ("eager", ctx_eager)):
             run = xg.MethodRun(cx, s, it=it, mode=1)
             try:
-                assert (run.engine_workgroups > 0) == (name == "engine" and run.nsteps >= 2), (name, run.nsteps)
+                assert (run.engine_workgroups > 0) == (name != "eager" and run.nsteps >= 2), (name, run.nsteps)
                 done, post, wall = run.run_timed()
                 assert all(0 <= a <= b for a, b in zip(done, done[1:])), done
                 assert done[-1] <= wall + 1e-4
