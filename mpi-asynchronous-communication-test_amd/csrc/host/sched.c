@@ -161,7 +161,7 @@ static void wait_list(prog_t *p, const int *idx, int n)
     }
     o = push(p);
     o->kind = OP_WAIT; o->wbeg = p->npool; o->wcnt = n;
-    memcpy(p->pool + p->npool, idx, sizeof(int) * n);
+    if (n) memcpy(p->pool + p->npool, idx, sizeof(int) * n);
     p->npool += n;
 }
 
@@ -1493,7 +1493,7 @@ size_t xg_sched_trace(const xg_sched *s, int rank, char *buf, size_t buflen)
         }
         else if (o->kind == OP_WAIT) {
             int *v = (int *)xmalloc(sizeof(int) * (o->wcnt + 1)), a = 0;
-            memcpy(v, p->pool + o->wbeg, sizeof(int) * o->wcnt);
+            if (o->wcnt) memcpy(v, p->pool + o->wbeg, sizeof(int) * o->wcnt);
             qsort(v, o->wcnt, sizeof(int), icmp);
             if (!first) sb_put(&b, " ");
             first = 0;
@@ -1628,7 +1628,7 @@ int xg_sched_ntimes(const xg_sched *s) { return s->ntimes; }
 
 int xg_sched_barrier_epochs(const xg_sched *s, int32_t *out)
 {
-    if (out) memcpy(out, s->barrier_epoch, sizeof(int32_t) * s->nbarrier);
+    if (out && s->nbarrier) memcpy(out, s->barrier_epoch, sizeof(int32_t) * s->nbarrier);
     return s->nbarrier;
 }
 
@@ -1917,7 +1917,7 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
     /* post copies are stored after the pre copies in one array */
     dp->ncopy = pre.n + post.n;
     dp->copies = (xg_copy *)xmalloc(sizeof(xg_copy) * (dp->ncopy + 1));
-    memcpy(dp->copies, pre.v, sizeof(xg_copy) * pre.n);
+    if (pre.n) memcpy(dp->copies, pre.v, sizeof(xg_copy) * pre.n);
     if (post.n) memcpy(dp->copies + pre.n, post.v, sizeof(xg_copy) * post.n);
     for (st = 0; st < nst; ++st) dp->steps[st].post_begin += pre.n;
     dp->np2p = pp.n;

@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBDIR = os.path.join(HERE, "lib")
+LIBDIR = os.environ.get("XG_LIBDIR") or os.path.join(HERE, "lib")   # XG_LIBDIR: e.g. a sanitizer build of libxghost
 
 
 class XGError(RuntimeError):
