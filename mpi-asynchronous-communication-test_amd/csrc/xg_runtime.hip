@@ -122,6 +122,12 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     int ndev = 0;
     if (!out || nranks < 1 || rank < 0 || rank >= nranks) return XG_EARG;
     HIPCHK(hipGetDeviceCount(&ndev));
+    if (device >= ndev && ndev > 0 && nranks > 1) {
+        // a launcher that narrows each rank's view (HIP_VISIBLE_DEVICES per rank) leaves
+        // fewer visible GPUs than the local rank index
+        fprintf(stderr, "xg: device %d not visible (%d visible): using device %d\n", device, ndev, device % ndev);
+        device %= ndev;
+    }
     if (device < 0 || device >= ndev) {
         fprintf(stderr, "xg: device %d not present (%d visible)\n", device, ndev);
         return XG_EARG;
