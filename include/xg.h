@@ -53,9 +53,10 @@ int xg_get_unique_id(void *uid /* XG_UNIQUE_ID_BYTES */);
  * uid: from rank 0's xg_get_unique_id (ignored when nranks == 1). */
 int xg_init(xg_ctx **out, int rank, int nranks, int device, const void *uid);
 /* Test hook: GPU `rank` of an `nranks`-GPU job emulated on physical `device`
- * in this process (no RCCL).  Its plans run only via xg_vplans_run, which
- * executes every GPU of the job on one device and moves each RCCL send/recv
- * pair (xg_p2p) as a device-to-device copy -- the multi-GPU device plans,
+ * in this process (no communicator of its own).  Its plans run only via
+ * xg_vplans_run / xg_vplans_run_rccl, which execute every GPU of the job on one
+ * device and move each RCCL send/recv pair (xg_p2p) as a device-to-device copy
+ * or through RCCL on a 1-rank communicator -- the multi-GPU device plans,
  * packing and unpacking exercised on one MI355X.  Barrier / MAX are local. */
 int xg_init_virtual(xg_ctx **out, int rank, int nranks, int device);
 int xg_finalize(xg_ctx *ctx);
