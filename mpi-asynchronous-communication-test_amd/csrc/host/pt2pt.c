@@ -37,9 +37,14 @@ int main(int argc, char **argv)
     }
     /* :97-99 -- MPICH's MPI_STATUS_IGNORE / MPI_STATUSES_IGNORE are both (void*)1 */
     printf("status = %lld, statuses = %lld\n", 1LL, 1LL);
-    if (procs != 2) return 0;                                /* pt2pt_statistics returns 1 (:25-27) */
-    if (xg_rendezvous(rank, procs, uid, path, sizeof path)) DIE("rendezvous failed");
-    if (xg_init(&ctx, rank, procs, xg_env_int("LOCAL_RANK", "MPI_LOCALRANKID", rank), uid)) DIE("xg_init failed");
+    /* XG_PT2PT_SELF=1 (test hook, one process): rank 1's sends become self sends of rank 0 on a
+     * 1-rank RCCL communicator, so the timing loop and report run on a one-GPU box */
+    const int self = procs == 1 && getenv("XG_PT2PT_SELF") && atoi(getenv("XG_PT2PT_SELF"));
+    if (procs != 2 && !self) return 0;                       /* pt2pt_statistics returns 1 (:25-27) */
+    if (self) setenv("XG_SELF_COMM", "1", 1);
+    else if (xg_rendezvous(rank, procs, uid, path, sizeof path)) DIE("rendezvous failed");
+    if (xg_init(&ctx, rank, procs, xg_env_int("LOCAL_RANK", "MPI_LOCALRANKID", rank), self ? NULL : uid))
+        DIE("xg_init failed");
     if (xg_barrier(ctx)) DIE("barrier failed");
     if (rank == 0 && path[0]) unlink(path);
     {

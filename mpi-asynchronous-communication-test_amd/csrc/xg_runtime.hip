@@ -11,6 +11,7 @@
 // All on one HIP stream per context, so step s+1 starts after step s; the
 // cross-GPU order comes from RCCL send/recv matching.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 #include <rccl/rccl.h>
 
 #include <stdio.h>
@@ -108,8 +109,40 @@ extern "C" double xg_now(void)
 }
 
 // ------------------------------------------------------------------ context
+// RCCL writes its log -- and, under NCCL_DEBUG=WARN/VERSION, a version banner at
+// communicator creation -- to stdout unless NCCL_DEBUG_FILE says otherwise; stdout
+// here carries the reference's report (bin/test, bin/pt2pt_test) and bench.py's JSON
+// line, so send RCCL's output to stderr unless the user chose a file.  Called before
+// every first RCCL call (RCCL reads the variable when it first logs).
+static void rccl_log_to_stderr()
+{
+    if (!getenv("NCCL_DEBUG_FILE")) setenv("NCCL_DEBUG_FILE", "/dev/stderr", 0);
+}
+
+// RCCL 2.27 also prints a version banner (RCCL/HIP/ROCm version, host, library path)
+// straight to stdout when it creates a communicator: fd 1 points at fd 2 for that call.
+struct StdoutToStderr {
+    int saved;
+    StdoutToStderr() : saved(-1)
+    {
+        fflush(stdout);
+        saved = dup(1);
+        if (saved >= 0) dup2(2, 1);
+    }
+    ~StdoutToStderr()
+    {
+        fflush(stdout);
+        if (saved >= 0) {
+            dup2(saved, 1);
+            close(saved);
+        }
+    }
+};
+
 extern "C" int xg_get_unique_id(void *uid)
 {
+    rccl_log_to_stderr();
+    StdoutToStderr quiet;
     ncclUniqueId id;
     static_assert(sizeof(ncclUniqueId) == XG_UNIQUE_ID_BYTES, "unique id size");
     NCCLCHK(ncclGetUniqueId(&id));
@@ -154,11 +187,20 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->d_red, 64 * sizeof(double)));
+    rccl_log_to_stderr();
     if (nranks > 1) {
         ncclUniqueId id;
         if (!uid) return XG_EARG;
         memcpy(&id, uid, sizeof id);
+        StdoutToStderr quiet;
         NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
+    } else if (getenv("XG_SELF_COMM") && atoi(getenv("XG_SELF_COMM"))) {
+        // test hook: a 1-rank communicator, so the RCCL send/recv paths (xg_p2p_bench,
+        // bin/pt2pt_test) run as self send/recv on a one-GPU box
+        ncclUniqueId id;
+        StdoutToStderr quiet;
+        NCCLCHK(ncclGetUniqueId(&id));
+        NCCLCHK(ncclCommInitRank(&c->comm, 1, id, 0));
     }
     *out = c;
     return XG_OK;
@@ -792,6 +834,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
     for (int g = 0; g < n; ++g) HIPCHK(hipStreamSynchronize(plans[g]->ctx->stream));
     if (rccl && !c0->comm) {
         ncclUniqueId id;
+        StdoutToStderr quiet;
         NCCLCHK(ncclGetUniqueId(&id));
         NCCLCHK(ncclCommInitRank(&c0->comm, 1, id, 0));
     }
@@ -975,9 +1018,10 @@ extern "C" int xg_copy_ceiling(xg_ctx *c, int64_t bytes, int kind, int reps, dou
 extern "C" int xg_p2p_bench(xg_ctx *c, int64_t bytes, int mode, int reps, double *gbps, double *sec)
 {
     const int n = c->nranks, r = c->rank;
-    if (n < 2 || bytes <= 0 || reps < 1 || mode < 0 || mode > 2) return XG_EARG;
+    const bool self = n == 1 && c->comm && !c->virt;      // XG_SELF_COMM: rank 0 sends to itself
+    if ((n < 2 && !self) || bytes <= 0 || reps < 1 || mode < 0 || mode > 2) return XG_EARG;
     HIPCHK(hipSetDevice(c->device));
-    const int npeer = mode == 0 ? n - 1 : 1;
+    const int npeer = self ? 1 : (mode == 0 ? n - 1 : 1);
     uint8_t *sb, *rb;
     HIPCHK(hipMalloc(&sb, bytes * npeer));
     HIPCHK(hipMalloc(&rb, bytes * npeer));
@@ -988,7 +1032,10 @@ extern "C" int xg_p2p_bench(xg_ctx *c, int64_t bytes, int mode, int reps, double
     int rc = XG_OK;
     auto one = [&]() -> int {
         NCCLCHK(ncclGroupStart());
-        if (mode == 0) {
+        if (self) {
+            NCCLCHK(ncclSend(sb, (size_t)bytes, ncclUint8, 0, c->comm, c->stream));
+            NCCLCHK(ncclRecv(rb, (size_t)bytes, ncclUint8, 0, c->comm, c->stream));
+        } else if (mode == 0) {
             for (int k = 1; k < n; ++k) {
                 const int to = (r + k) % n, from = (r - k + n) % n;
                 NCCLCHK(ncclSend(sb + (int64_t)(k - 1) * bytes, (size_t)bytes, ncclUint8, to, c->comm, c->stream));
@@ -1016,7 +1063,7 @@ extern "C" int xg_p2p_bench(xg_ctx *c, int64_t bytes, int mode, int reps, double
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));
         const double s_rep = ms * 1e-3 / reps;
         if (sec) *sec = s_rep;
-        if (gbps) *gbps = (mode == 2 ? (r < 2 ? (double)bytes : 0.0) : (double)bytes * npeer) / s_rep / 1e9;
+        if (gbps) *gbps = (mode == 2 && !self ? (r < 2 ? (double)bytes : 0.0) : (double)bytes * npeer) / s_rep / 1e9;
     }
     HIPCHK(hipEventDestroy(e0));
     HIPCHK(hipEventDestroy(e1));

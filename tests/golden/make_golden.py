@@ -153,12 +153,36 @@ def main(selected=None):
         fp.write(u.stderr.replace(ref, "{argv0}"))
     work = tempfile.mkdtemp(prefix="xg_golden_")
     try:
+        if not selected or "pt2pt" in selected:
+            gen_pt2pt(work)
         for name, (P, args) in CONFIGS.items():
             if selected and name not in selected:
                 continue
             gen_config(name, P, args, work)
     finally:
         shutil.rmtree(work, ignore_errors=True)
+
+
+def gen_pt2pt(work):
+    """pt2pt_test (mpi_sendrecv_test.c): masked stdout at 2 processes (the measured case) and
+    1 process (only the status line, :25-27), and the CSV shape (one row per -k)."""
+    ref = os.path.join(REPO, "oracle", "_ref", "pt2pt_test")
+    outdir = os.path.join(HERE, "pt2pt")
+    os.makedirs(outdir, exist_ok=True)
+    meta = {"args": "-d 4096 -k 3 -i 5"}
+    for n in (1, 2):
+        csv_path = os.path.join(work, "sendrecv_results.csv")
+        if os.path.exists(csv_path):
+            os.unlink(csv_path)
+        out = subprocess.run([MPIEXEC, "-launcher", "fork", "-n", str(n), ref] + meta["args"].split(),
+                             capture_output=True, text=True, timeout=120, cwd=work)
+        assert out.returncode == 0, out.stderr
+        with open(os.path.join(outdir, "report_n%d.txt" % n), "w") as fp:
+            fp.write(mask_numbers(out.stdout))
+        meta["csv_rows_n%d" % n] = len(open(csv_path).read().splitlines()) if os.path.exists(csv_path) else None
+    with open(os.path.join(outdir, "meta.json"), "w") as fp:
+        json.dump(meta, fp, indent=1, sort_keys=True)
+    print("pt2pt", meta, flush=True)
 
 
 def gen_config(name, P, args, work):
