@@ -27,7 +27,9 @@ def xg(pkg):
 
 
 def golden_configs():
-    return sorted(n for n in os.listdir(GOLDEN) if os.path.isdir(os.path.join(GOLDEN, n)))
+    """the ./test configurations (tests/golden/pt2pt holds the pt2pt_test goldens)"""
+    return sorted(n for n in os.listdir(GOLDEN)
+                  if os.path.isdir(os.path.join(GOLDEN, n)) and os.path.exists(os.path.join(GOLDEN, n, "trace.txt.gz")))
 
 
 def load_golden(name):
