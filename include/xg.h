@@ -118,6 +118,8 @@ int xg_vplans_run_rccl(xg_plan *const *plans, int n, double *step_done);
  * the number of launches and their algorithmic HBM bytes (read + write). */
 int xg_ktime_begin(xg_ctx *ctx, int max_launches);
 int xg_ktime_end(xg_ctx *ctx, double *total_ms, int *launches, int64_t *bytes);
+/* After xg_ktime_end: launch k's time (ms) and algorithmic bytes (read + write). */
+int xg_ktime_launch(xg_ctx *ctx, int k, double *ms, int64_t *bytes);
 
 /* HBM copy ceiling microbenchmark on `bytes` contiguous bytes: kind 0 grid-stride
  * float4 copy, 1 copy_kernel over 64 KiB pieces, 2 span_copy_kernel; *gbps counts

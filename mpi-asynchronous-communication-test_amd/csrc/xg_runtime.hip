@@ -440,6 +440,9 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     HIPCHK(hipSetDevice(c->device));
     xg_plan *p = new xg_plan();
     p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant;
+    // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
+    // pieces for small launches were measured no faster, and slower where they stop
+    // dividing the segment size (profiles/r01_min_pieces_ab.txt)
     const int64_t chunk = c->chunk;
     std::vector<xgk::DCopy> pieces;
     auto add = [&](const xg_copy &cp) -> bool {
@@ -940,6 +943,16 @@ extern "C" int xg_ktime_end(xg_ctx *c, double *total_ms, int *launches, int64_t 
     if (total_ms) *total_ms = tot;
     if (launches) *launches = c->nk;
     if (bytes) *bytes = b;
+    return XG_OK;
+}
+
+extern "C" int xg_ktime_launch(xg_ctx *c, int k, double *ms, int64_t *bytes)
+{
+    if (k < 0 || k >= c->nk || c->kt_on) return XG_EARG;
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, c->kev[2 * k], c->kev[2 * k + 1]));
+    if (ms) *ms = t;
+    if (bytes) *bytes = c->kbytes[k];
     return XG_OK;
 }
 

@@ -314,6 +314,7 @@ def device():
         d.xg_plan_engine.argtypes = [vp]
         d.xg_ktime_begin.argtypes = [vp, ip]
         d.xg_ktime_end.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(ip), C.POINTER(i64)]
+        d.xg_ktime_launch.argtypes = [vp, ip, C.POINTER(C.c_double), C.POINTER(i64)]
         d.xg_set_copy_params.argtypes = [vp, i64, ip]
         d.xg_copy_ceiling.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double)]
         d.xg_p2p_bench.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -397,6 +398,15 @@ class Context:
         ms, n, b = C.c_double(), C.c_int(), C.c_int64()
         _check(_dev.xg_ktime_end(self._c, C.byref(ms), C.byref(n), C.byref(b)), "xg_ktime_end")
         return ms.value, n.value, b.value
+
+    def ktime_launches(self, n):
+        """per-launch (ms, algorithmic bytes) of the last kernel-timing session"""
+        out = []
+        for k in range(n):
+            ms, b = C.c_double(), C.c_int64()
+            _check(_dev.xg_ktime_launch(self._c, k, C.byref(ms), C.byref(b)), "xg_ktime_launch")
+            out.append((ms.value, b.value))
+        return out
 
     def close(self):
         if self._c:

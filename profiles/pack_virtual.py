@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Pack / unpack kernels of the 8-GPU plans on one MI355X (virtual GPUs, xg_vplans_run).
+
+BASELINE configs[2] shape: 64 logical ranks, 16 aggregators, -d 256 KiB, methods 5 and 8
+(MPI_Alltoallw -> per-peer pack into one staging buffer, grouped send/recv, unpack).  All 8
+GPUs' plans run on this device, every cross-GPU segment packed (pack_max_seg = 1 GiB), each
+RCCL pair moved as one device copy.  Run under rocprofv3 --kernel-trace; pack_summary.py
+reduces the trace to HBM GB/s per launch class (local gather, pack, unpack).  The local
+gather of a step that also exchanges runs on a side stream beside the packs (as on real
+GPUs), so its launches overlap others.  Delivery is verified before the profiled
+repetitions."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import __graft_entry__ as G  # noqa: E402
+
+xg = G.load_package().xg
+P, A, d, GPUS, REPS = 64, 16, 256 << 10, 8, int(os.environ.get("REPS", "10"))
+rl = xg.aggregator_list(P, A)
+ctxs = [xg.Context.virtual(g, GPUS, device=0) for g in range(GPUS)]
+for m in (5, 8):
+    s = xg.Schedule(m, P, A, d, 200000000, rl, ntimes=1)
+    runs = [xg.MethodRun(c, s, it=0, mode=0, pack_max_seg=1 << 30) for c in ctxs]
+    xg.run_virtual(runs)
+    bad = sum(sum(1 for b in r.verify()[1] if b) for r in runs)
+    if bad:
+        raise SystemExit("m%d: %d bad slots" % (m, bad))
+    for _ in range(REPS):
+        xg.run_virtual(runs)
+    for r in runs:
+        r.close()
+    print("m%d ok: %d GPUs x %d reps, every cross-GPU segment packed" % (m, GPUS, REPS), flush=True)
+for c in ctxs:
+    c.close()
