@@ -95,3 +95,22 @@ def test_strong_fingerprint_multi_gpu(xg, worlds, G, method):
         assert nb == 0, (method, G, src, dst)
         local = off - s.recv_offset(G, dst)
         assert ck == O.chk64(exp[dst][local: local + d]), (method, G, src, dst)
+
+
+@pytest.mark.parametrize("G", (2, 8))
+@pytest.mark.parametrize("method", [1, 2, 5, 8, 9, 10])
+def test_config2_full_size_through_rccl(xg, worlds, G, method):
+    """BASELINE configs[2] at full size (P64 A16 -d 256 KiB) as a G-GPU job on this device,
+    every cross-GPU segment through RCCL (1-rank communicator), packed and direct: zero
+    mismatching bytes against the closed-form strong fingerprint, sampled checksums equal
+    the oracle's (size-independent check: the CPU oracle does not replay 256 MiB here)."""
+    import xg_oracle as O
+    P, A, d, it = 64, 16, 256 << 10, 2
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(method, P, A, d, 200000000, rl, ntimes=1, iteration=it)
+    for pack in (0, 1 << 30):
+        res = _run_job(xg, worlds[G], s, it, 1, pack, rccl=True)
+        assert len(res) == P * A
+        assert all(nb == 0 for _slot, _ck, nb, _fb in res), (method, G, pack)
+        for (src, seed, _dst, _off), ck, _nb, _fb in res[:: max(1, len(res) // 6)]:
+            assert ck == O.chk64(O.fingerprint(1, src, seed, it, d)), (method, G, pack, src, seed)
