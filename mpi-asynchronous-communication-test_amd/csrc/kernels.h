@@ -10,11 +10,16 @@
 //  fill_kernel   fill_buffer / MAP_DATA (mpi_test.c:71-77, :23): byte o of a
 //                segment of `rank` with seed `seed` = (rank + o + seed + iter)
 //                mod 256, produced 16 bytes per lane with SWAR byte adds.
-//  copy_kernel   the exchange itself: one workgroup per <= chunk-byte piece of
-//                a segment transfer (local gather/scatter, pack into and unpack
+//  copy_kernel_g the exchange itself (default variant; copy_kernel / copy_kernel_b
+//                are measured alternatives): one workgroup per <= chunk-byte piece
+//                of a segment transfer (local gather/scatter, pack into and unpack
 //                out of RCCL staging).  Replaces the shared-memory copies MPI
 //                does inside Irecv/Issend/Alltoallw.
+//  step_engine_kernel  a whole GPU-local plan of small steps in one persistent
+//                launch: bursts per step, grid barrier + wall-clock stamp between.
 //  verify_kernel check_buffer (mpi_test.c:83-92) + xg_chk64 per receive slot.
+//  span_*, read_only, write_only, gridstride_copy: HBM ceiling microbenchmarks
+//                (xg_copy_ceiling), not on the exchange path.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
