@@ -306,8 +306,13 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_b(const DCopy *__restric
 // workgroups, then a grid barrier whose last arriver stamps the step's
 // completion time (wall clock).  No workgroup reads bytes another writes in
 // this launch (every piece reads SEND and writes RECV), so the barrier orders
-// and times steps but publishes no data: each workgroup drains its stores
-// (vmcnt(0)) before its arrival ticket, and the kernel end makes them visible.
+// and times steps but publishes no data, and the kernel end makes the stores
+// visible.  A workgroup arrives as soon as its stores of step s are ISSUED
+// (they may still land while step s+1 runs: -7..12 % per run of the
+// sync/pairwise chains, profiles/r01_engine_drain_ab.txt), except at steps the
+// host flags (engine_drains): there it waits for them first, so a step that
+// rewrites or reads bytes of an earlier step sees them complete.  The last step
+// always drains, so its stamp -- the anchor of every step time -- is a delivered time.
 // State (cumulative ticket counter + timeout word) is zeroed by a memset before
 // every launch; spins are bounded, and a timed-out workgroup sets *tmo and
 // leaves, so a broken residency assumption ends the launch instead of hanging.
@@ -340,6 +345,7 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
     // pending (into v[]) and stored once it opens: the load latency of each step
     // (HBM + address translation of fresh pages) overlaps the barrier.  pf is
     // workgroup-uniform.
+    const int *drain = step_begin + nsteps + 1;     // per-step flags (host: engine_drains)
     bool pf = false;
     DCopy nc = {nullptr, nullptr, 0};
     u32x4 v[B];
@@ -358,7 +364,7 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
             else
                 for (int64_t k = threadIdx.x; k < c.len; k += kThreads) c.dst[k] = c.src[k];
         }
-        __builtin_amdgcn_s_waitcnt(kVmcnt0);                // this wave's stores of step s performed
+        if (drain[s]) __builtin_amdgcn_s_waitcnt(kVmcnt0);  // this wave's stores so far performed
         __syncthreads();
         const unsigned target = base + (unsigned)(s + 1) * W;
         bool last = false;

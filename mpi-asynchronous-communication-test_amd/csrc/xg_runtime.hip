@@ -19,6 +19,7 @@
 #include <string.h>
 #include <time.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "kernels.h"
@@ -54,6 +55,7 @@ struct xg_ctx {
     int64_t chunk;          // bytes per copy workgroup
     int64_t engine_max_step;   // GPU-local plans whose largest step moves <= this many bytes use the step engine
     int engine_wmax;           // at most this many (co-resident) engine workgroups
+    int engine_drain;          // 1: always drain before each barrier arrival (XG_ENGINE_DRAIN=1)
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant
     // kernel timing session (xg_ktime_begin/end)
@@ -93,8 +95,9 @@ struct xg_plan {
     // step engine (one persistent launch for the whole plan), or engine_w == 0
     int engine_w;
     int engine_b;                  // 16-B loads per lane per unit (1, 4, 16)
-    int *d_step_begin;
+    int *d_step_begin;             // nsteps + 1 unit offsets, then nsteps drain flags
     xgk::DCopy *d_epieces;         // the engine's work units, step-major
+    int engine_ndrain;             // steps whose barrier arrival waits for the stores (engine_drains)
     xgk::EngineState *d_engine;    // state (16 B, zeroed at load) followed by nsteps stamps
     unsigned engine_base;          // barrier tickets taken by earlier launches (wraps)
     bool engine_reset;             // zero the state before the next launch
@@ -179,6 +182,8 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     env = getenv("XG_ENGINE_WG");
     c->engine_wmax = env && atoi(env) > 0 ? atoi(env) : 256;    // one per CU
     if (c->engine_wmax > 1024) c->engine_wmax = 1024;
+    env = getenv("XG_ENGINE_DRAIN");         // "1": drain every step even without a hazard
+    c->engine_drain = env && !strcmp(env, "1");
     {
         int khz = 0;
         HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
@@ -423,6 +428,46 @@ extern "C" int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_
 }
 
 // ------------------------------------------------------------------ plans
+// Per-step drain flags of the step engine: flag[t] = 1 makes every workgroup wait
+// for its stores (vmcnt 0) before arriving at step t's barrier, which completes
+// every store issued up to step t.  Step t drains when step t+1 writes or reads
+// bytes that a step since the previous drain wrote (the same receive slots
+// rewritten by the next -k repetition, typically: one drain per repetition);
+// the last step always drains (its stamp anchors every step time).  force: all.
+static std::vector<int> engine_drains(const std::vector<std::vector<xgk::DCopy>> &xfer, bool force)
+{
+    const int n = (int)xfer.size();
+    std::vector<int> fl(n, force ? 1 : 0);
+    std::vector<std::pair<uintptr_t, uintptr_t>> pend;     // writes since the last drain, sorted
+    std::vector<uintptr_t> pmax;                             // prefix max of their ends
+    auto hits = [&](uintptr_t a, uintptr_t b) {              // does [a, b) meet a pending write?
+        const size_t i = std::lower_bound(pend.begin(), pend.end(), std::make_pair(b, (uintptr_t)0)) - pend.begin();
+        return i > 0 && pmax[i - 1] > a;
+    };
+    for (int u = 1; u < n && !force; ++u) {
+        const size_t m = pend.size();
+        for (const xgk::DCopy &x : xfer[u - 1])
+            if (x.len > 0) pend.push_back({(uintptr_t)x.dst, (uintptr_t)x.dst + (uintptr_t)x.len});
+        std::sort(pend.begin() + m, pend.end());
+        std::inplace_merge(pend.begin(), pend.begin() + m, pend.end());
+        pmax.resize(pend.size());
+        for (size_t i = 0; i < pend.size(); ++i) pmax[i] = std::max(i ? pmax[i - 1] : 0, pend[i].second);
+        bool hit = false;
+        for (const xgk::DCopy &x : xfer[u])
+            if (x.len > 0 && (hits((uintptr_t)x.dst, (uintptr_t)x.dst + (uintptr_t)x.len) ||
+                              hits((uintptr_t)x.src, (uintptr_t)x.src + (uintptr_t)x.len))) {
+                hit = true;
+                break;
+            }
+        if (hit) {
+            fl[u - 1] = 1;
+            pend.clear();
+        }
+    }
+    if (n) fl[n - 1] = 1;
+    return fl;
+}
+
 extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_plan **out)
 {
     if (!c || !r || !dp || !out) return XG_EARG;
@@ -567,6 +612,10 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             p->engine_b = maxstep <= (1 << 20) ? 1 : (maxstep <= (4 << 20) ? 4 : 16);
             const int maxu = cut((int64_t)p->engine_b * xgk::kThreads * 16, ep, sb);
             p->engine_w = maxu < 1 ? 1 : (maxu > c->engine_wmax ? c->engine_wmax : maxu);
+            const std::vector<int> fl = engine_drains(xfer, c->engine_drain);  // after the step begins
+            p->engine_ndrain = 0;
+            for (int f : fl) p->engine_ndrain += f;
+            sb.insert(sb.end(), fl.begin(), fl.end());
             HIPCHK(hipMalloc(&p->d_step_begin, sizeof(int) * sb.size()));
             HIPCHK(hipMemcpy(p->d_step_begin, sb.data(), sizeof(int) * sb.size(), hipMemcpyHostToDevice));
             if (!ep.empty()) {
