@@ -102,7 +102,8 @@ int xg_plan_enqueue(xg_plan *p);
 /* Workgroups of the plan's step engine (one persistent launch runs every step of a
  * GPU-local plan of small steps, grid barrier + wall-clock stamp per step), or 0
  * when each step is its own launches.  XG_ENGINE_MAX_STEP (bytes, 0 = off) and
- * XG_ENGINE_WG tune the choice at xg_init. */
+ * XG_ENGINE_WG tune the choice at xg_init; XG_ENGINE_DRAIN=1 drains every step's
+ * stores before its barrier (default: only before a step that rewrites earlier bytes). */
 int xg_plan_engine(const xg_plan *p);
 /* plans[g] = GPU g's plan of one virtual job (xg_init_virtual, g = 0..n-1, same
  * schedule); step_done[nsteps]: device seconds from start to the end of each step. */
