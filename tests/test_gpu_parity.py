@@ -156,3 +156,42 @@ def test_step_engine_matches_per_step_launches(xg, ctx, method, d):
         assert res["engine"] == res["eager"]
     finally:
         ctx_eager.close()
+
+
+@pytest.mark.parametrize("k", [1, 3])
+@pytest.mark.parametrize("method", [6, 9, 12])
+def test_step_engine_drain_scan(xg, ctx, method, k):
+    """The engine waits for a step's stores only at the steps its host hazard scan flags
+    (before the next -k repetition rewrites the same slots, and the last step).  Same
+    bytes and ordered step times as with XG_ENGINE_DRAIN=1 (drain at every step)."""
+    import os
+    import xg_oracle as O
+    P, A, d, c, it = 32, 14, 2048, 3, 0
+    rl = xg.aggregator_list(P, A)
+    os.environ["XG_ENGINE_DRAIN"] = "1"
+    try:
+        ctx_drain = xg.Context(rank=0, nranks=1, device=0)
+    finally:
+        del os.environ["XG_ENGINE_DRAIN"]
+    try:
+        s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, iteration=it)
+        exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
+        res = {}
+        for name, cx in (("scan", ctx), ("drain", ctx_drain)):
+            run = xg.MethodRun(cx, s, it=it, mode=1)
+            try:
+                assert run.engine_workgroups > 0
+                done, _post, wall = run.run_timed()
+                assert all(0 <= a <= b for a, b in zip(done, done[1:])), done
+                assert done[-1] <= wall + 1e-4
+                chk, bad, _f = run.verify()
+                assert all(b == 0 for b in bad), name
+                for (src, seed, dst, off), ck in zip(run.slots, chk):
+                    local = off - s.recv_offset(1, dst)
+                    assert ck == O.chk64(exp[dst][local: local + d]), (name, method, src, dst)
+                res[name] = chk
+            finally:
+                run.close()
+        assert res["scan"] == res["drain"]
+    finally:
+        ctx_drain.close()
