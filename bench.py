@@ -11,15 +11,23 @@ reference (prepare_*_data is untimed).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-N > 1 is launched by torch.distributed.run (one process per GPU; RANK /
-WORLD_SIZE / LOCAL_RANK from the env): the same 32 logical ranks are
-block-mapped onto N GPUs and cross-GPU segments move with grouped RCCL
-send/recv (strong scaling).  The process never imports torch: barrier,
-MAX-reduction and device sync go through the framework's own C-ABI (RCCL +
-hipDeviceSynchronize), and the RCCL id is handed over through a file.
+One process per GPU.  N > 1 either under a launcher that sets RANK /
+WORLD_SIZE / LOCAL_RANK (torch.distributed.run, mpiexec) or on its own: with
+no WORLD_SIZE in the environment `--gpus N` makes this process a parent that
+never touches the GPU -- it runs the host-MPI baseline, starts N child
+processes of itself (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE and one
+rendezvous key set), waits for all of them, fails with the highest child exit
+code if any fails, and prints rank 0's JSON line with the baseline attached.
+The same 32 logical ranks are block-mapped onto N GPUs and cross-GPU segments
+move with grouped RCCL send/recv (strong scaling).  The processes never import
+torch: barrier, MAX-reduction and device sync go through the framework's own
+C-ABI (RCCL + hipDeviceSynchronize), and the RCCL id is handed over through a
+file.
 
 Before timing, every method's delivery is verified on the GPU (byte-exact
-against the fingerprint); the bench aborts on any mismatch.
+against the fingerprint); the bench aborts on any mismatch.  After timing, the
+step engine's timeout word is checked (a timed-out barrier would have moved
+only part of the bytes).
 """
 import argparse
 import json
@@ -27,6 +35,7 @@ import os
 import re
 import shutil
 import subprocess
+import threading
 import sys
 import time
 
@@ -55,7 +64,9 @@ def parse():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ktime", action="store_true",
-                    help="skip the roofline pass (no kernel-timing events at all)")
+                    help="N > 1: skip the per-launch roofline pass")
+    ap.add_argument("--child-timeout", type=float, default=0,
+                    help="parent mode: seconds before the children are stopped (0: none)")
     ap.add_argument("--cpu-reps", type=int, default=10, help="-k of the reference CPU run")
     return ap.parse_args()
 
@@ -113,13 +124,103 @@ def cpu_baseline_port(a, methods, note=""):
                       % (",".join(map(str, methods)), note)}
 
 
+# ---------------------------------------------------------------- N-GPU job without a launcher
+def spawn_ranks(a):
+    """Parent of an N-GPU job (no WORLD_SIZE in the environment): never touches the GPU.
+    Runs the host-MPI baseline, starts one child process of this script per GPU
+    (subprocess, not exec), waits, and prints rank 0's JSON line with the baseline
+    attached.  Exit code: the highest child exit code (a failed child stops the rest).
+    XG_BENCH_CHILD_STUB=1 (test hook): each child prints its rank environment and exits
+    with the code XG_BENCH_STUB_RC lists for it; the parent prints them all."""
+    stub = os.environ.get("XG_BENCH_CHILD_STUB") == "1"
+    methods = [int(x) for x in a.methods.split(",")]
+    cpu = None
+    if not a.no_cpu_baseline and not stub:
+        cpu = cpu_baseline(a, methods)
+    key = "bench%d_%d" % (os.getpid(), int(time.time() * 1e3))
+    argv = [x for x in sys.argv[1:]]
+    if "--no-cpu-baseline" not in argv:
+        argv.append("--no-cpu-baseline")
+    procs, outs = [], []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), XG_RDZV_KEY=key, XG_BENCH_PARENT=str(os.getpid()))
+        p = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                             stdout=subprocess.PIPE, text=True)
+        procs.append(p)
+        outs.append([])
+    readers = []
+    for p, o in zip(procs, outs):
+        t = threading.Thread(target=lambda p=p, o=o: o.extend(p.stdout), daemon=True)
+        t.start()
+        readers.append(t)
+    t0, failed_at = time.time(), None
+    while any(p.poll() is None for p in procs):
+        time.sleep(0.2)
+        rcs = [p.poll() for p in procs]
+        if failed_at is None and any(rc not in (None, 0) for rc in rcs):
+            failed_at = time.time()
+            sys.stderr.write("bench: rank(s) %s failed; stopping the others\n"
+                             % [r for r, rc in enumerate(rcs) if rc not in (None, 0)])
+        late = a.child_timeout and time.time() - t0 > a.child_timeout
+        if (failed_at is not None and time.time() - failed_at > 10) or late:
+            if late and failed_at is None:
+                failed_at = time.time()
+                sys.stderr.write("bench: children still running after %.0f s; stopping them\n" % a.child_timeout)
+            for p in procs:            # exact PIDs of this job's children
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.time() + 10
+            while any(p.poll() is None for p in procs) and time.time() < deadline:
+                time.sleep(0.2)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+    for t in readers:
+        t.join(timeout=5)
+    rcs = [p.wait() for p in procs]
+    rc = max((abs(x) if x < 0 else x) for x in rcs)
+    if stub:
+        kids = []
+        for o in outs:
+            kids += [json.loads(line) for line in o if line.startswith("{")]
+        print(json.dumps({"stub": True, "children": kids, "rcs": rcs, "rc": rc}))
+        return rc
+    for r, o in enumerate(outs):          # anything the children printed besides the JSON line
+        for line in o:
+            if not (r == 0 and line.startswith("{")):
+                sys.stderr.write(line)
+    lines = [line for line in outs[0] if line.startswith("{")]
+    if rc or not lines:
+        sys.stderr.write("bench: %d-GPU job failed (child exit codes %s)\n" % (a.gpus, rcs))
+        return rc or 1
+    out = json.loads(lines[-1])
+    out["cpu_baseline"] = cpu
+    out["launch"] = "bench.py parent: %d child processes (subprocess), one per GPU" % a.gpus
+    print(json.dumps(out))
+    return 0
+
+
+def child_stub():
+    """XG_BENCH_CHILD_STUB=1: report the rank environment the parent gave this child."""
+    r = int(os.environ["RANK"])
+    rcs = [int(x) for x in os.environ.get("XG_BENCH_STUB_RC", "").split(",") if x.strip()]
+    print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "XG_RDZV_KEY",
+                                                     "XG_BENCH_PARENT")}))
+    return rcs[r] if r < len(rcs) else 0
+
+
 # ---------------------------------------------------------------- rendezvous (no torch)
 def rendezvous_uid(xg, rank, world):
-    port = os.environ.get("MASTER_PORT", "0")
-    run = os.environ.get("TORCHELASTIC_RUN_ID", "")
-    # the launcher (torchrun agent) is the parent of every local rank: its pid keeps a
-    # stale file of an earlier launch on the same port from matching
-    path = "/tmp/xg_bench_rdzv_%s_%s_pp%d.bin" % (port, re.sub(r"[^A-Za-z0-9_-]", "_", run), os.getppid())
+    key = os.environ.get("XG_RDZV_KEY")
+    if key:
+        path = "/tmp/xg_bench_rdzv_%s.bin" % re.sub(r"[^A-Za-z0-9_-]", "_", key)
+    else:
+        port = os.environ.get("MASTER_PORT", "0")
+        run = os.environ.get("TORCHELASTIC_RUN_ID", "")
+        # the launcher (torchrun agent) is the parent of every local rank: its pid keeps a
+        # stale file of an earlier launch on the same port from matching
+        path = "/tmp/xg_bench_rdzv_%s_%s_pp%d.bin" % (port, re.sub(r"[^A-Za-z0-9_-]", "_", run), os.getppid())
     t_start = time.time()
     if rank == 0:
         uid = xg.unique_id()
@@ -131,20 +232,25 @@ def rendezvous_uid(xg, rank, world):
     while True:
         try:
             st = os.stat(path)
-            if st.st_mtime >= t_start - 60:
+            # rank 0 may run the host-MPI baseline before it writes the id (launcher mode)
+            if st.st_mtime >= t_start - 900:
                 with open(path, "rb") as f:
                     uid = f.read()
                 if len(uid) == 128:
                     return uid, None
         except FileNotFoundError:
             pass
-        if time.time() - t_start > 180:
+        if time.time() - t_start > 900:
             raise RuntimeError("rank %d: no RCCL id at %s" % (rank, path))
         time.sleep(0.01)
 
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return spawn_ranks(a)
+    if os.environ.get("XG_BENCH_CHILD_STUB") == "1":
+        return child_stub()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -152,9 +258,10 @@ def main():
         raise SystemExit("WORLD_SIZE=%d but --gpus %d" % (world, a.gpus))
     methods = [int(x) for x in a.methods.split(",")]
 
-    # CPU baseline first, before this process touches the GPU (rank 0, N=1 only)
+    # host-MPI baseline first, before this process touches the GPU (rank 0; a parent
+    # process of an N-GPU job runs it itself and passes --no-cpu-baseline)
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, methods)
 
     import __graft_entry__ as G
@@ -182,6 +289,7 @@ def main():
         for _ in range(reps):
             r.enqueue()
         ctx.device_sync()
+        r.check()
         return ctx.allreduce_max([time.perf_counter() - t0])[0] / reps
 
     # N > 1: per method, pick by measurement whether cross-GPU segments go to RCCL
@@ -229,38 +337,58 @@ def main():
         for r in runs:
             r.enqueue()
 
+    def check_all():
+        for r in runs:
+            r.check()
+
     for _ in range(a.warmup):
         step()
     ctx.device_sync()
+    check_all()
 
-    # timed region: K steps, nothing but the exchange on the stream
+    # timed region: K steps, nothing but the exchange on the stream.  One HIP event
+    # pair brackets the whole region on that stream (kernel-timing session, region
+    # mode): with nothing but copy launches in it (N = 1) its device time over the
+    # number of launches is the copy kernel's average launch duration, gaps between
+    # back-to-back launches included.
+    launches_per_step = sum(r.launches for r in runs)
+    region = world == 1 and not any(r.view.p2p for r in runs)
     ctx.barrier()
     ctx.device_sync()
     t0 = time.perf_counter()
+    if region:
+        ctx.ktime_begin(per_launch=False)
     for _ in range(a.steps):
         step()
+    # the region's end event goes in right behind the last launch, before the host waits:
+    # its device time is then inside the host-timed interval [t0, t1]
+    kms, nlaunch, kbytes = ctx.ktime_end() if region else (0.0, 0, 0)
     ctx.device_sync()
     t1 = time.perf_counter()
+    check_all()
     ctx.barrier()
     elapsed = ctx.allreduce_max([t1 - t0])[0]
-
-    # roofline pass: the same K steps again with a HIP event pair around every copy launch
-    # (on the stream it runs on).  The events cost ~7 us per launch of device time, so this
-    # pass is kept out of `value`; its own wall time is reported beside it.
-    kms, nlaunch, kbytes, elapsed_kt = 0.0, 0, 0, None
-    if not a.no_ktime:
-        launches_per_step = sum(4 * len(r.view.steps) for r in runs)   # <= stage, local, pack, post per step
+    how = None
+    if region:
+        how = ("one HIP event pair on the exchange stream around the timed region itself (%d back-to-back "
+               "launches; launch gaps included)" % nlaunch)
+    elif not a.no_ktime:
+        # N > 1 the region also holds RCCL: a second pass of the same K steps with an
+        # event pair around every copy launch (the events cost ~7 us of device time
+        # per launch, so this pass is kept out of `value`)
         ctx.barrier()
         ctx.device_sync()
-        ctx.ktime_begin(max(1, launches_per_step * a.steps))
+        ctx.ktime_begin(max(1, launches_per_step * a.steps), per_launch=True)
         t2 = time.perf_counter()
         for _ in range(a.steps):
             step()
         ctx.device_sync()
         t3 = time.perf_counter()
         kms, nlaunch, kbytes = ctx.ktime_end()
+        check_all()
         ctx.barrier()
-        elapsed_kt = ctx.allreduce_max([t3 - t2])[0]
+        how = ("HIP events around every copy launch, on its stream, over a second pass of the same %d steps "
+               "(that pass: %.4f ms per step)" % (a.steps, ctx.allreduce_max([t3 - t2])[0] / a.steps * 1e3))
 
     seg_bytes = float(a.procs) * a.aggs * a.size * len(methods) * a.steps
     value = seg_bytes / elapsed / 1e9
@@ -283,30 +411,35 @@ def main():
                                "(xg_p2p_bench mode 0)" % (per_pair, world)}
     if rank != 0:
         ctx.close()
-        return
+        return 0
     roof = None
     if nlaunch:
         avg_s = kms / nlaunch / 1e3
         per_launch = kbytes / nlaunch
         achieved = per_launch / avg_s / 1e9
-        traffic = None
+        if region and avg_s * launches_per_step > elapsed / a.steps * 1.001:
+            raise SystemExit("bench: kernel time %.1f us x %d launches exceeds the step time %.1f us"
+                             % (avg_s * 1e6, launches_per_step, elapsed / a.steps * 1e6))
+        traffic, traffic_src = None, None
         tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(tf):
             try:
-                traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+                pm = json.load(open(tf))
+                traffic, traffic_src = pm.get("hbm_bytes_per_launch"), pm.get("source")
             except (ValueError, OSError):
                 traffic = None
-        # the committed PMC figure is per launch of THIS workload at N = 1 (profiles/bench_rocprof.sh);
-        # any other launch size has not been counted
+        # the committed PMC figure is per launch of THIS workload at N = 1; any other
+        # launch size has not been counted
         if traffic and (world != 1 or abs(traffic - per_launch) > 0.05 * per_launch):
             traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": ("committed PMC measurement of this bench command (not counted in this run): "
+                                   "profiles/pmc_traffic.json, %s" % traffic_src) if traffic else None,
                 "kernel": "copy_kernel (intra-GPU gather/scatter)", "launches": nlaunch,
+                "launches_per_step": launches_per_step,
                 "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": int(per_launch),
-                "measured": "HIP events around every copy launch, on its stream, over a second pass of "
-                            "the same %d steps (that pass: %.4f ms per step with the events)"
-                            % (a.steps, elapsed_kt / a.steps * 1e3)}
+                "measured": how}
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
@@ -317,6 +450,7 @@ def main():
                                % (a.procs, a.aggs, a.size, ",".join(map(str, methods)), a.comm_size),
                    "procs": a.procs, "cb_nodes": a.aggs, "data_size": a.size, "methods": methods,
                    "ranks_per_gpu": -(-a.procs // world), "device": arch, "cus": cus,
+                   "copy_variant": a.copy_variant if a.copy_variant >= 0 else int(os.environ.get("XG_COPY_VARIANT", 0)),
                    "parallelism": "block-mapped logical ranks; intra-GPU copy_kernel + grouped RCCL p2p"},
         "max_total_time_s": max_total,      # per method, one -k repetition, median of 3 warm runs
         "roofline": roof,
@@ -326,7 +460,8 @@ def main():
     }
     print(json.dumps(out))
     ctx.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

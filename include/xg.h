@@ -80,6 +80,9 @@ int xg_regions_poison(xg_regions *r);
 /* Device pointer of a region (for tests that read buffers back). */
 void *xg_regions_ptr(xg_regions *r, int buf);
 int xg_regions_read(xg_regions *r, int buf, int64_t off, void *host, int64_t len);
+/* Test hook: overwrite bytes of a region (e.g. corrupt one received byte to check
+ * that xg_verify reports it). */
+int xg_regions_write(xg_regions *r, int buf, int64_t off, const void *host, int64_t len);
 
 int xg_fill(xg_regions *r, const xg_segrun *runs, int nruns, int64_t d, int iter, int mode);
 /* Per slot: chk[i] = xg_chk64 of the slot bytes, bad[i] = number of bytes that
@@ -97,14 +100,27 @@ int xg_plan_nsteps(const xg_plan *p);
  * since the run started) and the host enqueue time; *wall = host seconds from
  * start to the final synchronisation. */
 int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall);
-/* Enqueue all steps once without events or synchronisation (bench loops). */
+/* Enqueue all steps once without events or synchronisation (bench loops).  Check
+ * the step engine's timeout word with xg_plan_check after synchronising. */
 int xg_plan_enqueue(xg_plan *p);
-/* Workgroups of the plan's step engine (one persistent launch runs every step of a
- * GPU-local plan of small steps, grid barrier + wall-clock stamp per step), or 0
- * when each step is its own launches.  XG_ENGINE_MAX_STEP (bytes, 0 = off) and
- * XG_ENGINE_WG tune the choice at xg_init; XG_ENGINE_DRAIN=1 drains every step's
- * stores before its barrier (default: only before a step that rewrites earlier bytes). */
+/* XG_EHIP if a step-engine workgroup gave up at a grid barrier since the last
+ * check (its launch then moved only part of the bytes); waits for the stream. */
+int xg_plan_check(xg_plan *p);
+/* Step engine: every maximal run of >= 2 GPU-local steps (no RCCL op, no in-loop
+ * barrier, no unpack, each <= XG_ENGINE_MAX_STEP bytes; 0 = off) is ONE persistent
+ * launch of up to one workgroup per CU (XG_ENGINE_WG lowers it), grid barrier +
+ * wall-clock stamp per step; the other steps are their own launches.
+ * xg_plan_engine: workgroups of the first such segment (0: none);
+ * xg_plan_engine_steps: steps inside segments (*nseg segments, *nhaz hazard
+ * barriers, xg_engine_hazards); XG_ENGINE_DRAIN=1 drains every step's stores. */
 int xg_plan_engine(const xg_plan *p);
+int xg_plan_engine_steps(const xg_plan *p, int *nseg, int *nhaz);
+/* Kernel launches of one run (copy + engine launches; RCCL's own kernels aside). */
+int xg_plan_launches(const xg_plan *p);
+/* Staging displacements of the plan's packed segments as computed on the device
+ * at load (one wavefront prefix scan per step and direction: the alltoallw
+ * translate of mpi_test.c:233-302).  out == NULL: returns their number. */
+int xg_plan_displs(const xg_plan *p, int64_t *out, int n);
 /* plans[g] = GPU g's plan of one virtual job (xg_init_virtual, g = 0..n-1, same
  * schedule); step_done[nsteps]: device seconds from start to the end of each step. */
 int xg_vplans_run(xg_plan *const *plans, int n, double *step_done);
@@ -113,19 +129,16 @@ int xg_vplans_run(xg_plan *const *plans, int n, double *step_done);
  * in issue order) and ncclAllReduce for the in-loop barriers -- RCCL's calls on
  * the real plan buffers with one GPU. */
 int xg_vplans_run_rccl(xg_plan *const *plans, int n, double *step_done);
-/* Kernel timing session: while active, every copy_kernel launch of any plan
- * on this context is bracketed by HIP events on the stream it runs on.
- * xg_ktime_end waits for the stream and returns the summed kernel time (ms),
+/* Kernel timing session.  mode 1: every copy / engine launch of any plan on this
+ * context is bracketed by HIP events on the stream it runs on (at most
+ * max_launches); mode 2: one event pair on the main stream around the whole
+ * session, launches and bytes counted.  xg_ktime_end waits for the stream and
+ * returns the kernel time (mode 1: summed per launch; mode 2: the session),
  * the number of launches and their algorithmic HBM bytes (read + write). */
-int xg_ktime_begin(xg_ctx *ctx, int max_launches);
+int xg_ktime_begin(xg_ctx *ctx, int max_launches, int mode);
 int xg_ktime_end(xg_ctx *ctx, double *total_ms, int *launches, int64_t *bytes);
-/* After xg_ktime_end: launch k's time (ms) and algorithmic bytes (read + write). */
+/* After a mode-1 session: launch k's time (ms) and algorithmic bytes (read + write). */
 int xg_ktime_launch(xg_ctx *ctx, int k, double *ms, int64_t *bytes);
-
-/* HBM copy ceiling microbenchmark on `bytes` contiguous bytes: kind 0 grid-stride
- * float4 copy, 1 copy_kernel over 64 KiB pieces, 2 span_copy_kernel; *gbps counts
- * read + write bytes. */
-int xg_copy_ceiling(xg_ctx *ctx, int64_t bytes, int kind, int reps, double *gbps);
 
 /* RCCL point-to-point ceiling (rccl-tests sendrecv analogue; GPU version of
  * pt2pt_test, mpi_sendrecv_test.c:15-74).  mode 0: all pairs, 1: ring,
@@ -134,8 +147,10 @@ int xg_copy_ceiling(xg_ctx *ctx, int64_t bytes, int kind, int reps, double *gbps
 int xg_p2p_bench(xg_ctx *ctx, int64_t bytes, int mode, int reps, double *gbps, double *sec);
 
 /* Tuning: bytes per copy workgroup (default 32768) and copy kernel variant
- * (default 5 = copy_kernel_g<4>; variant < 0 keeps the current one; see
- * DESIGN.md and profiles/r01_copy_ab.txt).  Applied to plans loaded afterwards. */
+ * (0 = copy_kernel_g<4>, global loads/stores; 1/2/3 = copy_kernel_b<4>, buffer
+ * loads/stores with plain / sc1 write-through / nt stores; variant < 0 keeps the
+ * current one; XG_COPY_VARIANT / XG_COPY_CHUNK at xg_init).  Applied to plans
+ * loaded afterwards. */
 int xg_set_copy_params(xg_ctx *ctx, int64_t chunk_bytes, int variant);
 
 /* ------------------------------------------------------------------ method operators

@@ -189,6 +189,18 @@ int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf);
 xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg);
 void xg_devplan_free(xg_devplan *p);
 
+/* Step engine ordering (xg.h xg_plan_engine; kernels.h step_engine_kernel).  The
+ * transfers of step s are xfer[step_begin[s] .. step_begin[s+1]) (device addresses
+ * as integers).  flags[s] says what the barrier after step s orders:
+ *   2  step s+1 reads bytes written since the last hazard point, or rewrites them
+ *      with other bytes (another source at another dst-src offset): stores drained
+ *      + agent release/acquire, and no early load of step s+1;
+ *   1  stores drained before arriving (the last step; every step with force);
+ *   0  nothing (identical rewrites of the -k repetitions are not hazards).
+ * Returns the number of hazard points (flag 2). */
+typedef struct { uint64_t src, dst, len; } xg_span;
+int xg_engine_hazards(const xg_span *xfer, const int *step_begin, int nsteps, int force, int *flags);
+
 /* fill: `nsegs` consecutive d-byte segments at `off` in the SEND region,
  * segment i = fingerprint(rank, seed0 + i, iter) (prepare_*_data loops). */
 typedef struct { int32_t rank, seed0; int64_t off; int32_t nsegs, pad; } xg_segrun;

@@ -10,8 +10,10 @@
  *    P defaults to the number of processes (as `mpiexec -n P`); host more
  *    logical ranks per GPU with --procs N or XG_PROCS=N.
  *  - Launch: single process, or any launcher that sets RANK/WORLD_SIZE
- *    (torchrun --no-python) or PMI_RANK/PMI_SIZE (mpiexec).  The RCCL unique
- *    id is handed over through a file in $XG_RDZV_DIR (default /tmp).
+ *    (torchrun --no-python) or PMI_RANK/PMI_SIZE (mpiexec), or on its own
+ *    with --gpus N (XG_GPUS=N): the process then starts the N GPU processes
+ *    itself (xg_spawn_ranks) and exits with their highest exit code.  The RCCL
+ *    unique id is handed over through a file in $XG_RDZV_DIR (default /tmp).
  *  - -m 0 runs methods 1..20 like the reference, TAM (15/16) included.
  *  - Extra, opt-in: --verify (or XG_VERIFY=1) checks every received byte on
  *    the GPU and prints one extra "| <label> verify ..." line per method;
@@ -155,7 +157,9 @@ int main(int argc, char **argv)
         {"fingerprint", required_argument, 0, 1002},
         {"eager-limit", required_argument, 0, 1003},
         {"pack-max-seg", required_argument, 0, 1004},
+        {"gpus", required_argument, 0, 1005},
         {0, 0, 0, 0}};
+    int ngpus = xg_env_int("XG_GPUS", NULL, 1);
     prefix[0] = '\0';
 
     rank = xg_env_int("RANK", "PMI_RANK", 0);
@@ -184,12 +188,20 @@ int main(int argc, char **argv)
         case 1002: fp_mode = !strcmp(optarg, "strong") ? XG_FP_STRONG : XG_FP_REFERENCE; break;
         case 1003: eager = atoll(optarg); break;
         case 1004: pack_max = atoll(optarg); break;
+        case 1005: ngpus = atoi(optarg); break;
         default:
             if (rank == 0) usage(argv[0]);
             return 0;
         }
     }
 
+    /* no launcher + --gpus N (XG_GPUS=N): start the N GPU processes ourselves */
+    if ((i = xg_spawn_ranks(ngpus, argv)) >= 0) return i;
+    if (getenv("XG_SPAWN_STUB")) {    /* test hook: report the rank environment and stop */
+        printf("spawn-stub RANK=%s LOCAL_RANK=%s WORLD_SIZE=%s XG_RDZV_KEY=%s\n", getenv("RANK"),
+               getenv("LOCAL_RANK"), getenv("WORLD_SIZE"), getenv("XG_RDZV_KEY"));
+        return 0;
+    }
     if (procs <= 0) procs = nranks;
     if (nranks > procs) DIE("more GPU processes (%d) than logical ranks (%d)", nranks, procs);
     if (cb_nodes < 1 || cb_nodes > procs) DIE("-a %d: need 1 <= aggregators <= ranks (%d)", cb_nodes, procs);

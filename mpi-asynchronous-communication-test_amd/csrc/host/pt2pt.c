@@ -6,7 +6,8 @@
  * :38-46) as RCCL send/recv over xGMI, with a barrier between measurements
  * (:48).  Rank 0 writes every measurement to sendrecv_results.csv and prints
  * the same summary line (:56-67).
- * Launch: torchrun --no-python --nproc-per-node 2 bin/pt2pt_test -d N -k K -i I
+ * Launch: torchrun --no-python --nproc-per-node 2 bin/pt2pt_test -d N -k K -i I, or
+ * XG_GPUS=2 bin/pt2pt_test -d N -k K -i I (the process starts both ranks itself).
  */
 #include <getopt.h>
 #include <math.h>
@@ -27,6 +28,8 @@ int main(int argc, char **argv)
     xg_ctx *ctx;
     rank = xg_env_int("RANK", "PMI_RANK", 0);
     procs = xg_env_int("WORLD_SIZE", "PMI_SIZE", 1);
+    /* no launcher: XG_GPUS=2 starts the two GPU processes (xg_spawn_ranks) */
+    if ((i = xg_spawn_ranks(xg_env_int("XG_GPUS", NULL, 1), argv)) >= 0) return i;
     while ((i = getopt(argc, argv, "hk:d:i:")) != EOF) {   /* :82-96 */
         switch (i) {
         case 'd': data_size = atoi(optarg); break;

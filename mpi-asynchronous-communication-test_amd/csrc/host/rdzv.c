@@ -4,12 +4,17 @@
  * poll.  Key: XG_RDZV_KEY, else MASTER_PORT + TORCHELASTIC_RUN_ID (torchrun),
  * else the parent pid (mpiexec / any launcher that forks all ranks).
  */
+#include <signal.h>
+#include <spawn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <time.h>
 #include <unistd.h>
+
+extern char **environ;
 
 #include "rdzv.h"
 #include "xg.h"
@@ -72,4 +77,76 @@ int xg_env_int(const char *a, const char *b, int dflt)
     const char *v = getenv(a);
     if (!v && b) v = getenv(b);
     return v ? atoi(v) : dflt;
+}
+
+/* environment of child r: this process's, with the rank variables replaced */
+static char **child_env(int r, int n, const char *key)
+{
+    size_t m = 0, i, k = 0;
+    char **env;
+    static const char *drop[] = {"RANK=", "LOCAL_RANK=", "WORLD_SIZE=", "LOCAL_WORLD_SIZE=", "XG_RDZV_KEY=", NULL};
+    while (environ[m]) m++;
+    env = (char **)calloc(m + 6, sizeof(char *));
+    for (i = 0; i < m; ++i) {
+        int j, skip = 0;
+        for (j = 0; drop[j]; ++j)
+            if (!strncmp(environ[i], drop[j], strlen(drop[j]))) skip = 1;
+        if (!skip) env[k++] = environ[i];
+    }
+    env[k] = (char *)malloc(32); snprintf(env[k++], 32, "RANK=%d", r);
+    env[k] = (char *)malloc(32); snprintf(env[k++], 32, "LOCAL_RANK=%d", r);
+    env[k] = (char *)malloc(32); snprintf(env[k++], 32, "WORLD_SIZE=%d", n);
+    env[k] = (char *)malloc(32); snprintf(env[k++], 32, "LOCAL_WORLD_SIZE=%d", n);
+    env[k] = (char *)malloc(160); snprintf(env[k++], 160, "XG_RDZV_KEY=%s", key);
+    env[k] = NULL;
+    return env;
+}
+
+int xg_spawn_ranks(int ngpus, char **argv)
+{
+    pid_t *pid;
+    int *st, r, left, worst = 0, failed = 0;
+    char key[128];
+    double t_fail = 0;
+    if (ngpus <= 1 || getenv("RANK") || getenv("WORLD_SIZE") || getenv("PMI_RANK") || getenv("PMI_SIZE")) return -1;
+    snprintf(key, sizeof key, "spawn%ld_%ld", (long)getpid(), (long)time(NULL));
+    pid = (pid_t *)calloc(ngpus, sizeof(pid_t));
+    st = (int *)calloc(ngpus, sizeof(int));
+    for (r = 0; r < ngpus; ++r) {
+        char **env = child_env(r, ngpus, key);
+        if (posix_spawn(&pid[r], "/proc/self/exe", NULL, NULL, argv, env)) {
+            perror("posix_spawn");
+            pid[r] = 0;
+            failed = 1;
+            worst = 1;
+        }
+    }
+    for (left = 0, r = 0; r < ngpus; ++r) left += pid[r] > 0;
+    while (left > 0) {
+        int status;
+        pid_t w = waitpid(-1, &status, WNOHANG);
+        if (w > 0) {
+            for (r = 0; r < ngpus; ++r)
+                if (pid[r] == w) {
+                    int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + WTERMSIG(status);
+                    st[r] = code;
+                    pid[r] = -1;
+                    left--;
+                    if (code > worst) worst = code;
+                    if (code && !failed) {
+                        fprintf(stderr, "rank %d failed (exit %d): stopping the job\n", r, code);
+                        failed = 1;
+                        t_fail = now_s();
+                    }
+                }
+            continue;
+        }
+        if (failed && now_s() - t_fail > 10)      /* the survivors would wait for a dead peer */
+            for (r = 0; r < ngpus; ++r)
+                if (pid[r] > 0) kill(pid[r], now_s() - t_fail > 20 ? SIGKILL : SIGTERM);
+        { struct timespec ts = {0, 50000000}; nanosleep(&ts, NULL); }
+    }
+    free(pid);
+    free(st);
+    return worst;
 }

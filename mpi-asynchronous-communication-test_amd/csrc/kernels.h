@@ -2,24 +2,25 @@
 //
 // All of this path is byte movement, HBM-bound; nothing is GEMM-shaped, so no
 // MFMA.  The rules that matter (MI355X_MICROARCH.md, cdna_hip_programming.md):
-// 16-B per lane accesses (global_load/store_dwordx4), several loads in flight
-// per lane before the first store, 256-thread workgroups (4 wave64s) and
-// >> 256 workgroups per launch.  No workgroup reads another's output inside a
-// launch, so no inter-workgroup hand-off protocol is needed.
+// 16-B per lane accesses (global_load/store_dwordx4, buffer_load/store_dwordx4),
+// several loads in flight per lane before the first store, 256-thread
+// workgroups (4 wave64s) and >> 256 workgroups per launch.  No workgroup of a
+// copy launch reads another's output, so only the step engine (below) needs an
+// inter-workgroup protocol.
 //
-//  fill_kernel   fill_buffer / MAP_DATA (mpi_test.c:71-77, :23): byte o of a
-//                segment of `rank` with seed `seed` = (rank + o + seed + iter)
-//                mod 256, produced 16 bytes per lane with SWAR byte adds.
-//  copy_kernel_g the exchange itself (default variant; copy_kernel / copy_kernel_b
-//                are measured alternatives): one workgroup per <= chunk-byte piece
-//                of a segment transfer (local gather/scatter, pack into and unpack
-//                out of RCCL staging).  Replaces the shared-memory copies MPI
-//                does inside Irecv/Issend/Alltoallw.
-//  step_engine_kernel  a whole GPU-local plan of small steps in one persistent
-//                launch: bursts per step, grid barrier + wall-clock stamp between.
-//  verify_kernel check_buffer (mpi_test.c:83-92) + xg_chk64 per receive slot.
-//  span_*, read_only, write_only, gridstride_copy: HBM ceiling microbenchmarks
-//                (xg_copy_ceiling), not on the exchange path.
+//  fill_kernel        fill_buffer / MAP_DATA (mpi_test.c:71-77, :23): byte o of a
+//                     segment of `rank` with seed `seed` = (rank + o + seed + iter)
+//                     mod 256, produced 16 bytes per lane with SWAR byte adds.
+//  copy_kernel_g / _b the exchange itself: one workgroup per <= chunk-byte piece of
+//                     a segment transfer (local gather/scatter, pack into and unpack
+//                     out of RCCL staging).  Replaces the shared-memory copies MPI
+//                     does inside Irecv/Issend/Alltoallw.  Misaligned pieces (-d not
+//                     a multiple of 16) are realigned through LDS.
+//  step_engine_kernel a whole GPU-local run of small steps in one persistent
+//                     launch: bursts per step, grid barrier + wall-clock stamp between.
+//  displ_scan_kernel  staging displacements of packed segments (wave64 prefix scan),
+//  displ_apply_kernel the device replacement of *_alltoall_translate (:233-302).
+//  verify_kernel      check_buffer (mpi_test.c:83-92) + xg_chk64 per receive slot.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -119,81 +120,14 @@ __global__ __launch_bounds__(kThreads) void fill_kernel(uint8_t *__restrict__ ba
 }
 
 // ---------------------------------------------------------------- copy
-template <bool NT>
-__device__ __forceinline__ void st16(uint4 *p, uint4 v)
-{
-    if constexpr (NT) {
-        __builtin_nontemporal_store(v.x, &p->x);
-        __builtin_nontemporal_store(v.y, &p->y);
-        __builtin_nontemporal_store(v.z, &p->z);
-        __builtin_nontemporal_store(v.w, &p->w);
-    } else {
-        *p = v;
-    }
-}
-
-// One workgroup per DCopy piece.  U independent 16-B loads per lane are in
-// flight before the first store (4 KiB per wave-group step, U*4 KiB per block
-// iteration).
-template <int U, bool NT>
-__global__ __launch_bounds__(kThreads) void copy_kernel(const DCopy *__restrict__ pieces)
-{
-    const DCopy c = pieces[blockIdx.x];
-    const uint8_t *s = c.src;
-    uint8_t *t = c.dst;
-    const int64_t n = c.len;
-    if ((((uintptr_t)s | (uintptr_t)t | (uint64_t)n) & 15) == 0) {
-        const uint4 *__restrict__ s4 = reinterpret_cast<const uint4 *>(s);
-        uint4 *__restrict__ t4 = reinterpret_cast<uint4 *>(t);
-        const int64_t n4 = n >> 4;
-        int64_t i = threadIdx.x;
-        for (; i + (int64_t)(U - 1) * kThreads < n4; i += (int64_t)U * kThreads) {
-            uint4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = s4[i + u * kThreads];
-#pragma unroll
-            for (int u = 0; u < U; ++u) st16<NT>(t4 + i + u * kThreads, v[u]);
-        }
-        for (; i < n4; i += kThreads) st16<NT>(t4 + i, s4[i]);
-    } else if ((((uintptr_t)s ^ (uintptr_t)t) & 3) == 0) {
-        // same 4-byte phase: byte head, dword body, byte tail
-        int64_t head = (4 - ((uintptr_t)s & 3)) & 3;
-        if (head > n) head = n;
-        if ((int64_t)threadIdx.x < head) t[threadIdx.x] = s[threadIdx.x];
-        const int64_t nw = (n - head) >> 2;
-        const uint32_t *s1 = reinterpret_cast<const uint32_t *>(s + head);
-        uint32_t *t1 = reinterpret_cast<uint32_t *>(t + head);
-        for (int64_t i = threadIdx.x; i < nw; i += kThreads) t1[i] = s1[i];
-        for (int64_t i = head + nw * 4 + threadIdx.x; i < n; i += kThreads) t[i] = s[i];
-    } else {
-        for (int64_t i = threadIdx.x; i < n; i += kThreads) t[i] = s[i];
-    }
-}
-
-// Global-address-space, software-pipelined variant: the next U 16-B loads of a
-// lane are issued before the current U stores, so U..2U loads stay in flight
-// and the compiler emits global_load/store_dwordx4 (vmcnt only) instead of
-// flat ops (which also wait on lgkmcnt).
+// Global-address-space, software-pipelined piece copy: the next U 16-B loads of
+// a lane are issued before the current U stores, so U..2U loads stay in flight
+// and the compiler emits global_load/store_dwordx4 (vmcnt only).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_cu4;
 typedef __attribute__((address_space(1))) u32x4 g_u4;
 
-// LP / SP: load / store cache policy, 0 = default, 1 = nontemporal (`nt` bit)
-template <int LP>
-__device__ __forceinline__ u32x4 ld16(g_cu4 *p)
-{
-    if constexpr (LP == 1) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-
-template <int SP>
-__device__ __forceinline__ void st16g(g_u4 *p, u32x4 v)
-{
-    if constexpr (SP == 1) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
-template <int U, int LP = 0, int SP = 0>
+template <int U>
 __device__ __forceinline__ void pipelined_copy16(g_cu4 *__restrict__ s4, g_u4 *__restrict__ t4, int64_t n4)
 {
     int64_t i = threadIdx.x;
@@ -201,33 +135,21 @@ __device__ __forceinline__ void pipelined_copy16(g_cu4 *__restrict__ s4, g_u4 *_
     if (i + (U - 1) * (int64_t)kThreads < n4) {
         u32x4 cur[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = ld16<LP>(s4 + i + u * kThreads);
+        for (int u = 0; u < U; ++u) cur[u] = s4[i + u * kThreads];
         for (; i + step + (U - 1) * (int64_t)kThreads < n4; i += step) {
             u32x4 nxt[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) nxt[u] = ld16<LP>(s4 + i + step + u * kThreads);
+            for (int u = 0; u < U; ++u) nxt[u] = s4[i + step + u * kThreads];
 #pragma unroll
-            for (int u = 0; u < U; ++u) st16g<SP>(t4 + i + u * kThreads, cur[u]);
+            for (int u = 0; u < U; ++u) t4[i + u * kThreads] = cur[u];
 #pragma unroll
             for (int u = 0; u < U; ++u) cur[u] = nxt[u];
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) st16g<SP>(t4 + i + u * kThreads, cur[u]);
+        for (int u = 0; u < U; ++u) t4[i + u * kThreads] = cur[u];
         i += step;
     }
-    for (; i < n4; i += kThreads) st16g<SP>(t4 + i, ld16<LP>(s4 + i));
-}
-
-template <int U, int LP = 0, int SP = 0>
-__global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restrict__ pieces)
-{
-    const DCopy c = pieces[blockIdx.x];
-    const int64_t n = c.len;
-    if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)n) & 15) == 0) {
-        pipelined_copy16<U, LP, SP>((g_cu4 *)c.src, (g_u4 *)c.dst, n >> 4);
-    } else {
-        for (int64_t i = threadIdx.x; i < n; i += kThreads) c.dst[i] = c.src[i];
-    }
+    for (; i < n4; i += kThreads) t4[i] = s4[i];
 }
 
 // Raw buffer access (gfx9 buffer resource, stride 0, num_records = bytes): a load
@@ -237,9 +159,10 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restric
 // count, and puts vmcnt(0) before EVERY store (each store then waits for the
 // previous one to be acknowledged).
 typedef __amdgpu_buffer_rsrc_t brsrc;
-// s_waitcnt immediate (gfx9 encoding): vmcnt(0), expcnt(7) and lgkmcnt(15) = no wait on those
-constexpr int kVmcnt0 = 0x0F70;
 constexpr int kRsrcWord3 = 0x00020000;     // gfx9 (gfx950) raw buffer, as composable_kernel
+// store cache-policy bits (the `aux` operand): 0 plain, 2 nt, 16 sc1 (write-through:
+// the line leaves the XCD's L2 with the store, so nothing is left dirty at kernel end)
+constexpr int kAuxPlain = 0, kAuxNT = 2, kAuxSC1 = 16;
 
 __device__ __forceinline__ brsrc make_rsrc(const void *p, int64_t bytes)
 {
@@ -251,14 +174,155 @@ __device__ __forceinline__ u32x4 bload16(brsrc r, int off)
     return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 
+template <int AUX = kAuxPlain>
 __device__ __forceinline__ void bstore16(brsrc r, int off, u32x4 v)
 {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
 }
 
-// One workgroup moves up to B*4 KiB (len, 16-B aligned) in one burst: every lane
-// issues its B 16-B loads, then its B stores -- B*4 KiB in flight per workgroup, so
-// a few hundred resident workgroups keep enough bytes in flight to stream HBM.
+// Pipelined piece copy through buffer resources (n: bytes, a multiple of 16,
+// < 2^31): every lane keeps U 16-B loads of the next block in flight while it
+// stores the current block.  The trip count is wave-uniform; out-of-range
+// lanes of the last block load 0 and their stores are dropped by the range check.
+template <int U, int AUX>
+__device__ __forceinline__ void pipelined_copy16_b(const uint8_t *src, uint8_t *dst, int n)
+{
+    const brsrc rs = make_rsrc(src, n), rd = make_rsrc(dst, n);
+    constexpr int blk = U * kThreads * 16;
+    const int lane = (int)threadIdx.x * 16;
+    u32x4 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = bload16(rs, lane + u * kThreads * 16);
+    for (int base = 0; base < n; base += blk) {
+        u32x4 nxt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) nxt[u] = bload16(rs, base + blk + lane + u * kThreads * 16);
+#pragma unroll
+        for (int u = 0; u < U; ++u) bstore16<AUX>(rd, base + lane + u * kThreads * 16, cur[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+    }
+}
+
+// LDS-staged realignment for a piece whose source and destination disagree mod
+// 16 (any -d that is not a multiple of 16: segment offsets k*d land on every
+// phase).  The destination gets whole aligned 16-B stores: the head (< 16 B) and
+// tail (< 16 B) go byte by byte, the body in 4 KiB tiles.  Per tile every lane
+// loads one ALIGNED 16-B chunk of the source window into LDS (257 chunks cover a
+// 4 KiB window at any phase), then reads back five dwords at its own 16-B
+// position shifted by the phase and funnel-shifts them (v_alignbyte) into one
+// aligned 16-B store.  Each source byte is read from HBM once; the LDS ring has
+// two tiles, so one barrier per tile orders both the fill and the reuse.
+constexpr int kTile = kThreads * 16;
+constexpr int kTileWords = (kTile + 16) / 4;     // 257 chunks of 16 B
+
+__device__ __forceinline__ void bytes_copy(const uint8_t *s, uint8_t *t, int64_t n)
+{
+    for (int64_t i = threadIdx.x; i < n; i += kThreads) t[i] = s[i];
+}
+
+__device__ void realign_copy(const uint8_t *s, uint8_t *t, int64_t n, uint32_t (*lds)[kTileWords])
+{
+    const int64_t head = (int64_t)((16 - ((uintptr_t)t & 15)) & 15);
+    if (n < head + 16) {
+        bytes_copy(s, t, n);
+        return;
+    }
+    const int64_t body = (n - head) & ~(int64_t)15;
+    bytes_copy(s, t, head);
+    bytes_copy(s + head + body, t + head + body, n - head - body);
+    const uint8_t *sb = s + head;                    // body source (any phase)
+    uint8_t *tb = t + head;                          // body destination (16-B aligned)
+    const int phase = (int)((uintptr_t)sb & 15);
+    const uint8_t *sa = sb - phase;                  // aligned source window start
+    // whole 16-B chunks up to the one holding the body's last byte (inside the
+    // allocation: it is 16-B aligned); chunks past that read 0
+    const brsrc rs = make_rsrc(sa, (phase + body + 15) & ~(int64_t)15);
+    const brsrc rd = make_rsrc(tb, body);
+    const int lane = (int)threadIdx.x;
+    const int w0 = 4 * lane + (phase >> 2), sh = phase & 3;
+    const int ntiles = (int)((body + kTile - 1) / kTile);
+    u32x4 a = bload16(rs, lane * 16), b = bload16(rs, kTile);   // b: chunk 256 (lane 0 keeps it)
+    for (int k = 0; k < ntiles; ++k) {
+        uint32_t *L = lds[k & 1];
+        *reinterpret_cast<u32x4 *>(L + 4 * lane) = a;
+        if (lane == 0) *reinterpret_cast<u32x4 *>(L + 4 * kThreads) = b;
+        if (k + 1 < ntiles) {                         // next tile's loads fly while this one drains
+            a = bload16(rs, (k + 1) * kTile + lane * 16);
+            b = bload16(rs, (k + 2) * kTile);
+        }
+        __syncthreads();
+        const uint32_t x0 = L[w0], x1 = L[w0 + 1], x2 = L[w0 + 2], x3 = L[w0 + 3], x4 = L[w0 + 4];
+        u32x4 v;
+        v.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
+        v.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
+        v.z = __builtin_amdgcn_alignbyte(x3, x2, sh);
+        v.w = __builtin_amdgcn_alignbyte(x4, x3, sh);
+        bstore16(rd, k * kTile + lane * 16, v);
+    }
+}
+
+// One workgroup per DCopy piece (<= the context's chunk bytes).  Variants:
+//   copy_kernel_g<U>       global loads/stores, U-deep software pipeline (round-1 default)
+//   copy_kernel_b<U, AUX>  the same through buffer resources, store policy AUX
+// Pieces whose pointers or length are not 16-B aligned take realign_copy.
+template <int U>
+__global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restrict__ pieces)
+{
+    __shared__ uint32_t lds[2][kTileWords];
+    const DCopy c = pieces[blockIdx.x];
+    if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
+        pipelined_copy16<U>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
+    else
+        realign_copy(c.src, c.dst, c.len, lds);
+}
+
+template <int U, int AUX>
+__global__ __launch_bounds__(kThreads) void copy_kernel_b(const DCopy *__restrict__ pieces)
+{
+    __shared__ uint32_t lds[2][kTileWords];
+    const DCopy c = pieces[blockIdx.x];
+    if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
+        pipelined_copy16_b<U, AUX>(c.src, c.dst, (int)c.len);
+    else
+        realign_copy(c.src, c.dst, c.len, lds);
+}
+
+// ---------------------------------------------------------------- step engine
+// A GPU-local plan of many small steps (sync / pairwise / throttled schedules
+// at small -d) is bound by the per-step kernel boundary + timing event, not by
+// HBM.  The engine runs the whole plan in ONE launch of W co-resident
+// workgroups: step s = units [step_begin[s], step_begin[s+1]) strided over the
+// workgroups, then a grid barrier whose last arriver stamps the step's
+// completion time (wall clock).
+//
+// What the barrier after step s must order is decided per step by the host
+// (xg_engine_hazards, include/xg_sched.h), flag[s]:
+//   0  nothing: step s+1 neither reads bytes written since the last ordering
+//      point nor rewrites them with different bytes.  A workgroup arrives as
+//      soon as its stores of step s are ISSUED (they may still land while step
+//      s+1 runs) and loads its first unit of step s+1 while the barrier is
+//      pending.  The stamp is then the step's issue time, not its delivery.
+//   1  timing: every wave waits for its stores (vmcnt 0) before arriving, so
+//      the stamp is a delivered time (the last step: it anchors every step time).
+//   2  hazard (step s+1 reads, or rewrites with other bytes, what was written
+//      since the last such point): stores drained, then the agent-scope
+//      release/acquire pair of cdna_hip_programming.md Guideline 16 around the
+//      barrier (release fence by one lane before arriving, acquire fence after
+//      the wait, before any load of step s+1), and no early load.
+// State: a cumulative ticket counter (never reset between launches: each launch
+// gets the tickets taken before it as `base`; the host re-zeroes it only after a
+// timeout) and a timeout word.  Spins are bounded: a timed-out workgroup sets
+// the word and leaves, so a broken residency assumption ends the launch
+// instead of hanging; the host checks the word after the launch (xg_plan_check).
+struct EngineState {
+    unsigned count;     // arrival tickets, cumulative over every launch of the plan
+    unsigned tmo;       // != 0: some workgroup gave up waiting
+    unsigned pad[2];
+};
+
+typedef __attribute__((address_space(1))) unsigned g_u32;
+
 template <int B>
 __device__ __forceinline__ void burst_load16(const uint8_t *src, int64_t len, u32x4 *v)
 {
@@ -275,55 +339,6 @@ __device__ __forceinline__ void burst_store16(uint8_t *dst, int64_t len, const u
     for (int k = 0; k < B; ++k) bstore16(r, ((int)threadIdx.x + k * kThreads) * 16, v[k]);
 }
 
-template <int B>
-__device__ __forceinline__ void burst_copy16(const uint8_t *src, uint8_t *dst, int64_t len)
-{
-    u32x4 v[B];
-    burst_load16<B>(src, len, v);
-    burst_store16<B>(dst, len, v);
-}
-
-// Piece copy in bursts (copy variant 12): one workgroup per DCopy piece, B*4 KiB per
-// burst, every load of a burst issued before its first store.
-template <int B>
-__global__ __launch_bounds__(kThreads) void copy_kernel_b(const DCopy *__restrict__ pieces)
-{
-    const DCopy c = pieces[blockIdx.x];
-    if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0) {
-        constexpr int64_t step = (int64_t)B * kThreads * 16;
-        for (int64_t o = 0; o < c.len; o += step)
-            burst_copy16<B>(c.src + o, c.dst + o, c.len - o < step ? c.len - o : step);
-    } else {
-        for (int64_t i = threadIdx.x; i < c.len; i += kThreads) c.dst[i] = c.src[i];
-    }
-}
-
-// ---------------------------------------------------------------- step engine
-// A GPU-local plan of many small steps (sync / pairwise / throttled schedules
-// at small -d) is bound by the per-step kernel boundary + timing event, not by
-// HBM.  The engine runs the whole plan in ONE launch of W co-resident
-// workgroups: step s = pieces [step_begin[s], step_begin[s+1]) strided over the
-// workgroups, then a grid barrier whose last arriver stamps the step's
-// completion time (wall clock).  No workgroup reads bytes another writes in
-// this launch (every piece reads SEND and writes RECV), so the barrier orders
-// and times steps but publishes no data, and the kernel end makes the stores
-// visible.  A workgroup arrives as soon as its stores of step s are ISSUED
-// (they may still land while step s+1 runs: -7..12 % per run of the
-// sync/pairwise chains, profiles/r01_engine_drain_ab.txt), except at steps the
-// host flags (engine_drains): there it waits for them first, so a step that
-// rewrites or reads bytes of an earlier step sees them complete.  The last step
-// always drains, so its stamp -- the anchor of every step time -- is a delivered time.
-// State (cumulative ticket counter + timeout word) is zeroed by a memset before
-// every launch; spins are bounded, and a timed-out workgroup sets *tmo and
-// leaves, so a broken residency assumption ends the launch instead of hanging.
-struct EngineState {
-    unsigned count;     // arrival tickets, cumulative over every launch of the plan
-    unsigned tmo;       // != 0: some workgroup gave up waiting
-    unsigned pad[2];
-};
-
-typedef __attribute__((address_space(1))) unsigned g_u32;
-
 // B: 16-B loads per lane per unit -> units of B * 4 KiB (the host cuts the step's
 // transfers to that size and picks B so that a step has enough units to spread).
 template <int B>
@@ -332,9 +347,7 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
                                                                EngineState *st, unsigned long long *stamps,
                                                                unsigned base)
 {
-    // base: tickets taken by this plan's earlier launches (count is never reset
-    // between launches, so no memset precedes a launch); compare by difference,
-    // which is wrap-safe
+    // compare tickets by difference, which is wrap-safe
     const unsigned W = gridDim.x;
     g_u32 *count = (g_u32 *)&st->count;
     g_u32 *tmo = (g_u32 *)&st->tmo;
@@ -345,7 +358,7 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
     // pending (into v[]) and stored once it opens: the load latency of each step
     // (HBM + address translation of fresh pages) overlaps the barrier.  pf is
     // workgroup-uniform.
-    const int *drain = step_begin + nsteps + 1;     // per-step flags (host: engine_drains)
+    const int *flag = step_begin + nsteps + 1;     // per-step flags (host: xg_engine_hazards)
     bool pf = false;
     DCopy nc = {nullptr, nullptr, 0};
     u32x4 v[B];
@@ -359,21 +372,29 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
         }
         for (; i < e; i += (int)W) {
             const DCopy c = pieces[i];       // <= B * 4 KiB
-            if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
-                burst_copy16<B>(c.src, c.dst, c.len);
-            else
-                for (int64_t k = threadIdx.x; k < c.len; k += kThreads) c.dst[k] = c.src[k];
+            if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0) {
+                u32x4 w[B];
+                burst_load16<B>(c.src, c.len, w);
+                burst_store16<B>(c.dst, c.len, w);
+            } else {
+                bytes_copy(c.src, c.dst, c.len);
+            }
         }
-        if (drain[s]) __builtin_amdgcn_s_waitcnt(kVmcnt0);  // this wave's stores so far performed
+        const int fl = flag[s];
+        if (fl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores performed
         __syncthreads();
         const unsigned target = base + (unsigned)(s + 1) * W;
         bool last = false;
         if (threadIdx.x == 0) {
+            if (fl == 2) {               // publish: write the XCD's L2 back before arriving
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             const unsigned t = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
             last = t == target;
             if (last) stamps[s] = (unsigned long long)wall_clock64();
         }
-        if (s + 1 < nsteps) {              // no step reads what another writes: safe to load early
+        if (s + 1 < nsteps && fl != 2) {   // step s+1 reads nothing written since the last hazard point
             const int j = step_begin[s + 1] + (int)blockIdx.x;
             if (j < step_begin[s + 2]) {
                 nc = pieces[j];
@@ -392,74 +413,36 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
                 }
             }
         }
+        if (fl == 2 && threadIdx.x == 0) {   // acquire: drop this CU's stale L1 lines
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __syncthreads();
         if (give_up) return;
     }
 }
 
-// ---------------------------------------------------------------- balanced byte-range copy
-// The launch's copies form one virtual byte space [0, total) (prefix[k] =
-// start of copy k, an exclusive scan of the lengths).  Workgroup b streams the
-// contiguous virtual range [b*per, (b+1)*per) -- equal bytes per workgroup, so
-// no tail wave; it crosses copy boundaries as it goes.  per is a multiple of
-// 16 and every copy length/pointer is 16-B aligned in this fast path (the
-// host falls back to copy_kernel otherwise).
-struct DSpan {
-    const uint8_t *src;
-    uint8_t *dst;
-    int64_t len;
-    int64_t start;      // exclusive prefix of len
-};
-
-template <int U>
-__global__ __launch_bounds__(kThreads) void span_copy_kernel(const DSpan *__restrict__ spans, int nspans,
-                                                             int64_t total, int64_t per)
-{
-    int64_t pos = (int64_t)blockIdx.x * per;
-    const int64_t end = pos + per < total ? pos + per : total;
-    if (pos >= end) return;
-    // first span containing pos (binary search, wave-uniform)
-    int lo = 0, hi = nspans - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (spans[mid].start <= pos) lo = mid; else hi = mid - 1;
-    }
-    int k = lo;
-    while (pos < end) {
-        const DSpan sp = spans[k];
-        const int64_t off = pos - sp.start;
-        const int64_t stop = (sp.start + sp.len < end ? sp.start + sp.len : end) - sp.start;
-        const uint4 *__restrict__ s4 = reinterpret_cast<const uint4 *>(sp.src + off);
-        uint4 *__restrict__ t4 = reinterpret_cast<uint4 *>(sp.dst + off);
-        const int64_t n4 = (stop - off) >> 4;
-        int64_t i = threadIdx.x;
-        for (; i + (int64_t)(U - 1) * kThreads < n4; i += (int64_t)U * kThreads) {
-            uint4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = s4[i + u * kThreads];
-#pragma unroll
-            for (int u = 0; u < U; ++u) t4[i + u * kThreads] = v[u];
-        }
-        for (; i < n4; i += kThreads) t4[i] = s4[i];
-        pos = sp.start + stop;
-        ++k;
-    }
-}
-
-// exclusive prefix scan of span lengths, one workgroup (wave64 shuffles +
-// LDS across the 4 waves), carried across 256-span tiles -- the device
-// replacement of the displacement loops of *_alltoall_translate (:233-302)
-__global__ __launch_bounds__(kThreads) void span_scan_kernel(DSpan *spans, int n, int64_t *total)
+// ---------------------------------------------------------------- displacement scan
+// The device replacement of *_alltoall_translate's displacement loops
+// (mpi_test.c:233-302): staging displacements of the packed per-peer segments of
+// one step = exclusive prefix sum of their lengths.  One workgroup per group
+// (a step's pack list or unpack list, groups[g] .. groups[g+1]): wave64 inclusive
+// scan with shuffles, wave totals through LDS, a carry across 256-entry tiles.  disp[i] = base + sum of len[j] for j < i inside the group.
+__global__ __launch_bounds__(kThreads) void displ_scan_kernel(const int64_t *__restrict__ len,
+                                                              const int *__restrict__ groups,
+                                                              const int64_t *__restrict__ group_base,
+                                                              int64_t *__restrict__ disp)
 {
     __shared__ int64_t wsum[kThreads / 64];
     __shared__ int64_t carry;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) carry = 0;
+    const int b = groups[blockIdx.x], e = groups[blockIdx.x + 1];
+    if (threadIdx.x == 0) carry = group_base[blockIdx.x];
     __syncthreads();
-    for (int base = 0; base < n; base += kThreads) {
-        const int i = base + threadIdx.x;
-        const int64_t v = i < n ? spans[i].len : 0;
-        int64_t x = v;                                 // inclusive scan inside the wave
+    for (int t = b; t < e; t += kThreads) {
+        const int i = t + (int)threadIdx.x;
+        const int64_t x0 = i < e ? len[i] : 0;
+        int64_t x = x0;                                // inclusive scan inside the wave
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int64_t y = __shfl_up(x, o, 64);
@@ -469,37 +452,33 @@ __global__ __launch_bounds__(kThreads) void span_scan_kernel(DSpan *spans, int n
         __syncthreads();
         int64_t before = carry;
         for (int w = 0; w < wave; ++w) before += wsum[w];
-        if (i < n) spans[i].start = before + x - v;
+        if (i < e) disp[i] = before + x - x0;
         __syncthreads();
         if (threadIdx.x == kThreads - 1) carry = before + x;
         __syncthreads();
     }
-    if (threadIdx.x == 0) *total = carry;
 }
 
-// ---------------------------------------------------------------- microbenchmarks
-__global__ __launch_bounds__(kThreads) void read_only_kernel(g_cu4 *__restrict__ s, int64_t n4, unsigned *sink)
-{
-    uint32_t x = 0;
-    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads) {
-        const u32x4 v = s[i];
-        x ^= v.x ^ v.y ^ v.z ^ v.w;
-    }
-    if (x == 0x9e3779b9u) atomicAdd(sink, 1u);
-}
+// Piece table fix-up after the scan: piece k of a packed copy c moves
+// [o, o + len) of it; its staging side (dst of a pack, src of an unpack) is
+// staging base + disp[c] + o.
+struct DFix {
+    int piece;          // index into the plan's piece table
+    int copy;           // index into disp[]
+    int64_t off;        // byte offset of the piece inside its copy
+    int side;           // 0: patch dst (pack), 1: patch src (unpack)
+    int pad;
+};
 
-__global__ __launch_bounds__(kThreads) void write_only_kernel(g_u4 *__restrict__ t, int64_t n4)
+__global__ __launch_bounds__(kThreads) void displ_apply_kernel(DCopy *__restrict__ pieces, const DFix *__restrict__ fix,
+                                                               int nfix, const int64_t *__restrict__ disp,
+                                                               uint8_t *stage_send, uint8_t *stage_recv)
 {
-    const u32x4 v = {1u, 2u, 3u, 4u};
-    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads)
-        t[i] = v;
-}
-
-__global__ __launch_bounds__(kThreads) void gridstride_copy_kernel(const uint4 *__restrict__ s, uint4 *__restrict__ t,
-                                                                   int64_t n4)
-{
-    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads)
-        t[i] = s[i];
+    const int k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= nfix) return;
+    const DFix f = fix[k];
+    if (f.side == 0) pieces[f.piece].dst = stage_send + disp[f.copy] + f.off;
+    else pieces[f.piece].src = stage_recv + disp[f.copy] + f.off;
 }
 
 // ---------------------------------------------------------------- verify

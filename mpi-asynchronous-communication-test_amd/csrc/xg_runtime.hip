@@ -57,12 +57,15 @@ struct xg_ctx {
     int engine_wmax;           // at most this many (co-resident) engine workgroups
     int engine_drain;          // 1: always drain before each barrier arrival (XG_ENGINE_DRAIN=1)
     double wall_hz;            // wall_clock64() rate
-    int variant;            // copy kernel variant
-    // kernel timing session (xg_ktime_begin/end)
-    bool kt_on;
+    int variant;            // copy kernel variant (launch_copy)
+    int engine_occ;            // co-resident step-engine workgroups the device admits (plan load caps W)
+    // kernel timing session (xg_ktime_begin/end): 1 = an event pair around every
+    // copy launch, 2 = one pair around the whole session on the main stream
+    int kt_mode;
     int nk;
-    std::vector<hipEvent_t> kev;   // start/end pairs per copy launch
-    std::vector<int64_t> kbytes;   // algorithmic bytes (read + write) per launch
+    std::vector<hipEvent_t> kev;   // start/end pairs per copy launch (mode 1), or the region pair
+    std::vector<int64_t> kbytes;   // algorithmic bytes (read + write) per launch (mode 1)
+    int64_t kt_bytes;              // their sum (both modes)
 };
 
 struct xg_regions {
@@ -80,6 +83,17 @@ struct StepR {
     bool split;
 };
 
+// A run of >= 2 consecutive GPU-local steps (no RCCL op, no in-loop barrier, no
+// TAM stage copy, no unpack, each <= engine_max_step bytes) executed by ONE
+// step_engine_kernel launch; every other step is its own launches.
+struct EngSeg {
+    int s0, s1;                    // steps [s0, s1)
+    int w, b;                      // workgroups; 16-B loads per lane per unit (1, 4, 16)
+    int sb_off;                    // its block in d_sb: (n + 1) unit offsets, then n flags
+    int nhaz;                      // hazard points (xg_engine_hazards flag 2)
+    int64_t bytes;                 // bytes copied per run
+};
+
 struct xg_plan {
     xg_ctx *ctx;
     xg_regions *reg;
@@ -92,16 +106,18 @@ struct xg_plan {
     std::vector<hipEvent_t> fork, join;   // per split step: main -> side, side -> main
     hipEvent_t ev0;
     int variant;
-    // step engine (one persistent launch for the whole plan), or engine_w == 0
-    int engine_w;
-    int engine_b;                  // 16-B loads per lane per unit (1, 4, 16)
-    int *d_step_begin;             // nsteps + 1 unit offsets, then nsteps drain flags
-    xgk::DCopy *d_epieces;         // the engine's work units, step-major
-    int engine_ndrain;             // steps whose barrier arrival waits for the stores (engine_drains)
+    // step engine segments
+    std::vector<int> seg_of;       // per step: index into segs, or -1
+    std::vector<EngSeg> segs;
+    int *d_sb;
+    xgk::DCopy *d_epieces;         // every segment's work units, step-major
     xgk::EngineState *d_engine;    // state (16 B, zeroed at load) followed by nsteps stamps
     unsigned engine_base;          // barrier tickets taken by earlier launches (wraps)
     bool engine_reset;             // zero the state before the next launch
-    int64_t engine_bytes;          // bytes copied per run
+    // staging displacements of the packed segments, computed on the device at load
+    int64_t *d_disp;
+    int ndisp;
+    int nlaunch;                   // kernel launches per run (copies + engine), RCCL's aside
 };
 
 extern "C" double xg_now(void)
@@ -171,7 +187,7 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     HIPCHK(hipSetDevice(device));
     xg_ctx *c = new xg_ctx();
     c->rank = rank; c->nranks = nranks; c->device = device; c->comm = nullptr; c->virt = false;
-    c->chunk = 32768; c->variant = 5; c->kt_on = false; c->nk = 0;   // measured best: profiles/r01_copy_ab.txt
+    c->chunk = 32768; c->variant = 0; c->kt_mode = 0; c->nk = 0; c->kt_bytes = 0;   // profiles/r01_copy_ab.txt
     const char *env = getenv("XG_COPY_CHUNK");
     if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
     env = getenv("XG_COPY_VARIANT");
@@ -179,9 +195,20 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->engine_max_step = 16 << 20;    // crossover vs one launch per step: profiles/r01_engine_sweep.txt
     env = getenv("XG_ENGINE_MAX_STEP");      // 0: never use the step engine
     if (env) c->engine_max_step = atol(env);
-    env = getenv("XG_ENGINE_WG");
-    c->engine_wmax = env && atoi(env) > 0 ? atoi(env) : 256;    // one per CU
-    if (c->engine_wmax > 1024) c->engine_wmax = 1024;
+    {
+        // the engine's grid barrier needs every workgroup resident at once: at most one
+        // per CU by design (XG_ENGINE_WG lowers it), never more than the device admits
+        // (a partitioned device has fewer CUs; several ranks per GPU share them)
+        int cus = 0, per_cu = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, xgk::step_engine_kernel<16>, xgk::kThreads, 0));
+        c->engine_occ = cus * (per_cu < 1 ? 1 : per_cu);
+        env = getenv("XG_ENGINE_WG");
+        c->engine_wmax = env && atoi(env) > 0 ? atoi(env) : cus;
+        if (c->engine_wmax > cus) c->engine_wmax = cus;
+        if (c->engine_wmax > c->engine_occ) c->engine_wmax = c->engine_occ;
+        if (c->engine_wmax < 1) c->engine_wmax = 1;
+    }
     env = getenv("XG_ENGINE_DRAIN");         // "1": drain every step even without a hazard
     c->engine_drain = env && !strcmp(env, "1");
     {
@@ -348,6 +375,14 @@ extern "C" int xg_regions_free(xg_regions *r)
 
 extern "C" void *xg_regions_ptr(xg_regions *r, int buf) { return buf >= 0 && buf < XG_NBUF ? r->ptr[buf] : nullptr; }
 
+extern "C" int xg_regions_write(xg_regions *r, int buf, int64_t off, const void *host, int64_t len)
+{
+    if (buf < 0 || buf >= XG_NBUF || off < 0 || len < 0 || off + len > r->bytes[buf]) return XG_EARG;
+    HIPCHK(hipMemcpyAsync(r->ptr[buf] + off, host, (size_t)len, hipMemcpyHostToDevice, r->ctx->stream));
+    HIPCHK(hipStreamSynchronize(r->ctx->stream));
+    return XG_OK;
+}
+
 extern "C" int xg_regions_read(xg_regions *r, int buf, int64_t off, void *host, int64_t len)
 {
     if (buf < 0 || buf >= XG_NBUF || off < 0 || len < 0 || off + len > r->bytes[buf]) return XG_EARG;
@@ -428,45 +463,160 @@ extern "C" int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_
 }
 
 // ------------------------------------------------------------------ plans
-// Per-step drain flags of the step engine: flag[t] = 1 makes every workgroup wait
-// for its stores (vmcnt 0) before arriving at step t's barrier, which completes
-// every store issued up to step t.  Step t drains when step t+1 writes or reads
-// bytes that a step since the previous drain wrote (the same receive slots
-// rewritten by the next -k repetition, typically: one drain per repetition);
-// the last step always drains (its stamp anchors every step time).  force: all.
-static std::vector<int> engine_drains(const std::vector<std::vector<xgk::DCopy>> &xfer, bool force)
+// Engine eligibility of one step: GPU-local copies only, small enough that the
+// per-launch boundary dominates (profiles/r01_engine_sweep.txt: crossover ~16 MiB).
+static bool engine_step(const xg_ctx *c, const StepR &st)
 {
-    const int n = (int)xfer.size();
-    std::vector<int> fl(n, force ? 1 : 0);
-    std::vector<std::pair<uintptr_t, uintptr_t>> pend;     // writes since the last drain, sorted
-    std::vector<uintptr_t> pmax;                             // prefix max of their ends
-    auto hits = [&](uintptr_t a, uintptr_t b) {              // does [a, b) meet a pending write?
-        const size_t i = std::lower_bound(pend.begin(), pend.end(), std::make_pair(b, (uintptr_t)0)) - pend.begin();
-        return i > 0 && pmax[i - 1] > a;
-    };
-    for (int u = 1; u < n && !force; ++u) {
-        const size_t m = pend.size();
-        for (const xgk::DCopy &x : xfer[u - 1])
-            if (x.len > 0) pend.push_back({(uintptr_t)x.dst, (uintptr_t)x.dst + (uintptr_t)x.len});
-        std::sort(pend.begin() + m, pend.end());
-        std::inplace_merge(pend.begin(), pend.begin() + m, pend.end());
-        pmax.resize(pend.size());
-        for (size_t i = 0; i < pend.size(); ++i) pmax[i] = std::max(i ? pmax[i - 1] : 0, pend[i].second);
-        bool hit = false;
-        for (const xgk::DCopy &x : xfer[u])
-            if (x.len > 0 && (hits((uintptr_t)x.dst, (uintptr_t)x.dst + (uintptr_t)x.len) ||
-                              hits((uintptr_t)x.src, (uintptr_t)x.src + (uintptr_t)x.len))) {
-                hit = true;
-                break;
-            }
-        if (hit) {
-            fl[u - 1] = 1;
-            pend.clear();
-        }
-    }
-    if (n) fl[n - 1] = 1;
-    return fl;
+    return !st.p2p_n && !st.sync_after && !st.stage_n && !st.post_n &&
+           st.local_bytes + st.pack_bytes <= c->engine_max_step;
 }
+
+// Build the engine segments of a loaded plan from its host piece table: every
+// maximal run of >= 2 eligible steps.  Units: the step's transfers (chunk-sized
+// pieces re-joined) cut to B * 4 KiB, one burst of B 16-B loads per lane per
+// workgroup visit.  B grows with the segment's largest step so a step spreads
+// over up to one workgroup per CU with bytes enough in flight
+// (profiles/r01_engine_sweep.txt: small units starve big steps, big units leave
+// small steps on a handful of workgroups).  Barrier flags: xg_engine_hazards.
+static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
+{
+    xg_ctx *c = p->ctx;
+    p->seg_of.assign(p->nsteps, -1);
+    if (c->engine_max_step <= 0) return XG_OK;
+    std::vector<xgk::DCopy> ep;
+    std::vector<int> sb;
+    for (int s = 0; s < p->nsteps;) {
+        int e = s;
+        while (e < p->nsteps && engine_step(c, p->steps[e])) ++e;
+        // steps where this GPU copies nothing cost nothing as their own "launches": trim
+        // them off both ends, and keep the run only if >= 2 steps copy something
+        const int run_end = e;
+        int busy = 0;
+        while (s < e && !p->steps[s].pre_n) ++s;
+        while (e > s && !p->steps[e - 1].pre_n) --e;
+        for (int t = s; t < e; ++t) busy += p->steps[t].pre_n > 0;
+        if (busy < 2) {
+            s = run_end > s ? run_end : s + 1;
+            continue;
+        }
+        EngSeg g;
+        g.s0 = s; g.s1 = e; g.bytes = 0;
+        int64_t maxstep = 0;
+        std::vector<std::vector<xgk::DCopy>> xfer(e - s);
+        for (int t = s; t < e; ++t) {
+            const StepR &st = p->steps[t];
+            for (int i = st.pre_b; i < st.pre_b + st.pre_n;) {
+                const uint8_t *src = pieces[i].src;
+                uint8_t *dst = pieces[i].dst;
+                int64_t len = pieces[i].len;
+                for (++i; i < st.pre_b + st.pre_n && pieces[i].src == src + len && pieces[i].dst == dst + len; ++i)
+                    len += pieces[i].len;
+                xfer[t - s].push_back({src, dst, len});
+            }
+            g.bytes += st.local_bytes + st.pack_bytes;
+            maxstep = std::max(maxstep, st.local_bytes + st.pack_bytes);
+        }
+        g.b = maxstep <= (1 << 20) ? 1 : (maxstep <= (4 << 20) ? 4 : 16);
+        const int64_t unit = (int64_t)g.b * xgk::kThreads * 16;
+        const int n = e - s, u0 = (int)ep.size();
+        std::vector<int> beg(n + 1);
+        std::vector<xg_span> spans;
+        int maxu = 0;
+        for (int t = 0; t < n; ++t) {
+            beg[t] = (int)ep.size() - u0;
+            for (const xgk::DCopy &x : xfer[t]) {
+                spans.push_back({(uint64_t)(uintptr_t)x.src, (uint64_t)(uintptr_t)x.dst, (uint64_t)x.len});
+                for (int64_t o = 0; o < x.len; o += unit)
+                    ep.push_back({x.src + o, x.dst + o, x.len - o < unit ? x.len - o : unit});
+            }
+            maxu = std::max(maxu, (int)ep.size() - u0 - beg[t]);
+        }
+        beg[n] = (int)ep.size() - u0;
+        // hazards over whole transfers: re-cut beg in transfer units for the host scan
+        std::vector<int> tb(n + 1, 0);
+        for (int t = 0; t < n; ++t) tb[t + 1] = tb[t] + (int)xfer[t].size();
+        std::vector<int> fl(n);
+        g.nhaz = xg_engine_hazards(spans.data(), tb.data(), n, c->engine_drain, fl.data());
+        g.w = std::max(1, std::min(maxu, c->engine_wmax));
+        g.sb_off = (int)sb.size();
+        for (int t = 0; t <= n; ++t) sb.push_back(u0 + beg[t]);
+        sb.insert(sb.end(), fl.begin(), fl.end());
+        for (int t = s; t < e; ++t) p->seg_of[t] = (int)p->segs.size();
+        p->segs.push_back(g);
+        s = e;
+    }
+    if (p->segs.empty()) return XG_OK;
+    HIPCHK(hipMalloc(&p->d_sb, sizeof(int) * sb.size()));
+    HIPCHK(hipMemcpy(p->d_sb, sb.data(), sizeof(int) * sb.size(), hipMemcpyHostToDevice));
+    if (!ep.empty()) {
+        HIPCHK(hipMalloc(&p->d_epieces, sizeof(xgk::DCopy) * ep.size()));
+        HIPCHK(hipMemcpy(p->d_epieces, ep.data(), sizeof(xgk::DCopy) * ep.size(), hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipMalloc(&p->d_engine, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps));
+    HIPCHK(hipMemset(p->d_engine, 0, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps));
+    return XG_OK;
+}
+
+// The staging displacements of the packed segments (alltoallw translate,
+// mpi_test.c:233-302) on the device: one scan group per step and direction,
+// then the pack pieces' destinations / unpack pieces' sources are patched.
+// The host's own layout (xg_devplan_build) is the cross-check: a mismatch
+// refuses the plan before any copy runs.
+struct DisplScan {
+    std::vector<int64_t> len, host;   // per packed copy (in group order): length, host displacement
+    std::vector<int> groups{0};
+    std::vector<xgk::DFix> fix;
+    void close_group()
+    {
+        if ((int)len.size() > groups.back()) groups.push_back((int)len.size());
+    }
+};
+
+static int run_displ_scan(xg_plan *p, DisplScan &ds)
+{
+    xg_ctx *c = p->ctx;
+    p->ndisp = (int)ds.len.size();
+    if (!p->ndisp) return XG_OK;
+    const int ng = (int)ds.groups.size() - 1;
+    int64_t *d_len, *d_base;
+    int *d_groups;
+    xgk::DFix *d_fix;
+    const std::vector<int64_t> base(ng, 0);    // every step's staging starts at 0 (xg_devplan_build)
+    HIPCHK(hipMalloc(&p->d_disp, sizeof(int64_t) * p->ndisp));
+    HIPCHK(hipMalloc(&d_len, sizeof(int64_t) * p->ndisp));
+    HIPCHK(hipMalloc(&d_base, sizeof(int64_t) * ng));
+    HIPCHK(hipMalloc(&d_groups, sizeof(int) * (ng + 1)));
+    HIPCHK(hipMalloc(&d_fix, sizeof(xgk::DFix) * ds.fix.size()));
+    HIPCHK(hipMemcpyAsync(d_len, ds.len.data(), sizeof(int64_t) * p->ndisp, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_base, base.data(), sizeof(int64_t) * ng, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_groups, ds.groups.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_fix, ds.fix.data(), sizeof(xgk::DFix) * ds.fix.size(), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(xgk::displ_scan_kernel, dim3(ng), dim3(xgk::kThreads), 0, c->stream, d_len, d_groups, d_base,
+                       p->d_disp);
+    HIPCHK(hipGetLastError());
+    std::vector<int64_t> got(p->ndisp);
+    HIPCHK(hipMemcpyAsync(got.data(), p->d_disp, sizeof(int64_t) * p->ndisp, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < p->ndisp; ++i)
+        if (got[i] != ds.host[i]) {
+            fprintf(stderr, "xg_plan_load: device displacement %d = %lld, host layout %lld\n", i, (long long)got[i],
+                    (long long)ds.host[i]);
+            return XG_EARG;
+        }
+    const int nfix = (int)ds.fix.size();
+    hipLaunchKernelGGL(xgk::displ_apply_kernel, dim3((nfix + xgk::kThreads - 1) / xgk::kThreads), dim3(xgk::kThreads),
+                       0, c->stream, p->d_pieces, d_fix, nfix, p->d_disp, p->reg->ptr[XG_BUF_STAGE_SEND],
+                       p->reg->ptr[XG_BUF_STAGE_RECV]);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipFree(d_len));
+    HIPCHK(hipFree(d_base));
+    HIPCHK(hipFree(d_groups));
+    HIPCHK(hipFree(d_fix));
+    return XG_OK;
+}
+
+extern "C" int xg_plan_free(xg_plan *p);
 
 extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_plan **out)
 {
@@ -485,22 +635,35 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     HIPCHK(hipSetDevice(c->device));
     xg_plan *p = new xg_plan();
     p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant;
+    p->d_pieces = nullptr; p->d_sb = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->d_disp = nullptr;
+    p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
     // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
     // pieces for small launches were measured no faster, and slower where they stop
     // dividing the segment size (profiles/r01_min_pieces_ab.txt)
     const int64_t chunk = c->chunk;
     std::vector<xgk::DCopy> pieces;
-    auto add = [&](const xg_copy &cp) -> bool {
+    DisplScan ds;
+    int rc;
+    // side: -1 plain copy; 0 pack (destination in STAGE_SEND, displacement from the
+    // device scan); 1 unpack (source in STAGE_RECV, likewise)
+    auto add = [&](const xg_copy &cp, int side) -> bool {
         if (cp.len <= 0) return true;
         if (cp.src_buf < 0 || cp.src_buf >= XG_NBUF || cp.dst_buf < 0 || cp.dst_buf >= XG_NBUF) return false;
         if (cp.src_off < 0 || cp.dst_off < 0 || cp.src_off + cp.len > r->bytes[cp.src_buf] ||
             cp.dst_off + cp.len > r->bytes[cp.dst_buf])
             return false;
+        const int ci = (int)ds.len.size();
+        if (side >= 0) {
+            ds.len.push_back(cp.len);
+            ds.host.push_back(side == 0 ? cp.dst_off : cp.src_off);
+        }
         for (int64_t o = 0; o < cp.len; o += chunk) {
             xgk::DCopy d;
-            d.src = r->ptr[cp.src_buf] + cp.src_off + o;
-            d.dst = r->ptr[cp.dst_buf] + cp.dst_off + o;
+            // staging side of a packed copy: displacement 0 until the device scan patches it
+            d.src = r->ptr[cp.src_buf] + (side == 1 ? 0 : cp.src_off) + o;
+            d.dst = r->ptr[cp.dst_buf] + (side == 0 ? 0 : cp.dst_off) + o;
             d.len = cp.len - o < chunk ? cp.len - o : chunk;
+            if (side >= 0) ds.fix.push_back({(int)pieces.size(), ci, o, side, 0});
             pieces.push_back(d);
         }
         return true;
@@ -512,26 +675,32 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         if (sp.stage_count < 0 || sp.stage_count > sp.pre_count) goto bad;
         st.stage_b = (int)pieces.size();
         for (int i = 0; i < sp.stage_count; ++i)
-            if (!add(dp->copies[sp.pre_begin + i])) goto bad;
+            if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
         st.stage_n = (int)pieces.size() - st.stage_b;
         st.stage_bytes = 0;
         for (int i = st.stage_b; i < st.stage_b + st.stage_n; ++i) st.stage_bytes += pieces[i].len;
         st.pre_b = (int)pieces.size();
         st.local_bytes = st.pack_bytes = 0;
+        st.local_n = 0;
         for (int i = sp.stage_count; i < sp.pre_count; ++i) {
             const xg_copy &cp = dp->copies[sp.pre_begin + i];
             const bool pack = cp.dst_buf == XG_BUF_STAGE_SEND;   // the plan lists local copies, then packs
             const int before = (int)pieces.size();
             if (!pack && st.pack_bytes) goto bad;
-            if (!add(cp)) goto bad;
+            if (!add(cp, pack ? 0 : -1)) goto bad;
             for (int k = before; k < (int)pieces.size(); ++k) (pack ? st.pack_bytes : st.local_bytes) += pieces[k].len;
             if (!pack) st.local_n = (int)pieces.size() - st.pre_b;
         }
+        ds.close_group();
         st.pre_n = (int)pieces.size() - st.pre_b;
         if (!st.local_bytes) st.local_n = 0;
         st.post_b = (int)pieces.size();
-        for (int i = 0; i < sp.post_count; ++i)
-            if (!add(dp->copies[sp.post_begin + i])) goto bad;
+        for (int i = 0; i < sp.post_count; ++i) {
+            const xg_copy &cp = dp->copies[sp.post_begin + i];
+            if (cp.src_buf != XG_BUF_STAGE_RECV) goto bad;       // post copies are unpacks
+            if (!add(cp, 1)) goto bad;
+        }
+        ds.close_group();
         st.post_n = (int)pieces.size() - st.post_b;
         st.post_bytes = 0;
         for (int i = st.post_b; i < st.post_b + st.post_n; ++i) st.post_bytes += pieces[i].len;
@@ -548,7 +717,6 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.split = st.p2p_n > 0 && st.local_n > 0;
     }
     p->npieces = (int)pieces.size();
-    p->d_pieces = nullptr;
     if (p->npieces) {
         HIPCHK(hipMalloc(&p->d_pieces, sizeof(xgk::DCopy) * pieces.size()));
         HIPCHK(hipMemcpy(p->d_pieces, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
@@ -563,70 +731,17 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             HIPCHK(hipEventCreateWithFlags(&p->join[s], hipEventDisableTiming));
         }
     HIPCHK(hipEventCreate(&p->ev0));
-    p->engine_w = 0; p->d_step_begin = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->engine_bytes = 0;
-    {
-        bool ok = !c->virt && c->engine_max_step > 0 && p->nsteps >= 2;
-        for (const StepR &st : p->steps)
-            ok = ok && !st.p2p_n && !st.sync_after && !st.stage_n && !st.post_n &&
-                 st.local_bytes + st.pack_bytes <= c->engine_max_step;
-        if (ok) {
-            // the engine's work units: the step's transfers (chunk-sized pieces re-joined) cut
-            // to B * 4 KiB, one burst of B 16-B loads per lane per workgroup visit.  B grows
-            // with the largest step so a step spreads over up to ~256 workgroups with bytes
-            // enough in flight (profiles/r01_engine_sweep.txt: small units starve big steps,
-            // big units leave small steps on a handful of workgroups).  One workgroup for a
-            // whole plan of tiny steps (workgroup barrier instead of the grid barrier) was
-            // measured 2x slower per step: profiles/r01_engine_wg_probe.txt, r01_engine_sweep.txt
-            int64_t maxstep = 0;
-            for (const StepR &st : p->steps)
-                if (st.local_bytes + st.pack_bytes > maxstep) maxstep = st.local_bytes + st.pack_bytes;
-            std::vector<std::vector<xgk::DCopy>> xfer(p->nsteps);
-            for (int s = 0; s < p->nsteps; ++s) {
-                const StepR &st = p->steps[s];
-                for (int i = st.pre_b; i < st.pre_b + st.pre_n;) {
-                    const uint8_t *src = pieces[i].src;
-                    uint8_t *dst = pieces[i].dst;
-                    int64_t len = pieces[i].len;
-                    for (++i; i < st.pre_b + st.pre_n && pieces[i].src == src + len && pieces[i].dst == dst + len; ++i)
-                        len += pieces[i].len;
-                    xfer[s].push_back({src, dst, len});
-                }
-                p->engine_bytes += st.local_bytes + st.pack_bytes;
-            }
-            auto cut = [&](int64_t unit, std::vector<xgk::DCopy> &ep, std::vector<int> &sb) -> int {
-                int maxu = 0;
-                ep.clear();
-                sb.assign(p->nsteps + 1, 0);
-                for (int s = 0; s < p->nsteps; ++s) {
-                    sb[s] = (int)ep.size();
-                    for (const xgk::DCopy &x : xfer[s])
-                        for (int64_t o = 0; o < x.len; o += unit)
-                            ep.push_back({x.src + o, x.dst + o, x.len - o < unit ? x.len - o : unit});
-                    if ((int)ep.size() - sb[s] > maxu) maxu = (int)ep.size() - sb[s];
-                }
-                sb[p->nsteps] = (int)ep.size();
-                return maxu;
-            };
-            std::vector<xgk::DCopy> ep;
-            std::vector<int> sb;
-            p->engine_b = maxstep <= (1 << 20) ? 1 : (maxstep <= (4 << 20) ? 4 : 16);
-            const int maxu = cut((int64_t)p->engine_b * xgk::kThreads * 16, ep, sb);
-            p->engine_w = maxu < 1 ? 1 : (maxu > c->engine_wmax ? c->engine_wmax : maxu);
-            const std::vector<int> fl = engine_drains(xfer, c->engine_drain);  // after the step begins
-            p->engine_ndrain = 0;
-            for (int f : fl) p->engine_ndrain += f;
-            sb.insert(sb.end(), fl.begin(), fl.end());
-            HIPCHK(hipMalloc(&p->d_step_begin, sizeof(int) * sb.size()));
-            HIPCHK(hipMemcpy(p->d_step_begin, sb.data(), sizeof(int) * sb.size(), hipMemcpyHostToDevice));
-            if (!ep.empty()) {
-                HIPCHK(hipMalloc(&p->d_epieces, sizeof(xgk::DCopy) * ep.size()));
-                HIPCHK(hipMemcpy(p->d_epieces, ep.data(), sizeof(xgk::DCopy) * ep.size(), hipMemcpyHostToDevice));
-            }
-            HIPCHK(hipMalloc(&p->d_engine, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps));
-            HIPCHK(hipMemset(p->d_engine, 0, sizeof(xgk::EngineState)));
-            p->engine_base = 0;
-            p->engine_reset = false;
+    if ((rc = run_displ_scan(p, ds)) || (rc = build_segments(p, pieces))) {
+        xg_plan_free(p);
+        return rc;
+    }
+    for (int s = 0; s < p->nsteps; ++s) {
+        const StepR &st = p->steps[s];
+        if (p->seg_of[s] >= 0) {
+            p->nlaunch += p->segs[p->seg_of[s]].s0 == s;
+            continue;
         }
+        p->nlaunch += (st.stage_n > 0) + (st.split ? 1 + (st.pre_n > st.local_n) : st.pre_n > 0) + (st.post_n > 0);
     }
     *out = p;
     return XG_OK;
@@ -640,60 +755,88 @@ extern "C" int xg_plan_free(xg_plan *p)
 {
     if (!p) return XG_OK;
     HIPCHK(hipStreamSynchronize(p->ctx->stream));
-    if (p->d_pieces) HIPCHK(hipFree(p->d_pieces));
     HIPCHK(hipStreamSynchronize(p->ctx->side));
-    if (p->d_step_begin) HIPCHK(hipFree(p->d_step_begin));
+    if (p->d_pieces) HIPCHK(hipFree(p->d_pieces));
+    if (p->d_sb) HIPCHK(hipFree(p->d_sb));
     if (p->d_epieces) HIPCHK(hipFree(p->d_epieces));
     if (p->d_engine) HIPCHK(hipFree(p->d_engine));
+    if (p->d_disp) HIPCHK(hipFree(p->d_disp));
     for (auto &e : p->ev) HIPCHK(hipEventDestroy(e));
     for (auto &e : p->fork) if (e) HIPCHK(hipEventDestroy(e));
     for (auto &e : p->join) if (e) HIPCHK(hipEventDestroy(e));
-    HIPCHK(hipEventDestroy(p->ev0));
+    if (p->ev0) HIPCHK(hipEventDestroy(p->ev0));
     delete p;
     return XG_OK;
 }
 
 extern "C" int xg_plan_nsteps(const xg_plan *p) { return p->nsteps; }
-extern "C" int xg_plan_engine(const xg_plan *p) { return p->engine_w; }
+extern "C" int xg_plan_engine(const xg_plan *p) { return p->segs.empty() ? 0 : p->segs[0].w; }
+extern "C" int xg_plan_launches(const xg_plan *p) { return p->nlaunch; }
+
+extern "C" int xg_plan_engine_steps(const xg_plan *p, int *nseg, int *nhaz)
+{
+    int n = 0, h = 0;
+    for (const EngSeg &g : p->segs) {
+        n += g.s1 - g.s0;
+        h += g.nhaz;
+    }
+    if (nseg) *nseg = (int)p->segs.size();
+    if (nhaz) *nhaz = h;
+    return n;
+}
+
+extern "C" int xg_plan_displs(const xg_plan *p, int64_t *out, int n)
+{
+    if (!out) return p->ndisp;
+    if (n < p->ndisp) return XG_EARG;
+    if (p->ndisp) HIPCHK(hipMemcpy(out, p->d_disp, sizeof(int64_t) * p->ndisp, hipMemcpyDeviceToHost));
+    return XG_OK;
+}
 
 static int launch_copy(xg_plan *p, int b, int n, hipStream_t st)
 {
     const xgk::DCopy *pc = p->d_pieces + b;
     switch (p->variant) {
-    case 1: hipLaunchKernelGGL((xgk::copy_kernel<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 2: hipLaunchKernelGGL((xgk::copy_kernel<8, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 3: hipLaunchKernelGGL((xgk::copy_kernel<8, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 4: hipLaunchKernelGGL((xgk::copy_kernel<2, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 5: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 6: hipLaunchKernelGGL((xgk::copy_kernel_g<2>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 7: hipLaunchKernelGGL((xgk::copy_kernel_g<4, 1, 0>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 8: hipLaunchKernelGGL((xgk::copy_kernel_g<4, 1, 1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 9: hipLaunchKernelGGL((xgk::copy_kernel_g<4, 0, 1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 10: hipLaunchKernelGGL((xgk::copy_kernel_g<8>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 11: hipLaunchKernelGGL((xgk::copy_kernel_g<8, 1, 1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 12: hipLaunchKernelGGL((xgk::copy_kernel_b<8>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 13: hipLaunchKernelGGL((xgk::copy_kernel_b<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 0: hipLaunchKernelGGL((xgk::copy_kernel<4, false>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 1: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxPlain>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 2: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxSC1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 3: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 4: hipLaunchKernelGGL((xgk::copy_kernel_b<8, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 5: hipLaunchKernelGGL((xgk::copy_kernel_b<2, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     }
     HIPCHK(hipGetLastError());
     return XG_OK;
 }
 
-// one copy launch, bracketed by kernel-timing events when a session is on
-static int timed_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t stream)
+// kernel-timing session bookkeeping around one launch of `bytes` copied bytes
+static int kt_before(xg_ctx *c, hipStream_t stream, bool *kt)
 {
-    xg_ctx *c = p->ctx;
-    int rc;
-    const bool kt = c->kt_on && 2 * (size_t)c->nk + 1 < c->kev.size();
-    if (kt) HIPCHK(hipEventRecord(c->kev[2 * c->nk], stream));
-    if ((rc = launch_copy(p, b, n, stream))) return rc;
+    *kt = c->kt_mode == 1 && 2 * (size_t)c->nk + 1 < c->kev.size();
+    if (*kt) HIPCHK(hipEventRecord(c->kev[2 * c->nk], stream));
+    return XG_OK;
+}
+
+static int kt_after(xg_ctx *c, hipStream_t stream, bool kt, int64_t bytes)
+{
     if (kt) {
         HIPCHK(hipEventRecord(c->kev[2 * c->nk + 1], stream));
         c->kbytes[c->nk] = 2 * bytes;      // algorithmic HBM bytes: read + write
+    }
+    if (kt || c->kt_mode == 2) {
         c->nk++;
+        c->kt_bytes += 2 * bytes;
     }
     return XG_OK;
+}
+
+// one copy launch, bracketed by kernel-timing events when a per-launch session is on
+static int timed_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t stream)
+{
+    int rc;
+    bool kt;
+    if ((rc = kt_before(p->ctx, stream, &kt))) return rc;
+    if ((rc = launch_copy(p, b, n, stream))) return rc;
+    return kt_after(p->ctx, stream, kt, bytes);
 }
 
 // step part 1: stage copies, then local gather/scatter + packs.  A split step
@@ -756,60 +899,61 @@ static int enqueue_step(xg_plan *p, int s)
     return XG_OK;
 }
 
-// one launch of the step engine (state zeroed first); timed as one copy launch
-static int launch_engine(xg_plan *p)
+// one launch of the step engine over segment g
+static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream)
 {
     xg_ctx *c = p->ctx;
+    int rc;
     if (p->engine_reset) {
-        HIPCHK(hipMemsetAsync(p->d_engine, 0, sizeof(xgk::EngineState), c->stream));
+        HIPCHK(hipMemsetAsync(p->d_engine, 0, sizeof(xgk::EngineState), stream));
         p->engine_base = 0;
+        p->engine_reset = false;
     }
+    const int n = g.s1 - g.s0;
     const unsigned base = p->engine_base;
-    p->engine_base += (unsigned)p->nsteps * (unsigned)p->engine_w;
-    const bool kt = c->kt_on && 2 * (size_t)c->nk + 1 < c->kev.size();
-    if (kt) HIPCHK(hipEventRecord(c->kev[2 * c->nk], c->stream));
-    unsigned long long *stamps = reinterpret_cast<unsigned long long *>(p->d_engine + 1);
-    if (p->engine_b == 1)
-        hipLaunchKernelGGL(xgk::step_engine_kernel<1>, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream,
-                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps, base);
-    else if (p->engine_b == 4)
-        hipLaunchKernelGGL(xgk::step_engine_kernel<4>, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream,
-                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps, base);
+    p->engine_base += (unsigned)n * (unsigned)g.w;
+    bool kt;
+    if ((rc = kt_before(c, stream, &kt))) return rc;
+    unsigned long long *stamps = reinterpret_cast<unsigned long long *>(p->d_engine + 1) + g.s0;
+    const int *sb = p->d_sb + g.sb_off;
+    if (g.b == 1)
+        hipLaunchKernelGGL(xgk::step_engine_kernel<1>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb, n,
+                           p->d_engine, stamps, base);
+    else if (g.b == 4)
+        hipLaunchKernelGGL(xgk::step_engine_kernel<4>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb, n,
+                           p->d_engine, stamps, base);
     else
-        hipLaunchKernelGGL(xgk::step_engine_kernel<16>, dim3(p->engine_w), dim3(xgk::kThreads), 0, c->stream,
-                           p->d_epieces, p->d_step_begin, p->nsteps, p->d_engine, stamps, base);
+        hipLaunchKernelGGL(xgk::step_engine_kernel<16>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb,
+                           n, p->d_engine, stamps, base);
     HIPCHK(hipGetLastError());
-    if (kt) {
-        HIPCHK(hipEventRecord(c->kev[2 * c->nk + 1], c->stream));
-        c->kbytes[c->nk] = 2 * p->engine_bytes;
-        c->nk++;
+    return kt_after(c, stream, kt, g.bytes);
+}
+
+// after a synchronised run: did an engine workgroup give up at a grid barrier?
+// Then the tickets are inconsistent: zero the state before the next launch.
+extern "C" int xg_plan_check(xg_plan *p)
+{
+    if (p->segs.empty()) return XG_OK;
+    xgk::EngineState es;
+    HIPCHK(hipSetDevice(p->ctx->device));
+    HIPCHK(hipStreamSynchronize(p->ctx->stream));
+    HIPCHK(hipMemcpy(&es, p->d_engine, sizeof es, hipMemcpyDeviceToHost));
+    if (es.tmo) {
+        p->engine_reset = true;
+        fprintf(stderr, "xg: step engine: a workgroup timed out at a grid barrier (workgroups not co-resident?)\n");
+        return XG_EHIP;
     }
     return XG_OK;
 }
 
-// after a synchronised engine run: per-step completion times from the wall-clock
-// stamps, anchored at the stream events around the launch
-static int engine_times(xg_plan *p, double *step_done)
+// step s of this plan as enqueued on (stream, side): an engine segment is one
+// launch at its first step and nothing at the others
+static int enqueue_unit(xg_plan *p, int s)
 {
-    std::vector<unsigned long long> h(2 + (size_t)p->nsteps);
-    HIPCHK(hipMemcpy(h.data(), p->d_engine, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
-    const xgk::EngineState *es = reinterpret_cast<const xgk::EngineState *>(h.data());
-    if (es->tmo) {
-        p->engine_reset = true;        // the tickets are inconsistent now: zero before every launch
-        fprintf(stderr, "xg: step engine: a workgroup timed out at a grid barrier (workgroups not co-resident?)\n");
-        return XG_EHIP;
-    }
-    if (step_done) {
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[p->nsteps - 1]));
-        const unsigned long long *st = h.data() + 2;
-        const double total = ms * 1e-3, last = (double)st[p->nsteps - 1];
-        for (int s = 0; s < p->nsteps; ++s) {
-            const double t = total - (last - (double)st[s]) / p->ctx->wall_hz;
-            step_done[s] = t > 0 ? t : 0;
-        }
-    }
-    return XG_OK;
+    const int gi = p->seg_of[s];
+    if (gi < 0) return enqueue_step(p, s);
+    if (p->segs[gi].s0 != s) return XG_OK;
+    return launch_seg(p, p->segs[gi], p->ctx->stream);
 }
 
 extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
@@ -817,52 +961,62 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     xg_ctx *c = p->ctx;
     int rc;
     HIPCHK(hipSetDevice(c->device));
-    if (p->engine_w) {
-        const double t0 = xg_now();
-        HIPCHK(hipEventRecord(p->ev0, c->stream));
-        if ((rc = launch_engine(p))) return rc;
-        HIPCHK(hipEventRecord(p->ev[p->nsteps - 1], c->stream));
-        if (step_post) {               // one launch posts every step
-            step_post[0] = xg_now() - t0;
-            for (int s = 1; s < p->nsteps; ++s) step_post[s] = 0;
-        }
-        HIPCHK(hipStreamSynchronize(c->stream));
-        if (wall) *wall = xg_now() - t0;
-        return engine_times(p, step_done);
-    }
     const double t0 = xg_now();
     HIPCHK(hipEventRecord(p->ev0, c->stream));
-    for (int s = 0; s < p->nsteps; ++s) {
+    for (int s = 0; s < p->nsteps;) {
         const double tp = xg_now();
-        if ((rc = enqueue_step(p, s))) return rc;
-        HIPCHK(hipEventRecord(p->ev[s], c->stream));
-        if (step_post) step_post[s] = xg_now() - tp;
+        const int gi = p->seg_of[s];
+        const int e = gi >= 0 ? p->segs[gi].s1 : s + 1;     // one launch posts a whole segment
+        if ((rc = enqueue_unit(p, s))) return rc;
+        HIPCHK(hipEventRecord(p->ev[e - 1], c->stream));
+        if (step_post) {
+            step_post[s] = xg_now() - tp;
+            for (int t = s + 1; t < e; ++t) step_post[t] = 0;
+        }
+        s = e;
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     if (wall) *wall = xg_now() - t0;
-    if (step_done)
-        for (int s = 0; s < p->nsteps; ++s) {
-            float ms = 0;
-            HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[s]));
-            step_done[s] = ms * 1e-3;
+    if ((rc = xg_plan_check(p))) return rc;
+    if (!step_done) return XG_OK;
+    std::vector<unsigned long long> st;
+    if (!p->segs.empty()) {
+        st.resize(p->nsteps);
+        HIPCHK(hipMemcpy(st.data(), p->d_engine + 1, 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
+    }
+    for (int s = 0; s < p->nsteps;) {
+        const int gi = p->seg_of[s];
+        const int e = gi >= 0 ? p->segs[gi].s1 : s + 1;
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[e - 1]));
+        const double end = ms * 1e-3;
+        // inside a segment: the wall-clock stamps, anchored at the event after its launch
+        // (the last step of a segment is drained, so its stamp is a delivered time)
+        for (int t = s; t < e; ++t) {
+            const double x = end - (double)(st.empty() ? 0 : st[e - 1] - st[t]) / c->wall_hz;
+            step_done[t] = t == e - 1 ? end : (x > 0 ? x : 0);
         }
+        s = e;
+    }
     return XG_OK;
 }
 
 extern "C" int xg_plan_enqueue(xg_plan *p)
 {
     int rc;
-    if (p->engine_w) return launch_engine(p);
     for (int s = 0; s < p->nsteps; ++s)
-        if ((rc = enqueue_step(p, s))) return rc;
+        if ((rc = enqueue_unit(p, s))) return rc;
     return XG_OK;
 }
 
 // Every GPU of a virtual job (xg_init_virtual), step by step on plans[0]'s
-// stream: all pre copies, then each RCCL send/recv pair as one device copy
-// (sends of g to h matched in order with h's receives from g -- RCCL's
-// per-peer FIFO inside a group), then all post copies, then the step event.
-// step_done[s] = device seconds from the start to the end of step s.
+// stream: all pre copies (or a GPU's whole engine segment, at its first step:
+// its steps touch only that GPU's regions and hold none of its cross-GPU ops,
+// so running them together is what a real GPU does too), then each RCCL
+// send/recv pair as one device copy (sends of g to h matched in order with h's
+// receives from g -- RCCL's per-peer FIFO inside a group), then all post
+// copies, then the step event.  step_done[s] = device seconds from the start to
+// the end of step s.
 // rccl = true: the same pairs go through RCCL instead -- a 1-rank communicator
 // on the device (created once, held by plans[0]'s context), each step's pairs as
 // one ncclGroupStart/End of self ncclSend + ncclRecv (matched in issue order),
@@ -893,8 +1047,13 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
     HIPCHK(hipEventRecord(plans[0]->ev0, st));
     std::vector<std::vector<const xg_p2p *>> sends((size_t)n * n), recvs((size_t)n * n);
     for (int s = 0; s < nst; ++s) {
-        for (int g = 0; g < n; ++g)
-            if ((rc = enqueue_pre(plans[g], s, st, plans[g]->ctx->side))) return rc;
+        for (int g = 0; g < n; ++g) {
+            xg_plan *pg = plans[g];
+            const int gi = pg->seg_of[s];
+            if (gi < 0) rc = enqueue_pre(pg, s, st, pg->ctx->side);
+            else rc = pg->segs[gi].s0 == s ? launch_seg(pg, pg->segs[gi], st) : XG_OK;
+            if (rc) return rc;
+        }
         for (auto &v : sends) v.clear();
         for (auto &v : recvs) v.clear();
         for (int g = 0; g < n; ++g) {
@@ -937,12 +1096,14 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
             }
         if (grouped) NCCLCHK(ncclGroupEnd());
         for (int g = 0; g < n; ++g)
-            if ((rc = enqueue_post(plans[g], s, st))) return rc;
+            if (plans[g]->seg_of[s] < 0 && (rc = enqueue_post(plans[g], s, st))) return rc;
         if (rccl && plans[0]->steps[s].sync_after)
             NCCLCHK(ncclAllReduce(c0->d_red, c0->d_red, 1, ncclFloat64, ncclMax, c0->comm, st));
         HIPCHK(hipEventRecord(plans[0]->ev[s], st));
     }
     HIPCHK(hipStreamSynchronize(st));
+    for (int g = 0; g < n; ++g)
+        if ((rc = xg_plan_check(plans[g]))) return rc;
     if (step_done)
         for (int s = 0; s < nst; ++s) {
             float ms = 0;
@@ -962,112 +1123,58 @@ extern "C" int xg_vplans_run_rccl(xg_plan *const *plans, int n, double *step_don
     return vplans_run(plans, n, step_done, true);
 }
 
-extern "C" int xg_ktime_begin(xg_ctx *c, int max_launches)
+// mode 1: an event pair around every copy / engine launch (max_launches of them);
+// mode 2: one pair around the whole session on the main stream, launches counted
+extern "C" int xg_ktime_begin(xg_ctx *c, int max_launches, int mode)
 {
-    if (max_launches < 1) return XG_EARG;
+    if (mode != 1 && mode != 2) return XG_EARG;
+    if (mode == 1 && max_launches < 1) return XG_EARG;
     HIPCHK(hipSetDevice(c->device));
-    while (c->kev.size() < 2 * (size_t)max_launches) {
+    const size_t need = mode == 1 ? 2 * (size_t)max_launches : 2;
+    while (c->kev.size() < need) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
         c->kev.push_back(e);
     }
-    c->kbytes.resize(max_launches);
+    c->kbytes.resize(mode == 1 ? max_launches : 0);
     c->nk = 0;
-    c->kt_on = true;
+    c->kt_bytes = 0;
+    c->kt_mode = mode;
+    if (mode == 2) HIPCHK(hipEventRecord(c->kev[0], c->stream));
     return XG_OK;
 }
 
 extern "C" int xg_ktime_end(xg_ctx *c, double *total_ms, int *launches, int64_t *bytes)
 {
     double tot = 0;
-    int64_t b = 0;
-    c->kt_on = false;
+    const int mode = c->kt_mode;
+    c->kt_mode = 0;
+    if (mode == 2) HIPCHK(hipEventRecord(c->kev[1], c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    for (int k = 0; k < c->nk; ++k) {
+    if (mode == 2) {
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, c->kev[2 * k], c->kev[2 * k + 1]));
-        tot += ms;
-        b += c->kbytes[k];
+        HIPCHK(hipEventElapsedTime(&ms, c->kev[0], c->kev[1]));
+        tot = ms;
+    } else {
+        for (int k = 0; k < c->nk; ++k) {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, c->kev[2 * k], c->kev[2 * k + 1]));
+            tot += ms;
+        }
     }
     if (total_ms) *total_ms = tot;
     if (launches) *launches = c->nk;
-    if (bytes) *bytes = b;
+    if (bytes) *bytes = c->kt_bytes;
     return XG_OK;
 }
 
 extern "C" int xg_ktime_launch(xg_ctx *c, int k, double *ms, int64_t *bytes)
 {
-    if (k < 0 || k >= c->nk || c->kt_on) return XG_EARG;
+    if (k < 0 || k >= c->nk || c->kt_mode || (int)c->kbytes.size() <= k) return XG_EARG;
     float t = 0;
     HIPCHK(hipEventElapsedTime(&t, c->kev[2 * k], c->kev[2 * k + 1]));
     if (ms) *ms = t;
     if (bytes) *bytes = c->kbytes[k];
-    return XG_OK;
-}
-
-// ------------------------------------------------------------------ microbenchmark: HBM copy ceiling
-// kind 0: grid-stride float4 copy (the canonical copy), grid = 256 CUs x 8 blocks
-// kind 1: copy_kernel<4> over 64 KiB pieces (the exchange's default)
-// kind 2: span_copy_kernel<4>, 2048 workgroups, equal contiguous byte ranges
-// gbps = 2 * bytes / average time (read + write)
-extern "C" int xg_copy_ceiling(xg_ctx *c, int64_t bytes, int kind, int reps, double *gbps)
-{
-    HIPCHK(hipSetDevice(c->device));
-    bytes &= ~(int64_t)65535;
-    if (bytes <= 0 || reps < 1) return XG_EARG;
-    uint8_t *a, *b;
-    HIPCHK(hipMalloc(&a, bytes));
-    HIPCHK(hipMalloc(&b, bytes));
-    HIPCHK(hipMemsetAsync(a, 1, bytes, c->stream));
-    std::vector<xgk::DCopy> pieces;
-    for (int64_t o = 0; o < bytes; o += 65536) pieces.push_back({a + o, b + o, 65536});
-    xgk::DCopy *dp;
-    xgk::DSpan sp = {a, b, bytes, 0}, *ds;
-    HIPCHK(hipMalloc(&dp, sizeof(xgk::DCopy) * pieces.size()));
-    HIPCHK(hipMemcpy(dp, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMalloc(&ds, sizeof sp));
-    HIPCHK(hipMemcpy(ds, &sp, sizeof sp, hipMemcpyHostToDevice));
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    const int nb = 2048;
-    const int64_t per = ((bytes + nb - 1) / nb + 4095) & ~(int64_t)4095;
-    for (int r = -2; r < reps; ++r) {          // 2 warm-up launches
-        if (r == 0) HIPCHK(hipEventRecord(e0, c->stream));
-        if (kind == 0)
-            hipLaunchKernelGGL(xgk::gridstride_copy_kernel, dim3(nb), dim3(xgk::kThreads), 0, c->stream,
-                               (const uint4 *)a, (uint4 *)b, bytes / 16);
-        else if (kind == 1)
-            hipLaunchKernelGGL((xgk::copy_kernel<4, false>), dim3((unsigned)pieces.size()), dim3(xgk::kThreads), 0,
-                               c->stream, dp);
-        else if (kind == 2)
-            hipLaunchKernelGGL((xgk::span_copy_kernel<4>), dim3(nb), dim3(xgk::kThreads), 0, c->stream, ds, 1, bytes,
-                               per);
-        else if (kind == 3)
-            hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3((unsigned)pieces.size()), dim3(xgk::kThreads), 0,
-                               c->stream, dp);
-        else if (kind == 4)
-            hipLaunchKernelGGL((xgk::copy_kernel_g<2>), dim3((unsigned)pieces.size()), dim3(xgk::kThreads), 0,
-                               c->stream, dp);
-        else if (kind == 5)
-            hipLaunchKernelGGL(xgk::read_only_kernel, dim3(nb * 2), dim3(xgk::kThreads), 0, c->stream,
-                               (xgk::g_cu4 *)a, bytes / 16, (unsigned *)ds);
-        else
-            hipLaunchKernelGGL(xgk::write_only_kernel, dim3(nb * 2), dim3(xgk::kThreads), 0, c->stream,
-                               (xgk::g_u4 *)b, bytes / 16);
-        HIPCHK(hipGetLastError());
-    }
-    HIPCHK(hipEventRecord(e1, c->stream));
-    HIPCHK(hipEventSynchronize(e1));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-    *gbps = (kind >= 5 ? 1.0 : 2.0) * (double)bytes * reps / (ms * 1e-3) / 1e9;
-    HIPCHK(hipEventDestroy(e0));
-    HIPCHK(hipEventDestroy(e1));
-    HIPCHK(hipFree(a));
-    HIPCHK(hipFree(b));
-    HIPCHK(hipFree(dp));
-    HIPCHK(hipFree(ds));
     return XG_OK;
 }
 

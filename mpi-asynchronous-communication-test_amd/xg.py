@@ -60,6 +60,10 @@ class DevPlan(C.Structure):
                 ("remote_recv_bytes", C.c_int64)]
 
 
+class Span(C.Structure):
+    _fields_ = [("src", C.c_uint64), ("dst", C.c_uint64), ("len", C.c_uint64)]
+
+
 class SegRun(C.Structure):
     _fields_ = [("rank", C.c_int32), ("seed0", C.c_int32), ("off", C.c_int64), ("nsegs", C.c_int32),
                 ("pad", C.c_int32)]
@@ -128,6 +132,7 @@ def host():
         h.xg_devplan_free.argtypes = [C.POINTER(DevPlan)]
         h.xg_fill_runs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(SegRun)]
         h.xg_verify_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(Slot)]
+        h.xg_engine_hazards.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int)]
         h.xg_summarize_results.argtypes = [C.c_int] * 6 + [C.c_char_p, C.c_char_p, Timer, Timer]
         _host = h
     return _host
@@ -138,6 +143,20 @@ def aggregator_list(procs, cb_nodes, proc_node=1, agg_type=1):
     if host().xg_aggregator_list(procs, cb_nodes, proc_node, agg_type, rl) != 0:
         raise XGError("aggregator type %d is not defined by the reference" % agg_type)
     return list(rl)
+
+
+def engine_hazards(steps, force=False):
+    """xg_engine_hazards over steps = [[(src, dst, len), ...], ...] (byte addresses):
+    returns (flags per step, number of hazard points)."""
+    spans = [x for st in steps for x in st]
+    arr = (Span * max(1, len(spans)))(*[Span(*x) for x in spans])
+    beg = [0]
+    for st in steps:
+        beg.append(beg[-1] + len(st))
+    sb = (C.c_int * len(beg))(*beg)
+    fl = (C.c_int * max(1, len(steps)))()
+    n = host().xg_engine_hazards(arr, sb, len(steps), 1 if force else 0, fl)
+    return list(fl)[:len(steps)], n
 
 
 def method_label(method):
@@ -303,6 +322,7 @@ def device():
         d.xg_regions_ptr.restype = vp
         d.xg_regions_ptr.argtypes = [vp, ip]
         d.xg_regions_read.argtypes = [vp, ip, i64, vp, i64]
+        d.xg_regions_write.argtypes = [vp, ip, i64, vp, i64]
         d.xg_fill.argtypes = [vp, C.POINTER(SegRun), ip, i64, ip, ip]
         d.xg_verify.argtypes = [vp, C.POINTER(Slot), ip, i64, ip, ip, C.POINTER(C.c_uint64),
                                 C.POINTER(i64), C.POINTER(i64)]
@@ -312,11 +332,14 @@ def device():
         d.xg_plan_run.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
         d.xg_plan_enqueue.argtypes = [vp]
         d.xg_plan_engine.argtypes = [vp]
-        d.xg_ktime_begin.argtypes = [vp, ip]
+        d.xg_plan_check.argtypes = [vp]
+        d.xg_plan_launches.argtypes = [vp]
+        d.xg_plan_engine_steps.argtypes = [vp, C.POINTER(ip), C.POINTER(ip)]
+        d.xg_plan_displs.argtypes = [vp, C.POINTER(i64), ip]
+        d.xg_ktime_begin.argtypes = [vp, ip, ip]
         d.xg_ktime_end.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(ip), C.POINTER(i64)]
         d.xg_ktime_launch.argtypes = [vp, ip, C.POINTER(C.c_double), C.POINTER(i64)]
         d.xg_set_copy_params.argtypes = [vp, i64, ip]
-        d.xg_copy_ceiling.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double)]
         d.xg_p2p_bench.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         _dev = d
     return _dev
@@ -381,18 +404,15 @@ class Context:
     def set_copy_params(self, chunk=0, variant=0):
         _check(_dev.xg_set_copy_params(self._c, chunk, variant), "xg_set_copy_params")
 
-    def copy_ceiling(self, nbytes, kind, reps=20):
-        g = C.c_double()
-        _check(_dev.xg_copy_ceiling(self._c, nbytes, kind, reps, C.byref(g)), "xg_copy_ceiling")
-        return g.value
-
     def p2p_bench(self, nbytes, mode=0, reps=20):
         g, sec = C.c_double(), C.c_double()
         _check(_dev.xg_p2p_bench(self._c, nbytes, mode, reps, C.byref(g), C.byref(sec)), "xg_p2p_bench")
         return g.value, sec.value
 
-    def ktime_begin(self, max_launches=4096):
-        _check(_dev.xg_ktime_begin(self._c, max_launches), "xg_ktime_begin")
+    def ktime_begin(self, max_launches=4096, per_launch=True):
+        """per_launch: an event pair around every copy / engine launch; else one pair
+        around the whole session on the main stream (launches and bytes counted)."""
+        _check(_dev.xg_ktime_begin(self._c, max_launches, 1 if per_launch else 2), "xg_ktime_begin")
 
     def ktime_end(self):
         ms, n, b = C.c_double(), C.c_int(), C.c_int64()
@@ -466,6 +486,33 @@ class MethodRun:
 
     def enqueue(self):
         _check(_dev.xg_plan_enqueue(self._p), "xg_plan_enqueue")
+
+    def check(self):
+        """after a synchronised enqueue(): raise if a step-engine barrier timed out"""
+        _check(_dev.xg_plan_check(self._p), "xg_plan_check")
+
+    @property
+    def launches(self):
+        """kernel launches per run (copy + engine launches)"""
+        return _dev.xg_plan_launches(self._p)
+
+    def engine_steps(self):
+        """(steps inside engine segments, segments, hazard barriers)"""
+        ns, nh = C.c_int(), C.c_int()
+        n = _dev.xg_plan_engine_steps(self._p, C.byref(ns), C.byref(nh))
+        return n, ns.value, nh.value
+
+    def displs(self):
+        """staging displacements of the packed segments, as the device scan computed them"""
+        n = _dev.xg_plan_displs(self._p, None, 0)
+        out = (C.c_int64 * max(1, n))()
+        _check(_dev.xg_plan_displs(self._p, out, n), "xg_plan_displs")
+        return list(out)[:n]
+
+    def write(self, buf, off, data):
+        """test hook: overwrite bytes of a region"""
+        b = C.create_string_buffer(bytes(data), len(data))
+        _check(_dev.xg_regions_write(self._r, buf, off, b, len(data)), "xg_regions_write")
 
     def poison(self):
         _check(_dev.xg_regions_poison(self._r), "xg_regions_poison")
