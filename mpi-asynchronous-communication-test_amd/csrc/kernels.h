@@ -18,6 +18,8 @@
 //                     a multiple of 16) are realigned through LDS.
 //  step_engine_kernel a whole GPU-local run of small steps in one persistent
 //                     launch: bursts per step, grid barrier + wall-clock stamp between.
+//  solo_engine_kernel the same for small plans in ONE workgroup: workgroup barrier
+//                     between steps, loads of later steps in flight ahead of the stores.
 //  displ_scan_kernel  staging displacements of packed segments (wave64 prefix scan),
 //  displ_apply_kernel the device replacement of *_alltoall_translate (:233-302).
 //  verify_kernel      check_buffer (mpi_test.c:83-92) + xg_chk64 per receive slot.
@@ -321,8 +323,6 @@ struct EngineState {
     unsigned pad[2];
 };
 
-typedef __attribute__((address_space(1))) unsigned g_u32;
-
 template <int B>
 __device__ __forceinline__ void burst_load16(const uint8_t *src, int64_t len, u32x4 *v)
 {
@@ -339,13 +339,46 @@ __device__ __forceinline__ void burst_store16(uint8_t *dst, int64_t len, const u
     for (int k = 0; k < B; ++k) bstore16(r, ((int)threadIdx.x + k * kThreads) * 16, v[k]);
 }
 
+// Doorbell (host-pinned memory, one per plan): an ARMED engine launch announces
+// `ready` once it runs and waits for the host to ring before its first step, so
+// the launch and dispatch latency falls before the timed region starts (as a
+// persistent MPI request is set up before MPI_Start); `done` is written after
+// the last step's stores are performed.  Every word is accessed with
+// system-scope vector loads/stores by one lane; every wait is bounded.
+struct Doorbell {
+    unsigned ring, ready, done, pad;
+};
+
+typedef __attribute__((address_space(1))) unsigned g_u32;
+
+constexpr unsigned kRingSpins = 1u << 26;     // ~2 s of s_sleep(1) polls: then give up
+
+// lane 0: announce, wait for the ring; false = gave up (the launch does nothing)
+__device__ __forceinline__ bool wait_ring(Doorbell *db, unsigned epoch)
+{
+    g_u32 *ring = (g_u32 *)&db->ring;
+    __hip_atomic_store((g_u32 *)&db->ready, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (unsigned spins = 0; __hip_atomic_load(ring, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kRingSpins) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ void ring_done(Doorbell *db, unsigned epoch)
+{
+    __hip_atomic_store((g_u32 *)&db->done, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // B: 16-B loads per lane per unit -> units of B * 4 KiB (the host cuts the step's
 // transfers to that size and picks B so that a step has enough units to spread).
+// db != nullptr: armed launch -- workgroup 0 waits for the ring, then every
+// workgroup passes one extra grid barrier (tickets base .. base + W) before step 0.
 template <int B>
 __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__restrict__ pieces,
                                                                const int *__restrict__ step_begin, int nsteps,
                                                                EngineState *st, unsigned long long *stamps,
-                                                               unsigned base)
+                                                               unsigned base, Doorbell *db, unsigned epoch)
 {
     // compare tickets by difference, which is wrap-safe
     const unsigned W = gridDim.x;
@@ -354,6 +387,29 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
     __shared__ int give_up;
     if (threadIdx.x == 0) give_up = 0;
     __syncthreads();
+    if (db) {
+        if (threadIdx.x == 0) {
+            bool ok = blockIdx.x != 0 || wait_ring(db, epoch);
+            if (!ok) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned target = base + W;
+            __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (unsigned spins = 0;
+                 (int)(__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0;) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kRingSpins || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            if (__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) give_up = 1;
+        }
+        __syncthreads();
+        if (give_up) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) ring_done(db, epoch);
+            return;
+        }
+        base += W;
+    }
     // This workgroup's first unit of the next step is LOADED while the barrier is
     // pending (into v[]) and stored once it opens: the load latency of each step
     // (HBM + address translation of fresh pages) overlaps the barrier.  pf is
@@ -392,7 +448,10 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
             }
             const unsigned t = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
             last = t == target;
-            if (last) stamps[s] = (unsigned long long)wall_clock64();
+            if (last) {
+                stamps[s] = (unsigned long long)wall_clock64();
+                if (db && s + 1 == nsteps) ring_done(db, epoch);
+            }
         }
         if (s + 1 < nsteps && fl != 2) {   // step s+1 reads nothing written since the last hazard point
             const int j = step_begin[s + 1] + (int)blockIdx.x;
@@ -419,6 +478,158 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
         }
         __syncthreads();
         if (give_up) return;
+    }
+}
+
+// ---------------------------------------------------------------- solo engine
+// The same plans when they are small (README-sized latency chains: tens of steps
+// of tens of KiB): ONE workgroup of 16 waves runs every step, so the step
+// boundary is a workgroup barrier (tens of ns) instead of a grid barrier across
+// CUs (~1 us of device-scope atomics and polling).  The plan is cut into rows of
+// 16 pieces of <= 1 KiB, piece (row, w) moved by wave w (64 lanes x 16 B); a
+// step's pieces are padded to whole rows.  K rows are loaded at once (every
+// lane has K 16-B loads in flight, 16 x K KiB per workgroup) and stored in
+// order, with a barrier + wall-clock stamp wherever a step ends: the loads of
+// later steps run ahead of the stores of earlier ones -- valid because no step
+// reads what another writes (the host uses this engine only for plans without
+// hazard points, xg_engine_hazards) -- while stores keep the step order.  Like
+// flag 0 of the grid engine, a step's stamp is the time its stores were issued;
+// the last step waits for its stores (delivered time).
+constexpr int kSoloWaves = 16;
+constexpr int kSoloThreads = kSoloWaves * 64;
+constexpr int kSoloPiece = 64 * 16;              // bytes per wave per row
+constexpr int kSoloK = 8;                        // rows per chunk (2 chunks x 8 x 16 KiB in flight)
+constexpr int kSoloMaxSteps = 2048;              // stamps kept in LDS (16 KiB)
+constexpr int kSoloMaxPieces = 4608;             // descriptors kept in LDS (4608 x 24 B = 108 KiB)
+
+// One solo piece in 64 bits: source and destination offsets (16-B units, 24 bits)
+// from the segment's two base pointers, the length (16-B units, <= 64, 7 bits) and
+// `before` (5 bits): how many of its row's step barriers come before this piece.
+// Steps are packed back to back, so a row may hold the end of one step and the
+// start of the next: every wave executes all of the row's barriers, its store
+// after the first `before` of them.
+__host__ __device__ constexpr unsigned long long solo_desc(uint64_t src16, uint64_t dst16, uint64_t len16,
+                                                           uint64_t before)
+{
+    return src16 | (dst16 << 24) | (len16 << 48) | (before << 55);
+}
+constexpr uint64_t kSoloOffMax = 1ull << 24;     // offsets < 256 MiB from the bases
+
+// Host contract (build_segments): every piece 16-B aligned, <= 1 KiB, within 256 MiB
+// of the bases; row_close[r] = step barriers inside or in front of row r (rows + 1
+// entries), each piece's `before` field saying where it sits among them;
+// rows form an even number of chunks of K plus one spare empty chunk;
+// nsteps <= kSoloMaxSteps; pieces <= kSoloMaxPieces.  The descriptor table is
+// staged into LDS before the doorbell (plan set-up: no payload byte moves before
+// the ring), read back a chunk at a time in one batch; each piece becomes a
+// buffer resource whose range check drops the lanes past its end (an empty
+// padding piece moves nothing), so the body has no branch but the step barriers.
+template <int K>
+struct SoloChunk {
+    unsigned long long d[K];
+    u32x4 v[K];
+};
+
+// issue the K 16-B loads of chunk c of this wave
+template <int K>
+__device__ __forceinline__ void solo_load(SoloChunk<K> &b, const unsigned long long *ldesc, int c, int wave,
+                                          uint64_t l16, const uint8_t *src_base)
+{
+#pragma unroll
+    for (int k = 0; k < K; ++k) b.d[k] = ldesc[(c * K + k) * kSoloWaves + wave];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        // the descriptor is wave-uniform: a buffer resource in SGPRs whose range check
+        // (num_records = the piece's bytes) drops the lanes past its end -- an empty
+        // padding piece moves nothing
+        const unsigned long long d = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(b.d[k] >> 32)) << 32) |
+                                     (unsigned)__builtin_amdgcn_readfirstlane((int)b.d[k]);
+        const brsrc r = make_rsrc(src_base + ((d & (kSoloOffMax - 1)) << 4), (int64_t)((d >> 48) & 127) << 4);
+        b.v[k] = bload16(r, (int)l16 * 16);
+    }
+}
+
+// close the next step: every wave has issued its stores of it; stamp
+__device__ __forceinline__ void solo_close(unsigned long long *ts, int &s)
+{
+    __syncthreads();
+    if (threadIdx.x == 0) ts[s] = (unsigned long long)wall_clock64();
+    ++s;
+}
+
+// store chunk c in row order; a row that begins new steps first closes the ones before
+// it: barrier (every wave issued their stores), stamp
+template <int K>
+__device__ __forceinline__ void solo_store(const SoloChunk<K> &b, const unsigned short *lclose,
+                                          unsigned long long *ts, int &s, int c, uint64_t l16, uint8_t *dst_base)
+{
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int n = __builtin_amdgcn_readfirstlane((int)lclose[c * K + k]);     // barriers in this row
+        const int bf = __builtin_amdgcn_readfirstlane((int)(b.d[k] >> 55));      // ... before my piece
+        int j = 0;
+        for (; j < bf; ++j) solo_close(ts, s);
+        asm volatile("" ::: "memory");        // the store stays between its steps' barriers
+        const unsigned long long d = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(b.d[k] >> 32)) << 32) |
+                                     (unsigned)__builtin_amdgcn_readfirstlane((int)b.d[k]);
+        const brsrc r = make_rsrc(dst_base + (((d >> 24) & (kSoloOffMax - 1)) << 4), (int64_t)((d >> 48) & 127) << 4);
+        bstore16(r, (int)l16 * 16, b.v[k]);
+        asm volatile("" ::: "memory");
+        for (; j < n; ++j) solo_close(ts, s);
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigned long long *__restrict__ desc,
+                                                                   int npieces, const uint8_t *src_base,
+                                                                   uint8_t *dst_base,
+                                                                   const int *__restrict__ row_close, int nsteps,
+                                                                   EngineState *st,
+                                                                   unsigned long long *stamps, Doorbell *db,
+                                                                   unsigned epoch)
+{
+    const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    __shared__ unsigned long long ldesc[kSoloMaxPieces];
+    __shared__ unsigned short lclose[kSoloMaxPieces / kSoloWaves + 1];
+    __shared__ unsigned long long ts[kSoloMaxSteps];
+    __shared__ int give_up;
+    const int nrows = npieces / kSoloWaves;
+    for (int i = (int)threadIdx.x; i < npieces; i += kSoloThreads) ldesc[i] = desc[i];
+    for (int i = (int)threadIdx.x; i <= nrows; i += kSoloThreads) lclose[i] = (unsigned short)row_close[i];
+    if (threadIdx.x == 0) give_up = db && !wait_ring(db, epoch);
+    __syncthreads();
+    if (give_up) {
+        if (threadIdx.x == 0) {
+            __hip_atomic_store((g_u32 *)&st->tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ring_done(db, epoch);
+        }
+        return;
+    }
+    const uint64_t l16 = (uint64_t)lane;
+    // double buffer: chunk c+1's loads fly while chunk c stores.  The host pads the
+    // table to an even number of chunks plus one spare empty chunk, so every load
+    // below is unconditional (a conditional one would make the compiler wait on it).
+    const int nchunks = nrows / K - 1;
+    SoloChunk<K> A, B;
+    int s = 0;
+    solo_load<K>(A, ldesc, 0, wave, l16, src_base);
+    for (int c = 0; c < nchunks; c += 2) {
+        solo_load<K>(B, ldesc, c + 1, wave, l16, src_base);
+        solo_store<K>(A, lclose, ts, s, c, l16, dst_base);
+        solo_load<K>(A, ldesc, c + 2, wave, l16, src_base);
+        solo_store<K>(B, lclose, ts, s, c + 1, l16, dst_base);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last steps: delivered
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long t = (unsigned long long)wall_clock64();
+        for (; s < nsteps; ++s) ts[s] = t;
+    }
+    __syncthreads();
+    for (int i = (int)threadIdx.x; i < nsteps; i += kSoloThreads) stamps[i] = ts[i];
+    if (db && threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ring_done(db, epoch);
     }
 }
 

@@ -56,6 +56,9 @@ struct xg_ctx {
     int64_t engine_max_step;   // GPU-local plans whose largest step moves <= this many bytes use the step engine
     int engine_wmax;           // at most this many (co-resident) engine workgroups
     int engine_drain;          // 1: always drain before each barrier arrival (XG_ENGINE_DRAIN=1)
+    int64_t solo_step;         // hazard-free segments averaging <= this many bytes per step run solo
+    int64_t solo_max;          // ... and moving <= this many bytes in all
+    int engine_arm;            // 1: xg_plan_run arms single-segment plans (doorbell)
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
     int engine_occ;            // co-resident step-engine workgroups the device admits (plan load caps W)
@@ -90,7 +93,13 @@ struct EngSeg {
     int s0, s1;                    // steps [s0, s1)
     int w, b;                      // workgroups; 16-B loads per lane per unit (1, 4, 16)
     int sb_off;                    // its block in d_sb: (n + 1) unit offsets, then n flags
+                                   // (solo: n + 1 row offsets)
     int nhaz;                      // hazard points (xg_engine_hazards flag 2)
+    bool solo;                     // one workgroup (solo_engine_kernel), pieces from u0
+    int u0;                        // first unit / piece of the segment in d_epieces
+    int npieces;                   // solo: pieces (whole chunks of rows), from u0 in d_solo
+    const uint8_t *sbase;          // solo: base pointers of the descriptors' offsets
+    uint8_t *dbase;
     int64_t bytes;                 // bytes copied per run
 };
 
@@ -114,6 +123,10 @@ struct xg_plan {
     xgk::EngineState *d_engine;    // state (16 B, zeroed at load) followed by nsteps stamps
     unsigned engine_base;          // barrier tickets taken by earlier launches (wraps)
     bool engine_reset;             // zero the state before the next launch
+    xgk::Doorbell *db;             // host-pinned doorbell of armed runs (single-segment plans), or null
+    std::vector<unsigned long long> solo_desc;   // solo segments' packed pieces (host copy)
+    unsigned long long *d_solo;
+    unsigned epoch;                // armed launches so far
     // staging displacements of the packed segments, computed on the device at load
     int64_t *d_disp;
     int ndisp;
@@ -211,6 +224,14 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     }
     env = getenv("XG_ENGINE_DRAIN");         // "1": drain every step even without a hazard
     c->engine_drain = env && !strcmp(env, "1");
+    c->solo_step = 64 << 10;          // see DESIGN.md (solo engine) for the measured crossover
+    c->solo_max = 8 << 20;
+    env = getenv("XG_ENGINE_SOLO_STEP");     // 0: never solo
+    if (env) c->solo_step = atol(env);
+    env = getenv("XG_ENGINE_SOLO_MAX");
+    if (env) c->solo_max = atol(env);
+    env = getenv("XG_ENGINE_ARM");           // "0": launch latency inside the timed region
+    c->engine_arm = !(env && !strcmp(env, "0"));
     {
         int khz = 0;
         HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
@@ -539,8 +560,69 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         g.nhaz = xg_engine_hazards(spans.data(), tb.data(), n, c->engine_drain, fl.data());
         g.w = std::max(1, std::min(maxu, c->engine_wmax));
         g.sb_off = (int)sb.size();
-        for (int t = 0; t <= n; ++t) sb.push_back(u0 + beg[t]);
-        sb.insert(sb.end(), fl.begin(), fl.end());
+        bool aligned = true;
+        for (const auto &xs : xfer)
+            for (const xgk::DCopy &x : xs)
+                aligned = aligned && ((((uintptr_t)x.src | (uintptr_t)x.dst | (uint64_t)x.len) & 15) == 0);
+        // solo: rows of kSoloWaves pieces of <= 1 KiB, each step padded to whole rows, the
+        // segment to whole chunks of kSoloK rows; padding pieces (len 0) move nothing
+        int64_t solo_pieces = 0;
+        for (const auto &xs : xfer)
+            for (const xgk::DCopy &x : xs) solo_pieces += (x.len + xgk::kSoloPiece - 1) / xgk::kSoloPiece;
+        // whole chunks of kSoloK rows, an even number of them, plus the spare chunk the
+        // double-buffered loop prefetches past the end
+        const int64_t chunk_pieces = (int64_t)xgk::kSoloWaves * xgk::kSoloK;
+        solo_pieces = ((solo_pieces + 2 * chunk_pieces - 1) / (2 * chunk_pieces) * 2 + 1) * chunk_pieces;
+        // the segment's source and destination base pointers (solo descriptors are offsets)
+        uintptr_t slo = UINTPTR_MAX, shi = 0, dlo = UINTPTR_MAX, dhi = 0;
+        for (const auto &xs : xfer)
+            for (const xgk::DCopy &x : xs)
+                if (x.len > 0) {
+                    slo = std::min(slo, (uintptr_t)x.src); shi = std::max(shi, (uintptr_t)x.src + (uintptr_t)x.len);
+                    dlo = std::min(dlo, (uintptr_t)x.dst); dhi = std::max(dhi, (uintptr_t)x.dst + (uintptr_t)x.len);
+                }
+        const bool near = shi > slo && dhi > dlo && (shi - slo) / 16 < xgk::kSoloOffMax && (dhi - dlo) / 16 < xgk::kSoloOffMax;
+        g.solo = g.nhaz == 0 && aligned && near && n <= xgk::kSoloMaxSteps && solo_pieces <= xgk::kSoloMaxPieces &&
+                 c->solo_step > 0 && g.bytes <= c->solo_max && g.bytes <= c->solo_step * n;
+        if (g.solo) {
+            g.sbase = (const uint8_t *)slo;
+            g.dbase = (uint8_t *)dlo;
+            ep.resize(u0);
+            g.u0 = (int)p->solo_desc.size();
+            g.w = 1;
+            std::vector<unsigned long long> &sd = p->solo_desc;
+            const size_t d0 = sd.size();
+            std::vector<int64_t> pend(n);          // first piece after step t (its closing barrier)
+            for (int t = 0; t < n; ++t) {
+                for (const xgk::DCopy &x : xfer[t])
+                    for (int64_t o = 0; o < x.len; o += xgk::kSoloPiece)
+                        sd.push_back(xgk::solo_desc(((uintptr_t)x.src + o - slo) / 16, ((uintptr_t)x.dst + o - dlo) / 16,
+                                                    std::min<int64_t>(x.len - o, xgk::kSoloPiece) / 16, 0));
+                pend[t] = (int64_t)(sd.size() - d0);
+            }
+            const int64_t real = (int64_t)(sd.size() - d0);
+            while ((sd.size() - d0) % (2 * chunk_pieces)) sd.push_back(0);
+            sd.insert(sd.end(), chunk_pieces, 0ull);
+            g.npieces = (int)(sd.size() - d0);
+            // the barrier closing step t sits in front of piece pend[t]: in its row, and
+            // before the pieces at or after its column; steps ending with the last piece
+            // close after the loop
+            std::vector<int> close(g.npieces / xgk::kSoloWaves + 1, 0);
+            for (int t = 0; t < n; ++t) {
+                if (pend[t] >= real) continue;
+                const int64_t row = pend[t] / xgk::kSoloWaves, col = pend[t] % xgk::kSoloWaves;
+                close[row]++;
+                for (int64_t w = col; w < xgk::kSoloWaves; ++w) sd[d0 + row * xgk::kSoloWaves + w] += 1ull << 55;
+            }
+            for (size_t i = d0; i < sd.size(); ++i)
+                if ((sd[i] >> 55) > 31) return XG_EARG;      // cannot happen: <= 16 per row
+            sb.insert(sb.end(), close.begin(), close.end());
+        } else {
+            g.npieces = 0;
+            g.u0 = 0;
+            for (int t = 0; t <= n; ++t) sb.push_back(u0 + beg[t]);
+            sb.insert(sb.end(), fl.begin(), fl.end());
+        }
         for (int t = s; t < e; ++t) p->seg_of[t] = (int)p->segs.size();
         p->segs.push_back(g);
         s = e;
@@ -552,8 +634,18 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         HIPCHK(hipMalloc(&p->d_epieces, sizeof(xgk::DCopy) * ep.size()));
         HIPCHK(hipMemcpy(p->d_epieces, ep.data(), sizeof(xgk::DCopy) * ep.size(), hipMemcpyHostToDevice));
     }
+    if (!p->solo_desc.empty()) {
+        const size_t nb = sizeof(unsigned long long) * p->solo_desc.size();
+        HIPCHK(hipMalloc(&p->d_solo, nb));
+        HIPCHK(hipMemcpy(p->d_solo, p->solo_desc.data(), nb, hipMemcpyHostToDevice));
+    }
     HIPCHK(hipMalloc(&p->d_engine, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps));
     HIPCHK(hipMemset(p->d_engine, 0, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps));
+    // a plan that is ONE segment can be armed by xg_plan_run (doorbell in host memory)
+    if (c->engine_arm && !c->virt && p->segs.size() == 1 && p->segs[0].s0 == 0 && p->segs[0].s1 == p->nsteps) {
+        HIPCHK(hipHostMalloc((void **)&p->db, sizeof(xgk::Doorbell), hipHostMallocCoherent));
+        memset((void *)p->db, 0, sizeof(xgk::Doorbell));
+    }
     return XG_OK;
 }
 
@@ -637,6 +729,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant;
     p->d_pieces = nullptr; p->d_sb = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->d_disp = nullptr;
     p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
+    p->db = nullptr; p->epoch = 0; p->d_solo = nullptr;
     // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
     // pieces for small launches were measured no faster, and slower where they stop
     // dividing the segment size (profiles/r01_min_pieces_ab.txt)
@@ -761,6 +854,8 @@ extern "C" int xg_plan_free(xg_plan *p)
     if (p->d_epieces) HIPCHK(hipFree(p->d_epieces));
     if (p->d_engine) HIPCHK(hipFree(p->d_engine));
     if (p->d_disp) HIPCHK(hipFree(p->d_disp));
+    if (p->db) HIPCHK(hipHostFree((void *)p->db));
+    if (p->d_solo) HIPCHK(hipFree(p->d_solo));
     for (auto &e : p->ev) HIPCHK(hipEventDestroy(e));
     for (auto &e : p->fork) if (e) HIPCHK(hipEventDestroy(e));
     for (auto &e : p->join) if (e) HIPCHK(hipEventDestroy(e));
@@ -899,8 +994,8 @@ static int enqueue_step(xg_plan *p, int s)
     return XG_OK;
 }
 
-// one launch of the step engine over segment g
-static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream)
+// one launch of the step engine over segment g (armed: waits for the doorbell `epoch`)
+static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream, bool armed = false)
 {
     xg_ctx *c = p->ctx;
     int rc;
@@ -910,21 +1005,27 @@ static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream)
         p->engine_reset = false;
     }
     const int n = g.s1 - g.s0;
+    xgk::Doorbell *db = armed ? p->db : nullptr;
+    const unsigned epoch = armed ? ++p->epoch : 0;
     const unsigned base = p->engine_base;
-    p->engine_base += (unsigned)n * (unsigned)g.w;
+    if (!g.solo) p->engine_base += (unsigned)(n + (armed ? 1 : 0)) * (unsigned)g.w;
     bool kt;
     if ((rc = kt_before(c, stream, &kt))) return rc;
     unsigned long long *stamps = reinterpret_cast<unsigned long long *>(p->d_engine + 1) + g.s0;
     const int *sb = p->d_sb + g.sb_off;
-    if (g.b == 1)
+    if (g.solo)
+        hipLaunchKernelGGL(xgk::solo_engine_kernel<xgk::kSoloK>, dim3(1), dim3(xgk::kSoloThreads), 0, stream,
+                           p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, db,
+                           epoch);
+    else if (g.b == 1)
         hipLaunchKernelGGL(xgk::step_engine_kernel<1>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb, n,
-                           p->d_engine, stamps, base);
+                           p->d_engine, stamps, base, db, epoch);
     else if (g.b == 4)
         hipLaunchKernelGGL(xgk::step_engine_kernel<4>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb, n,
-                           p->d_engine, stamps, base);
+                           p->d_engine, stamps, base, db, epoch);
     else
         hipLaunchKernelGGL(xgk::step_engine_kernel<16>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb,
-                           n, p->d_engine, stamps, base);
+                           n, p->d_engine, stamps, base, db, epoch);
     HIPCHK(hipGetLastError());
     return kt_after(c, stream, kt, g.bytes);
 }
@@ -956,11 +1057,60 @@ static int enqueue_unit(xg_plan *p, int s)
     return launch_seg(p, p->segs[gi], p->ctx->stream);
 }
 
+// Armed run of a one-segment plan: the engine is launched, announces itself
+// through the doorbell, and waits; the timed region starts when the host rings
+// and ends when the engine reports its last step delivered (system-scope store
+// to host memory).  The launch and dispatch latency (several us from an idle
+// stream) thus stays outside, like the setup of a persistent MPI request before
+// MPI_Start; every byte still moves inside.  Step times: the wall-clock stamps,
+// anchored at the host-measured end.
+static int run_armed(xg_plan *p, double *step_done, double *step_post, double *wall)
+{
+    xg_ctx *c = p->ctx;
+    const EngSeg &g = p->segs[0];
+    int rc;
+    if ((rc = launch_seg(p, g, c->stream, true))) return rc;
+    const unsigned epoch = p->epoch;
+    const double tl = xg_now();
+    bool ready;
+    while (!(ready = __atomic_load_n(&p->db->ready, __ATOMIC_ACQUIRE) == epoch) && xg_now() - tl < 5.0) {
+    }
+    const double t0 = xg_now();
+    __atomic_store_n(&p->db->ring, epoch, __ATOMIC_RELEASE);
+    const double tp = xg_now();
+    bool done;
+    while (!(done = __atomic_load_n(&p->db->done, __ATOMIC_ACQUIRE) == epoch) && xg_now() - t0 < 10.0) {
+    }
+    const double t1 = xg_now();
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (wall) *wall = xg_now() - t0;
+    if ((rc = xg_plan_check(p))) return rc;
+    if (!ready || !done) {
+        fprintf(stderr, "xg: armed step engine: no %s from the device\n", ready ? "completion" : "ready signal");
+        return XG_EHIP;
+    }
+    if (step_post) {
+        step_post[0] = tp - t0;
+        for (int s = 1; s < p->nsteps; ++s) step_post[s] = 0;
+    }
+    if (step_done) {
+        std::vector<unsigned long long> st(p->nsteps);
+        HIPCHK(hipMemcpy(st.data(), p->d_engine + 1, 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
+        const double total = t1 - t0;
+        for (int s = 0; s < p->nsteps; ++s) {
+            const double x = total - (double)(st[p->nsteps - 1] - st[s]) / c->wall_hz;
+            step_done[s] = s == p->nsteps - 1 ? total : (x > 0 ? x : 0);
+        }
+    }
+    return XG_OK;
+}
+
 extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
 {
     xg_ctx *c = p->ctx;
     int rc;
     HIPCHK(hipSetDevice(c->device));
+    if (p->db && !c->kt_mode) return run_armed(p, step_done, step_post, wall);
     const double t0 = xg_now();
     HIPCHK(hipEventRecord(p->ev0, c->stream));
     for (int s = 0; s < p->nsteps;) {

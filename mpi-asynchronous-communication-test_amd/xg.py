@@ -451,18 +451,47 @@ def run_virtual(runs, rccl=False):
     return list(done)[:runs[0].nsteps]
 
 
+class Regions:
+    """HBM regions (xg_regions_alloc) that several MethodRuns may reuse in turn: at
+    hundreds of GiB, allocating and freeing per method costs seconds (the driver
+    clears fresh pages), refilling and re-poisoning costs milliseconds."""
+
+    def __init__(self, ctx, region_bytes):
+        self.bytes = list(region_bytes)
+        rb = (C.c_int64 * NBUF)(*self.bytes)
+        self._r = C.c_void_p()
+        _check(device().xg_regions_alloc(ctx.handle, rb, C.byref(self._r)), "xg_regions_alloc")
+
+    def fits(self, region_bytes):
+        return all(a <= b for a, b in zip(region_bytes, self.bytes))
+
+    def close(self):
+        if getattr(self, "_r", None):
+            if not self._shared:
+                _check(_dev.xg_regions_free(self._r), "xg_regions_free")
+            self._r = None
+
+
 class MethodRun:
     """prepare_*_data + the compiled plan of one method on this GPU:
-    HBM regions, fingerprint fill (untimed), plan upload."""
+    HBM regions, fingerprint fill (untimed), plan upload.  regions: a Regions
+    object to use (re-poisoned here, not freed by close()) instead of new ones."""
 
-    def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20):
+    def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None):
         d = device()
         self.ctx, self.sched, self.it, self.mode, self.pack_max_seg = ctx, sched, it, mode, pack_max_seg
         G, g = ctx.nranks, ctx.rank
         self.view = sched.devplan(G, g, pack_max_seg)
-        rb = (C.c_int64 * NBUF)(*self.view.region_bytes)
-        self._r = C.c_void_p()
-        _check(d.xg_regions_alloc(ctx.handle, rb, C.byref(self._r)), "xg_regions_alloc")
+        self._shared = regions is not None
+        if regions is not None:
+            if not regions.fits(self.view.region_bytes):
+                raise XGError("MethodRun: shared regions too small for this plan")
+            self._r = regions._r
+            _check(d.xg_regions_poison(self._r), "xg_regions_poison")
+        else:
+            rb = (C.c_int64 * NBUF)(*self.view.region_bytes)
+            self._r = C.c_void_p()
+            _check(d.xg_regions_alloc(ctx.handle, rb, C.byref(self._r)), "xg_regions_alloc")
         n = host().xg_fill_runs(sched.handle, G, g, None)
         runs = (SegRun * max(1, n))()
         host().xg_fill_runs(sched.handle, G, g, runs)
@@ -534,5 +563,6 @@ class MethodRun:
             _check(_dev.xg_plan_free(self._p), "xg_plan_free")
             self._p = None
         if getattr(self, "_r", None):
-            _check(_dev.xg_regions_free(self._r), "xg_regions_free")
+            if not self._shared:
+                _check(_dev.xg_regions_free(self._r), "xg_regions_free")
             self._r = None

@@ -84,3 +84,40 @@ def test_alltoallw_beyond_int32_displacements(xg, ctx, method):
             assert chk[i] == O.chk64(O.fingerprint(1, src, seed, 1, d)), (method, run.slots[i])
     finally:
         run.close()
+
+
+@pytest.fixture(scope="module")
+def big_regions(xg, ctx):
+    """one 256 GiB SEND + RECV allocation for the whole -c sweep (last tests of the module)"""
+    P, A, d = 256, 64, 8 << 20
+    r = xg.Regions(ctx, [P * A * d, P * A * d, 0, 0, 0])
+    yield r
+    r.close()
+
+
+@pytest.mark.parametrize("c", range(1, 9))
+def test_config5_largest_single_gpu_size(xg, ctx, big_regions, c):
+    """configs[4] (P256 A64, half-sync m7 / m11 / m12) at the largest -d one MI355X
+    holds -- 8 MiB: 128 GiB SEND + 128 GiB RECV in HBM -- at every -c of the
+    reference's sweep (script_theta_all_to_many_256.sh:33-106 sweeps -c; here 1..8).
+    Every received byte checked on the device (strong fingerprint), sampled slot
+    checksums against the oracle's closed form."""
+    P, A, d = 256, 64, 8 << 20
+    _arch, _cus, hbm = ctx.info()
+    rl = xg.aggregator_list(P, A)
+    for m in (7, 11, 12):
+        s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
+        need = sum(s.region_bytes(1, 0, b) for b in range(xg.NBUF))
+        assert need == 2 * P * A * d and need < hbm, (need, hbm)
+        run = xg.MethodRun(ctx, s, it=1, mode=1, regions=big_regions)
+        try:
+            done, _post, _wall = run.run_timed()
+            assert len(done) == s.nsteps and all(0 <= a <= b for a, b in zip(done, done[1:]))
+            chk, bad, first = run.verify()
+            assert len(run.slots) == P * A
+            assert not any(bad), (m, c, [(sl, b, f) for sl, b, f in zip(run.slots, bad, first) if b][:3])
+            for i in range(0, len(run.slots), len(run.slots) // 5):
+                src, seed, _dst, _off = run.slots[i]
+                assert chk[i] == O.chk64(O.fingerprint(1, src, seed, 1, d)), (m, c, i)
+        finally:
+            run.close()

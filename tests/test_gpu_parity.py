@@ -158,32 +158,49 @@ def test_step_engine_matches_per_step_launches(xg, ctx, method, d):
         ctx_eager.close()
 
 
+ENGINE_MODES = {
+    "solo_armed": {},                                           # default at README sizes
+    "grid_armed": {"XG_ENGINE_SOLO_STEP": "0"},
+    "solo_launch": {"XG_ENGINE_ARM": "0"},
+    "grid_drain": {"XG_ENGINE_SOLO_STEP": "0", "XG_ENGINE_DRAIN": "1", "XG_ENGINE_ARM": "0"},
+}
+
+
 @pytest.mark.parametrize("k", [1, 3])
-@pytest.mark.parametrize("method", [6, 9, 12])
-def test_step_engine_drain_scan(xg, ctx, method, k):
-    """The engine waits for a step's stores only at the steps its host hazard scan flags
-    (before the next -k repetition rewrites the same slots, and the last step).  Same
-    bytes and ordered step times as with XG_ENGINE_DRAIN=1 (drain at every step)."""
+@pytest.mark.parametrize("method", [6, 9, 12, 18])
+def test_step_engine_modes(xg, method, k):
+    """The README-sized chains under every engine form: one workgroup (solo) or a grid
+    barrier per step, armed by the doorbell or launched inside the timed region, and
+    the grid engine draining at every step (XG_ENGINE_DRAIN=1).  Same bytes (strong
+    fingerprint, every slot against the oracle), step times ordered and within the
+    run's wall time, repeated runs stay correct."""
     import os
     import xg_oracle as O
     P, A, d, c, it = 32, 14, 2048, 3, 0
     rl = xg.aggregator_list(P, A)
-    os.environ["XG_ENGINE_DRAIN"] = "1"
-    try:
-        ctx_drain = xg.Context(rank=0, nranks=1, device=0)
-    finally:
-        del os.environ["XG_ENGINE_DRAIN"]
-    try:
-        s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, iteration=it)
-        exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
-        res = {}
-        for name, cx in (("scan", ctx), ("drain", ctx_drain)):
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, iteration=it)
+    exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
+    res = {}
+    for name, env in ENGINE_MODES.items():
+        old = {key: os.environ.get(key) for key in env}
+        os.environ.update(env)
+        try:
+            cx = xg.Context(rank=0, nranks=1, device=0)
+        finally:
+            for key, v in old.items():
+                if v is None:
+                    del os.environ[key]
+                else:
+                    os.environ[key] = v
+        try:
             run = xg.MethodRun(cx, s, it=it, mode=1)
             try:
                 assert run.engine_workgroups > 0
-                done, _post, wall = run.run_timed()
-                assert all(0 <= a <= b for a, b in zip(done, done[1:])), done
-                assert done[-1] <= wall + 1e-4
+                assert (run.engine_workgroups == 1) == name.startswith("solo"), (name, run.engine_workgroups)
+                for _rep in range(3):
+                    done, _post, wall = run.run_timed()
+                    assert all(0 <= a <= b for a, b in zip(done, done[1:])), (name, done)
+                    assert done[-1] <= wall + 1e-4
                 chk, bad, _f = run.verify()
                 assert all(b == 0 for b in bad), name
                 for (src, seed, dst, off), ck in zip(run.slots, chk):
@@ -192,6 +209,6 @@ def test_step_engine_drain_scan(xg, ctx, method, k):
                 res[name] = chk
             finally:
                 run.close()
-        assert res["scan"] == res["drain"]
-    finally:
-        ctx_drain.close()
+        finally:
+            cx.close()
+    assert all(v == res["solo_armed"] for v in res.values())
