@@ -59,6 +59,8 @@ struct xg_ctx {
     int64_t solo_step;         // hazard-free segments averaging <= this many bytes per step run solo
     int64_t solo_max;          // ... and moving <= this many bytes in all
     int engine_arm;            // 1: xg_plan_run arms single-segment plans (doorbell)
+    int split_local;           // 1: a cross-GPU step's local gather runs on the side stream
+    int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
     int engine_occ;            // co-resident step-engine workgroups the device admits (plan load caps W)
@@ -78,12 +80,17 @@ struct xg_regions {
 };
 
 struct StepR {
-    // pre = [local gather/scatter pieces | pack-into-staging pieces], one launch
-    // unless the step also has cross-GPU ops: then the local part runs on the side
-    // stream beside the RCCL group and only the packs precede it (split).
-    int stage_b, stage_n, pre_b, pre_n, local_n, post_b, post_n, p2p_b, p2p_n, sync_after;
-    int64_t stage_bytes, local_bytes, pack_bytes, post_bytes;   // bytes copied by each launch (read + written once)
-    bool split;
+    // Launches of one step (piece ranges in the plan's piece table):
+    //   stage (TAM rank-local copies), then local gather/scatter + packs into staging
+    //   (one launch; a step with cross-GPU ops runs its local part on the side stream
+    //   beside the packs and the RCCL group: split), the RCCL group, the unpacks.
+    //   fused: this step's packs go in ONE launch with the previous step's unpacks
+    //   (deferred there); a pack only fills staging and delivers nothing, so every
+    //   message of this step is still delivered after every one of the previous step.
+    int stage_b, stage_n, local_b, local_n, pack_b, pack_n, post_b, post_n, p2p_b, p2p_n, sync_after;
+    int pre_n;                       // local_n + pack_n
+    int64_t stage_bytes, local_bytes, pack_bytes, post_bytes;   // bytes copied by each part (read + written once)
+    bool split, fused, deferred;
 };
 
 // A run of >= 2 consecutive GPU-local steps (no RCCL op, no in-loop barrier, no
@@ -131,6 +138,7 @@ struct xg_plan {
     int64_t *d_disp;
     int ndisp;
     int nlaunch;                   // kernel launches per run (copies + engine), RCCL's aside
+    bool rec_ev;                   // xg_plan_run is recording step events (fused launches record the previous step's)
 };
 
 extern "C" double xg_now(void)
@@ -232,6 +240,10 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     if (env) c->solo_max = atol(env);
     env = getenv("XG_ENGINE_ARM");           // "0": launch latency inside the timed region
     c->engine_arm = !(env && !strcmp(env, "0"));
+    env = getenv("XG_SPLIT_LOCAL");          // "0": local gather + packs in one launch
+    c->split_local = !(env && !strcmp(env, "0"));
+    env = getenv("XG_FUSE_UNPACK");          // "0": unpacks and the next step's packs apart
+    c->fuse_unpack = !(env && !strcmp(env, "0"));
     {
         int khz = 0;
         HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
@@ -488,8 +500,8 @@ extern "C" int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_
 // per-launch boundary dominates (profiles/r01_engine_sweep.txt: crossover ~16 MiB).
 static bool engine_step(const xg_ctx *c, const StepR &st)
 {
-    return !st.p2p_n && !st.sync_after && !st.stage_n && !st.post_n &&
-           st.local_bytes + st.pack_bytes <= c->engine_max_step;
+    return !st.p2p_n && !st.sync_after && !st.stage_n && !st.post_n && !st.pack_n && !st.fused && !st.deferred &&
+           st.local_bytes <= c->engine_max_step;
 }
 
 // Build the engine segments of a loaded plan from its host piece table: every
@@ -526,11 +538,11 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         std::vector<std::vector<xgk::DCopy>> xfer(e - s);
         for (int t = s; t < e; ++t) {
             const StepR &st = p->steps[t];
-            for (int i = st.pre_b; i < st.pre_b + st.pre_n;) {
+            for (int i = st.local_b; i < st.local_b + st.local_n;) {     // eligible steps hold no packs
                 const uint8_t *src = pieces[i].src;
                 uint8_t *dst = pieces[i].dst;
                 int64_t len = pieces[i].len;
-                for (++i; i < st.pre_b + st.pre_n && pieces[i].src == src + len && pieces[i].dst == dst + len; ++i)
+                for (++i; i < st.local_b + st.local_n && pieces[i].src == src + len && pieces[i].dst == dst + len; ++i)
                     len += pieces[i].len;
                 xfer[t - s].push_back({src, dst, len});
             }
@@ -729,7 +741,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant;
     p->d_pieces = nullptr; p->d_sb = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->d_disp = nullptr;
     p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
-    p->db = nullptr; p->epoch = 0; p->d_solo = nullptr;
+    p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false;
     // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
     // pieces for small launches were measured no faster, and slower where they stop
     // dividing the segment size (profiles/r01_min_pieces_ab.txt)
@@ -762,41 +774,19 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         return true;
     };
     p->steps.resize(dp->nsteps);
+    // pass 1: per step, what it holds and how it launches
     for (int s = 0; s < dp->nsteps; ++s) {
         const xg_stepplan &sp = dp->steps[s];
         StepR &st = p->steps[s];
-        if (sp.stage_count < 0 || sp.stage_count > sp.pre_count) goto bad;
-        st.stage_b = (int)pieces.size();
-        for (int i = 0; i < sp.stage_count; ++i)
-            if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
-        st.stage_n = (int)pieces.size() - st.stage_b;
-        st.stage_bytes = 0;
-        for (int i = st.stage_b; i < st.stage_b + st.stage_n; ++i) st.stage_bytes += pieces[i].len;
-        st.pre_b = (int)pieces.size();
-        st.local_bytes = st.pack_bytes = 0;
-        st.local_n = 0;
+        if (sp.stage_count < 0 || sp.stage_count > sp.pre_count || sp.post_count < 0) goto bad;
+        int nloc = 0, npack = 0;
         for (int i = sp.stage_count; i < sp.pre_count; ++i) {
-            const xg_copy &cp = dp->copies[sp.pre_begin + i];
-            const bool pack = cp.dst_buf == XG_BUF_STAGE_SEND;   // the plan lists local copies, then packs
-            const int before = (int)pieces.size();
-            if (!pack && st.pack_bytes) goto bad;
-            if (!add(cp, pack ? 0 : -1)) goto bad;
-            for (int k = before; k < (int)pieces.size(); ++k) (pack ? st.pack_bytes : st.local_bytes) += pieces[k].len;
-            if (!pack) st.local_n = (int)pieces.size() - st.pre_b;
+            const bool pack = dp->copies[sp.pre_begin + i].dst_buf == XG_BUF_STAGE_SEND;
+            if (!pack && npack) goto bad;                       // the plan lists local copies, then packs
+            (pack ? npack : nloc) += dp->copies[sp.pre_begin + i].len > 0;
         }
-        ds.close_group();
-        st.pre_n = (int)pieces.size() - st.pre_b;
-        if (!st.local_bytes) st.local_n = 0;
-        st.post_b = (int)pieces.size();
-        for (int i = 0; i < sp.post_count; ++i) {
-            const xg_copy &cp = dp->copies[sp.post_begin + i];
-            if (cp.src_buf != XG_BUF_STAGE_RECV) goto bad;       // post copies are unpacks
-            if (!add(cp, 1)) goto bad;
-        }
-        ds.close_group();
-        st.post_n = (int)pieces.size() - st.post_b;
-        st.post_bytes = 0;
-        for (int i = st.post_b; i < st.post_b + st.post_n; ++i) st.post_bytes += pieces[i].len;
+        for (int i = 0; i < sp.post_count; ++i)
+            if (dp->copies[sp.post_begin + i].src_buf != XG_BUF_STAGE_RECV) goto bad;   // post copies unpack
         st.p2p_b = (int)p->p2p.size();
         for (int i = 0; i < sp.p2p_count; ++i) {
             const xg_p2p &o = dp->p2p[sp.p2p_begin + i];
@@ -807,7 +797,61 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         }
         st.p2p_n = (int)p->p2p.size() - st.p2p_b;
         st.sync_after = sp.sync_after && c->nranks > 1;
-        st.split = st.p2p_n > 0 && st.local_n > 0;
+        st.split = c->split_local && st.p2p_n > 0 && nloc > 0;
+        st.deferred = false;
+        st.fused = c->fuse_unpack && s > 0 && npack > 0 && sp.stage_count == 0 && (st.split || nloc == 0) &&
+                   !p->steps[s - 1].sync_after && dp->steps[s - 1].post_count > 0;
+        if (st.fused) p->steps[s - 1].deferred = true;
+    }
+    // pass 2: the piece table, each launch's pieces contiguous (a fused launch: the
+    // previous step's unpacks, then this step's packs)
+    for (int s = 0; s < dp->nsteps; ++s) {
+        const xg_stepplan &sp = dp->steps[s];
+        StepR &st = p->steps[s];
+        auto span = [&](int b) {
+            int64_t n = 0;
+            for (int i = b; i < (int)pieces.size(); ++i) n += pieces[i].len;
+            return n;
+        };
+        auto add_post = [&](int t) -> bool {
+            const xg_stepplan &tp = dp->steps[t];
+            StepR &tt = p->steps[t];
+            tt.post_b = (int)pieces.size();
+            for (int i = 0; i < tp.post_count; ++i)
+                if (!add(dp->copies[tp.post_begin + i], 1)) return false;
+            ds.close_group();
+            tt.post_n = (int)pieces.size() - tt.post_b;
+            tt.post_bytes = span(tt.post_b);
+            return true;
+        };
+        st.stage_b = (int)pieces.size();
+        for (int i = 0; i < sp.stage_count; ++i)
+            if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
+        st.stage_n = (int)pieces.size() - st.stage_b;
+        st.stage_bytes = span(st.stage_b);
+        st.local_b = (int)pieces.size();
+        int first_pack = sp.pre_count;
+        for (int i = sp.stage_count; i < sp.pre_count; ++i) {
+            if (dp->copies[sp.pre_begin + i].dst_buf == XG_BUF_STAGE_SEND) {
+                first_pack = i;
+                break;
+            }
+            if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
+        }
+        st.local_n = (int)pieces.size() - st.local_b;
+        st.local_bytes = span(st.local_b);
+        if (st.fused && !add_post(s - 1)) goto bad;
+        st.pack_b = (int)pieces.size();
+        for (int i = first_pack; i < sp.pre_count; ++i)
+            if (!add(dp->copies[sp.pre_begin + i], 0)) goto bad;
+        ds.close_group();
+        st.pack_n = (int)pieces.size() - st.pack_b;
+        st.pack_bytes = span(st.pack_b);
+        st.pre_n = st.local_n + st.pack_n;
+        st.post_b = (int)pieces.size();
+        st.post_n = 0;
+        st.post_bytes = 0;
+        if (!st.deferred && !add_post(s)) goto bad;
     }
     p->npieces = (int)pieces.size();
     if (p->npieces) {
@@ -834,7 +878,8 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             p->nlaunch += p->segs[p->seg_of[s]].s0 == s;
             continue;
         }
-        p->nlaunch += (st.stage_n > 0) + (st.split ? 1 + (st.pre_n > st.local_n) : st.pre_n > 0) + (st.post_n > 0);
+        p->nlaunch += (st.stage_n > 0) + (st.split ? (st.local_n > 0) + (st.pack_n > 0 || st.fused) : st.pre_n > 0 || st.fused) +
+                      (st.post_n > 0 && !st.deferred);
     }
     *out = p;
     return XG_OK;
@@ -936,32 +981,40 @@ static int timed_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t strea
 
 // step part 1: stage copies, then local gather/scatter + packs.  A split step
 // forks its local part onto `side`, where it runs beside the packs and the RCCL
-// group on `stream`; enqueue_post joins it back before the step ends.
+// group on `stream`; enqueue_post joins it back before the step ends.  A fused
+// step's first launch also holds the previous step's unpacks: the previous step
+// ends with it (its event, when recording, goes right behind it), and the local
+// part forks after it, so no message of this step lands before one of the previous.
 static int enqueue_pre(xg_plan *p, int s, hipStream_t stream, hipStream_t side)
 {
     const StepR &st = p->steps[s];
     int rc;
     if (st.stage_n && (rc = timed_copy(p, st.stage_b, st.stage_n, st.stage_bytes, stream))) return rc;
+    if (st.fused) {
+        const StepR &pv = p->steps[s - 1];
+        if ((rc = timed_copy(p, pv.post_b, pv.post_n + st.pack_n, pv.post_bytes + st.pack_bytes, stream))) return rc;
+        if (p->rec_ev) HIPCHK(hipEventRecord(p->ev[s - 1], stream));
+    }
     if (st.split) {
         HIPCHK(hipEventRecord(p->fork[s], stream));
         HIPCHK(hipStreamWaitEvent(side, p->fork[s], 0));
-        if ((rc = timed_copy(p, st.pre_b, st.local_n, st.local_bytes, side))) return rc;
+        if ((rc = timed_copy(p, st.local_b, st.local_n, st.local_bytes, side))) return rc;
         HIPCHK(hipEventRecord(p->join[s], side));
-        if (st.pre_n > st.local_n &&
-            (rc = timed_copy(p, st.pre_b + st.local_n, st.pre_n - st.local_n, st.pack_bytes, stream)))
-            return rc;
-    } else if (st.pre_n && (rc = timed_copy(p, st.pre_b, st.pre_n, st.local_bytes + st.pack_bytes, stream))) {
+        if (!st.fused && st.pack_n && (rc = timed_copy(p, st.pack_b, st.pack_n, st.pack_bytes, stream))) return rc;
+    } else if (!st.fused && st.pre_n &&
+               (rc = timed_copy(p, st.local_b, st.pre_n, st.local_bytes + st.pack_bytes, stream))) {
         return rc;
     }
     return XG_OK;
 }
 
-// step part 3: unpack out of staging, then wait for the forked local part
+// step part 3: unpack out of staging (unless deferred into the next step's fused
+// launch), then wait for the forked local part
 static int enqueue_post(xg_plan *p, int s, hipStream_t stream)
 {
     const StepR &st = p->steps[s];
     int rc;
-    if (st.post_n && (rc = timed_copy(p, st.post_b, st.post_n, st.post_bytes, stream))) return rc;
+    if (st.post_n && !st.deferred && (rc = timed_copy(p, st.post_b, st.post_n, st.post_bytes, stream))) return rc;
     if (st.split) HIPCHK(hipStreamWaitEvent(stream, p->join[s], 0));
     return XG_OK;
 }
@@ -1113,18 +1166,24 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     if (p->db && !c->kt_mode) return run_armed(p, step_done, step_post, wall);
     const double t0 = xg_now();
     HIPCHK(hipEventRecord(p->ev0, c->stream));
+    p->rec_ev = true;
     for (int s = 0; s < p->nsteps;) {
         const double tp = xg_now();
         const int gi = p->seg_of[s];
         const int e = gi >= 0 ? p->segs[gi].s1 : s + 1;     // one launch posts a whole segment
-        if ((rc = enqueue_unit(p, s))) return rc;
-        HIPCHK(hipEventRecord(p->ev[e - 1], c->stream));
+        if ((rc = enqueue_unit(p, s))) {
+            p->rec_ev = false;
+            return rc;
+        }
+        // a deferred step's unpacks run in the next step's fused launch, which records its event
+        if (gi >= 0 || !p->steps[s].deferred) HIPCHK(hipEventRecord(p->ev[e - 1], c->stream));
         if (step_post) {
             step_post[s] = xg_now() - tp;
             for (int t = s + 1; t < e; ++t) step_post[t] = 0;
         }
         s = e;
     }
+    p->rec_ev = false;
     HIPCHK(hipStreamSynchronize(c->stream));
     if (wall) *wall = xg_now() - t0;
     if ((rc = xg_plan_check(p))) return rc;

@@ -467,8 +467,7 @@ class Regions:
 
     def close(self):
         if getattr(self, "_r", None):
-            if not self._shared:
-                _check(_dev.xg_regions_free(self._r), "xg_regions_free")
+            _check(_dev.xg_regions_free(self._r), "xg_regions_free")
             self._r = None
 
 

@@ -11,6 +11,7 @@ GPUs), so its launches overlap others.  Delivery is verified before the profiled
 repetitions."""
 import os
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -27,8 +28,12 @@ for m in (5, 8):
     bad = sum(sum(1 for b in r.verify()[1] if b) for r in runs)
     if bad:
         raise SystemExit("m%d: %d bad slots" % (m, bad))
+    t0 = time.perf_counter()
     for _ in range(REPS):
         xg.run_virtual(runs)
+    dt = (time.perf_counter() - t0) / REPS
+    print("m%d: %.1f us per virtual run (all %d GPUs' steps on one device), launches per run %d" % (
+        m, dt * 1e6, GPUS, sum(r.launches for r in runs)), flush=True)
     for r in runs:
         r.close()
     print("m%d ok: %d GPUs x %d reps, every cross-GPU segment packed" % (m, GPUS, REPS), flush=True)
