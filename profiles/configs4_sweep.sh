@@ -1,21 +1,16 @@
 #!/bin/bash
-# BASELINE configs[4] (P256 A64, half-sync m7 / m11 / m12, -c 1..8) through the drop-in CLI on
-# ONE MI355X at the largest -d it holds (8 MiB: 128 GiB SEND + 128 GiB RECV), every byte
-# verified (--verify), and the reference under MPICH on the box's host cores at a REDUCED
-# -d (64 KiB: 256 MPI processes on the box's CPU share are oversubscribed; labelled so).
-# usage: profiles/configs4_sweep.sh <outdir>
+# configs[4] -c sweep: the HIP path at -d 8 MiB (profiles/configs4_sweep.py) and the reference
+# under MPICH on the box's host cores at a REDUCED -d 64 KiB (1 TiB per direction does not fit a
+# host; 256 MPI processes share the box's CPUs, so these are oversubscribed -- labelled so).
 out=${1:-gpurun_out/configs4}; mkdir -p $out
-bin=$PWD/mpi-asynchronous-communication-test_amd/bin/test
-cd $out
-for c in 1 2 3 4 5 6 7 8; do
-  for m in 7 11 12; do
-    timeout -k 10 120 $bin --procs 256 --verify -a 64 -d 8388608 -c $c -m $m -i 1 -k 1 > gpu_m${m}_c$c.txt 2>> err.txt || exit 1
-  done
-done
-if [ -x ../../oracle/_ref/test ]; then
+timeout -k 10 300 python3 profiles/configs4_sweep.py > $out/gpu_d8m.txt 2> $out/gpu.err || exit 1
+if [ -x oracle/_ref/test ]; then
+  nproc > $out/host_cpus.txt
+  cd /tmp
   for c in 1 2 3 4 5 6 7 8; do
     for m in 7 11 12; do
-      timeout -k 10 120 /opt/conda/bin/mpiexec -launcher fork -n 256 ../../oracle/_ref/test -a 64 -d 65536 -c $c -m $m -i 1 -k 1 > ref_m${m}_c$c.txt 2>> ref.err || echo "reference m$m c$c failed or timed out" >> ref.err
+      timeout -k 5 60 /opt/conda/bin/mpiexec -launcher fork -n 256 $OLDPWD/oracle/_ref/test -a 64 -d 65536 -c $c -m $m -i 1 -k 1 \
+        > $OLDPWD/$out/ref_m${m}_c$c.txt 2>> $OLDPWD/$out/ref.err || echo "m$m c$c: no result (exit $?)" >> $OLDPWD/$out/ref.err
     done
   done
 fi
