@@ -129,7 +129,23 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_cu4;
 typedef __attribute__((address_space(1))) u32x4 g_u4;
 
-template <int U>
+// NT: non-temporal loads and stores (`nt`: streamed through the caches with an
+// early-eviction hint -- every byte of a copy is touched once)
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(g_cu4 *p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(g_u4 *p, u32x4 v)
+{
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int U, bool NT = false>
 __device__ __forceinline__ void pipelined_copy16(g_cu4 *__restrict__ s4, g_u4 *__restrict__ t4, int64_t n4)
 {
     int64_t i = threadIdx.x;
@@ -137,21 +153,21 @@ __device__ __forceinline__ void pipelined_copy16(g_cu4 *__restrict__ s4, g_u4 *_
     if (i + (U - 1) * (int64_t)kThreads < n4) {
         u32x4 cur[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = s4[i + u * kThreads];
+        for (int u = 0; u < U; ++u) cur[u] = ld16<NT>(s4 + i + u * kThreads);
         for (; i + step + (U - 1) * (int64_t)kThreads < n4; i += step) {
             u32x4 nxt[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) nxt[u] = s4[i + step + u * kThreads];
+            for (int u = 0; u < U; ++u) nxt[u] = ld16<NT>(s4 + i + step + u * kThreads);
 #pragma unroll
-            for (int u = 0; u < U; ++u) t4[i + u * kThreads] = cur[u];
+            for (int u = 0; u < U; ++u) st16<NT>(t4 + i + u * kThreads, cur[u]);
 #pragma unroll
             for (int u = 0; u < U; ++u) cur[u] = nxt[u];
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) t4[i + u * kThreads] = cur[u];
+        for (int u = 0; u < U; ++u) st16<NT>(t4 + i + u * kThreads, cur[u]);
         i += step;
     }
-    for (; i < n4; i += kThreads) t4[i] = s4[i];
+    for (; i < n4; i += kThreads) st16<NT>(t4 + i, ld16<NT>(s4 + i));
 }
 
 // Raw buffer access (gfx9 buffer resource, stride 0, num_records = bytes): a load
@@ -265,16 +281,16 @@ __device__ void realign_copy(const uint8_t *s, uint8_t *t, int64_t n, uint32_t (
 }
 
 // One workgroup per DCopy piece (<= the context's chunk bytes).  Variants:
-//   copy_kernel_g<U>       global loads/stores, U-deep software pipeline (round-1 default)
+//   copy_kernel_g<U, NT>   global loads/stores, U-deep software pipeline; NT: non-temporal
 //   copy_kernel_b<U, AUX>  the same through buffer resources, store policy AUX
 // Pieces whose pointers or length are not 16-B aligned take realign_copy.
-template <int U>
+template <int U, bool NT = false>
 __global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restrict__ pieces)
 {
     __shared__ uint32_t lds[2][kTileWords];
     const DCopy c = pieces[blockIdx.x];
     if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
-        pipelined_copy16<U>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
+        pipelined_copy16<U, NT>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
     else
         realign_copy(c.src, c.dst, c.len, lds);
 }

@@ -63,6 +63,7 @@ struct xg_ctx {
     int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
+    int64_t nt_min;         // variant 0: launches moving >= this many bytes use non-temporal loads/stores
     int engine_occ;            // co-resident step-engine workgroups the device admits (plan load caps W)
     // kernel timing session (xg_ktime_begin/end): 1 = an event pair around every
     // copy launch, 2 = one pair around the whole session on the main stream
@@ -213,6 +214,9 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
     env = getenv("XG_COPY_VARIANT");
     if (env) c->variant = atoi(env);
+    c->nt_min = 128 << 20;
+    env = getenv("XG_COPY_NT_MIN");
+    if (env) c->nt_min = atol(env);
     c->engine_max_step = 16 << 20;    // crossover vs one launch per step: profiles/r01_engine_sweep.txt
     env = getenv("XG_ENGINE_MAX_STEP");      // 0: never use the step engine
     if (env) c->engine_max_step = atol(env);
@@ -933,15 +937,21 @@ extern "C" int xg_plan_displs(const xg_plan *p, int64_t *out, int n)
     return XG_OK;
 }
 
-static int launch_copy(xg_plan *p, int b, int n, hipStream_t st)
+// Copy kernel per launch.  Variant 0 (default) picks by the launch's bytes: a launch
+// whose source + destination exceed the 256 MiB Infinity Cache streams through it with
+// non-temporal loads and stores (6.3 TB/s vs 5.5-5.6 plain from 256 MiB up), a smaller
+// one keeps the default policy, which re-runs serve from the cache
+// (profiles/r02/copy_nt_sizes.txt).  1..6 force one form (A/B, tests).
+static int launch_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t st)
 {
     const xgk::DCopy *pc = p->d_pieces + b;
-    switch (p->variant) {
-    case 1: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxPlain>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 2: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxSC1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 3: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 4: hipLaunchKernelGGL((xgk::copy_kernel_b<8, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 5: hipLaunchKernelGGL((xgk::copy_kernel_b<2, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    const int v = p->variant == 0 ? (bytes >= p->ctx->nt_min ? 6 : 1) : p->variant;
+    switch (v) {
+    case 2: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxPlain>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 3: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxSC1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 4: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 5: hipLaunchKernelGGL((xgk::copy_kernel_b<8, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 6: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     }
     HIPCHK(hipGetLastError());
@@ -975,7 +985,7 @@ static int timed_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t strea
     int rc;
     bool kt;
     if ((rc = kt_before(p->ctx, stream, &kt))) return rc;
-    if ((rc = launch_copy(p, b, n, stream))) return rc;
+    if ((rc = launch_copy(p, b, n, bytes, stream))) return rc;
     return kt_after(p->ctx, stream, kt, bytes);
 }
 

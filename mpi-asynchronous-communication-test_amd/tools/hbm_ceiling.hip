@@ -7,10 +7,16 @@
 //   kind 2  copy_kernel_b<4, sc1 stores> over 32 KiB pieces
 //   kind 3  read-only stream, 4096 workgroups (1 byte counted per byte)
 //   kind 4  write-only stream, 4096 workgroups (1 byte counted per byte)
+//   kind 5  hipMemcpyAsync device-to-device (the runtime's own copy)
+//   kind 6  grid-stride 16-B copy with non-temporal loads and stores, 2048 workgroups
+//   kind 7  one 256 KiB span per workgroup, 4 x 16-B loads in flight per lane
+//   kind 8  copy_kernel_g<4> over 64 KiB pieces
+//   kind 9  copy_kernel_g<4, nt> over 32 KiB pieces (non-temporal loads and stores)
 // *gbps = counted bytes / average launch time (a copy counts read + write).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../csrc/kernels.h"
@@ -41,6 +47,13 @@ __global__ __launch_bounds__(xgk::kThreads) void write_only(xgk::u32x4 *__restri
         t[i] = v;
 }
 
+__global__ __launch_bounds__(xgk::kThreads) void gridstride_copy_nt(const xgk::u32x4 *__restrict__ s,
+                                                                    xgk::u32x4 *__restrict__ t, int64_t n4)
+{
+    for (int64_t i = (int64_t)blockIdx.x * xgk::kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * xgk::kThreads)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), t + i);
+}
+
 }  // namespace
 
 #define CK(x)                                                                                             \
@@ -55,7 +68,7 @@ __global__ __launch_bounds__(xgk::kThreads) void write_only(xgk::u32x4 *__restri
 extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, double *gbps)
 {
     bytes &= ~(int64_t)32767;
-    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 4) return 3;
+    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 9) return 3;
     CK(hipSetDevice(device));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -65,8 +78,9 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipMalloc(&b, bytes));
     CK(hipMalloc(&sink, 4));
     CK(hipMemsetAsync(a, 1, bytes, st));
+    const int64_t piece = kind == 7 ? 262144 : (kind == 8 ? 65536 : 32768);
     std::vector<xgk::DCopy> pieces;
-    for (int64_t o = 0; o < bytes; o += 32768) pieces.push_back({a + o, b + o, 32768});
+    for (int64_t o = 0; o < bytes; o += piece) pieces.push_back({a + o, b + o, std::min<int64_t>(piece, bytes - o)});
     xgk::DCopy *dp;
     CK(hipMalloc(&dp, sizeof(xgk::DCopy) * pieces.size()));
     CK(hipMemcpy(dp, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
@@ -85,7 +99,12 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
                 break;
         case 3: hipLaunchKernelGGL(read_only, dim3(4096), dim3(xgk::kThreads), 0, st, (const xgk::u32x4 *)a, n4, sink);
                 break;
-        default: hipLaunchKernelGGL(write_only, dim3(4096), dim3(xgk::kThreads), 0, st, (xgk::u32x4 *)b, n4); break;
+        case 4: hipLaunchKernelGGL(write_only, dim3(4096), dim3(xgk::kThreads), 0, st, (xgk::u32x4 *)b, n4); break;
+        case 5: CK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, st)); break;
+        case 6: hipLaunchKernelGGL(gridstride_copy_nt, dim3(2048), dim3(xgk::kThreads), 0, st, (const xgk::u32x4 *)a,
+                                   (xgk::u32x4 *)b, n4); break;
+        case 9: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
         }
         CK(hipGetLastError());
     }
@@ -93,7 +112,7 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    *gbps = (kind >= 3 ? 1.0 : 2.0) * (double)bytes * reps / (ms * 1e-3) / 1e9;
+    *gbps = (kind == 3 || kind == 4 ? 1.0 : 2.0) * (double)bytes * reps / (ms * 1e-3) / 1e9;
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
     CK(hipFree(a));

@@ -7,9 +7,13 @@ import os
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 lib = C.CDLL(os.path.join(HERE, "mpi-asynchronous-communication-test_amd", "tools", "lib", "libxgtools.so"))
 lib.xgt_copy_ceiling.argtypes = [C.c_int, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_double)]
-names = {0: "grid-stride copy", 1: "copy_kernel_g<4>", 2: "copy_kernel_b<4,sc1>", 3: "read-only", 4: "write-only"}
-for nb in (448 << 20, 1 << 30, 4 << 30):
-    for kind in range(5):
+names = {0: "grid-stride copy", 1: "copy_kernel_g<4> 32K", 2: "copy_kernel_b<4,sc1>", 3: "read-only", 4: "write-only",
+         5: "hipMemcpy DtoD", 6: "grid-stride copy nt", 7: "copy_kernel_g<4> 256K", 8: "copy_kernel_g<4> 64K",
+         9: "copy_kernel_g<4,nt> 32K"}
+kinds = [int(k) for k in os.environ.get("KINDS", "0,1,2,3,4,5,6,7,8,9").split(",")]
+sizes = [int(x) << 20 for x in os.environ.get("SIZES_MIB", "448,1024,4096").split(",")]
+for nb in sizes:
+    for kind in kinds:
         g = C.c_double()
         assert lib.xgt_copy_ceiling(0, nb, kind, 20, C.byref(g)) == 0
         print("bytes=%d %-22s %.1f GB/s" % (nb, names[kind], g.value), flush=True)

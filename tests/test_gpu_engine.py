@@ -189,7 +189,7 @@ def test_random_plans_engine_and_launches(xg, ctx, seed, align):
         eager.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_copy_variants_every_phase(xg, variant):
     """Every copy-kernel variant moves pieces at every (source, destination) phase mod
     16 and lengths around the 4 KiB tile, byte-exact (misaligned ones through LDS)."""
