@@ -1,0 +1,75 @@
+"""bench.py's N > 1 control flow on the CPU, against a fake device layer (tests/fake_xg.py)
+with the REAL host scheduler: per-method direct-vs-packed tuning, the per-launch roofline
+pass, the xGMI object, the JSON line -- the code path only the driver's multi-GPU run
+executes on hardware, checked here for crashes and for the line's schema."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+DRIVER = r'''
+import os, sys, json
+sys.path.insert(0, {repo!r}); sys.path.insert(0, os.path.join({repo!r}, "tests"))
+import __graft_entry__ as G
+import fake_xg
+real = G.load_package()
+fx = fake_xg.install(real)
+sys.argv = ["bench.py"] + {argv!r}
+import bench
+rc = bench.main()
+print("CALLS " + json.dumps({{"p2p": fx.calls["p2p_bench"], "ktime": fx.calls["ktime"], "runs": fx.calls["runs"]}}))
+sys.exit(rc)
+'''
+
+
+def _run(world, rank, argv, tmp_path):
+    env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+               XG_RDZV_KEY="logic_%s_%d" % (tmp_path.name, world))
+    code = DRIVER.format(repo=REPO, argv=argv)
+    return subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_multi_gpu_rank0_line(world, tmp_path):
+    p = _run(world, 0, ["--gpus", str(world), "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], tmp_path)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "xgmi", "cpu_baseline"):
+        assert key in out, key
+    assert out["n_gpus"] == world and out["steps"] == 3 and out["unit"] == "GB/s"
+    assert out["xgmi"]["peak"] > 0 and out["xgmi"]["cross_gpu_bytes_per_step"] > 0
+    assert out["roofline"] and out["roofline"]["bound"] == "hbm"
+    assert set(out["pack_autotune_ms_per_run"]) == {"1", "2", "3", "4"}
+    calls = json.loads([l for l in p.stdout.splitlines() if l.startswith("CALLS ")][0][6:])
+    assert calls["p2p"] == 1
+    assert calls["ktime"] and calls["ktime"][0][1] is True      # N > 1: per-launch roofline pass
+
+
+def test_bench_multi_gpu_other_rank(tmp_path):
+    """a non-zero rank waits for rank 0's RCCL id, runs everything, prints nothing"""
+    key = "logic_%s_%d" % (tmp_path.name, 4)
+    with open("/tmp/xg_bench_rdzv_%s.bin" % key, "wb") as f:
+        f.write(b"\x02" * 128)
+    try:
+        p = _run(4, 3, ["--gpus", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"], tmp_path)
+    finally:
+        if os.path.exists("/tmp/xg_bench_rdzv_%s.bin" % key):
+            os.unlink("/tmp/xg_bench_rdzv_%s.bin" % key)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_single_gpu_line(tmp_path):
+    p = _run(1, 0, ["--steps", "2", "--warmup", "1", "--no-cpu-baseline"], tmp_path)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert out["n_gpus"] == 1 and out["xgmi"] is None
+    assert out["roofline"]["measured"].startswith("one HIP event pair")
+    assert out["roofline"]["avg_launch_us"] * out["roofline"]["launches_per_step"] <= out["ms_per_step"] * 1e3 * 1.001
