@@ -110,10 +110,15 @@ int xg_plan_check(xg_plan *p);
  * barrier, no unpack, each <= XG_ENGINE_MAX_STEP bytes; 0 = off) is ONE persistent
  * launch of up to one workgroup per CU (XG_ENGINE_WG lowers it), grid barrier +
  * wall-clock stamp per step; the other steps are their own launches.
+ * Small hazard-free segments run on the solo engine instead: each step's pieces
+ * dealt over up to XG_SOLO_RAILS (default 8) workgroups that each keep the step
+ * order with workgroup barriers and never wait for one another.
  * xg_plan_engine: workgroups of the first such segment (0: none);
+ * xg_plan_engine_rails: rails of the first solo segment (0: none);
  * xg_plan_engine_steps: steps inside segments (*nseg segments, *nhaz hazard
  * barriers, xg_engine_hazards); XG_ENGINE_DRAIN=1 drains every step's stores. */
 int xg_plan_engine(const xg_plan *p);
+int xg_plan_engine_rails(const xg_plan *p);
 int xg_plan_engine_steps(const xg_plan *p, int *nseg, int *nhaz);
 /* Kernel launches of one run (copy + engine launches; RCCL's own kernels aside). */
 int xg_plan_launches(const xg_plan *p);

@@ -336,7 +336,8 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_b(const DCopy *__restric
 struct EngineState {
     unsigned count;     // arrival tickets, cumulative over every launch of the plan
     unsigned tmo;       // != 0: some workgroup gave up waiting
-    unsigned pad[2];
+    unsigned rails;     // solo engine, armed: rails finished (cumulative; the last of a launch rings `done`)
+    unsigned pad;
 };
 
 template <int B>
@@ -499,24 +500,30 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
 
 // ---------------------------------------------------------------- solo engine
 // The same plans when they are small (README-sized latency chains: tens of steps
-// of tens of KiB): ONE workgroup of 16 waves runs every step, so the step
-// boundary is a workgroup barrier (tens of ns) instead of a grid barrier across
-// CUs (~1 us of device-scope atomics and polling).  The plan is cut into rows of
-// 16 pieces of <= 1 KiB, piece (row, w) moved by wave w (64 lanes x 16 B); a
-// step's pieces are padded to whole rows.  K rows are loaded at once (every
-// lane has K 16-B loads in flight, 16 x K KiB per workgroup) and stored in
-// order, with a barrier + wall-clock stamp wherever a step ends: the loads of
+// of tens of KiB): workgroups of 16 waves -- RAILS -- each run every step on their
+// own CU, so the step boundary is a workgroup barrier (tens of ns) instead of a
+// grid barrier across CUs (~1 us of device-scope atomics and polling).  The host
+// deals each step's 1 KiB pieces round-robin over the rails (a message striped
+// over R links, as a multi-rail network does); rail r cuts its share into rows of
+// 16 pieces, piece (row, w) moved by wave w (64 lanes x 16 B), rows packed back to
+// back across steps.  K rows are loaded at once (every lane has K 16-B loads in
+// flight, 16 x K KiB per workgroup) and stored in order, with a barrier + wall-
+// clock stamp wherever a step that had pieces on this rail ends: the loads of
 // later steps run ahead of the stores of earlier ones -- valid because no step
 // reads what another writes (the host uses this engine only for plans without
-// hazard points, xg_engine_hazards) -- while stores keep the step order.  Like
-// flag 0 of the grid engine, a step's stamp is the time its stores were issued;
-// the last step waits for its stores (delivered time).
+// hazard points, xg_engine_hazards) -- while each rail's stores keep the step
+// order.  Rails never wait for each other: step s is over when every rail has
+// closed it, so its time is the MAX over rails of their stamps for it (a rail with
+// nothing in step s carries its previous stamp; the host reduces).  Like flag 0 of
+// the grid engine a stamp is the time the stores were issued; the last step waits
+// for its stores (delivered time).  One CU moves ~120 GB/s of load + store
+// traffic, so R rails lift the single-workgroup bound R-fold.
 constexpr int kSoloWaves = 16;
 constexpr int kSoloThreads = kSoloWaves * 64;
 constexpr int kSoloPiece = 64 * 16;              // bytes per wave per row
 constexpr int kSoloK = 8;                        // rows per chunk (2 chunks x 8 x 16 KiB in flight)
 constexpr int kSoloMaxSteps = 2048;              // stamps kept in LDS (16 KiB)
-constexpr int kSoloMaxPieces = 4608;             // descriptors kept in LDS (4608 x 24 B = 108 KiB)
+constexpr int kSoloMaxPieces = 4608;             // descriptors per rail kept in LDS (36 KiB)
 
 // One solo piece in 64 bits: source and destination offsets (16-B units, 24 bits)
 // from the segment's two base pointers, the length (16-B units, <= 64, 7 bits) and
@@ -530,16 +537,20 @@ __host__ __device__ constexpr unsigned long long solo_desc(uint64_t src16, uint6
     return src16 | (dst16 << 24) | (len16 << 48) | (before << 55);
 }
 constexpr uint64_t kSoloOffMax = 1ull << 24;     // offsets < 256 MiB from the bases
+constexpr int kSoloMaxRails = 16;
 
-// Host contract (build_segments): every piece 16-B aligned, <= 1 KiB, within 256 MiB
-// of the bases; row_close[r] = step barriers inside or in front of row r (rows + 1
-// entries), each piece's `before` field saying where it sits among them;
-// rows form an even number of chunks of K plus one spare empty chunk;
-// nsteps <= kSoloMaxSteps; pieces <= kSoloMaxPieces.  The descriptor table is
-// staged into LDS before the doorbell (plan set-up: no payload byte moves before
-// the ring), read back a chunk at a time in one batch; each piece becomes a
-// buffer resource whose range check drops the lanes past its end (an empty
-// padding piece moves nothing), so the body has no branch but the step barriers.
+// Host contract (build_segments), per rail r of R = gridDim.x: pieces
+// desc[r * npieces ..], every piece 16-B aligned, <= 1 KiB, within 256 MiB of the
+// bases; rows form an even number of chunks of K plus one spare empty chunk;
+// meta = [R][nrows + 1] row_close (step barriers inside or in front of row r, each
+// piece's `before` saying where it sits among them), then [R][nsteps] the step
+// each barrier closes, in order (-1 past the last); nsteps <= kSoloMaxSteps;
+// npieces <= kSoloMaxPieces.  The descriptor table is staged into LDS before the
+// doorbell (plan set-up: no payload byte moves before the ring), read back a chunk
+// at a time in one batch; each piece becomes a buffer resource whose range check
+// drops the lanes past its end (an empty padding piece moves nothing), so the body
+// has no branch but the step barriers.  stamps[r * stride + t]: rail r's stamp of
+// step t, 0 where it closed nothing (the host carries and reduces).
 template <int K>
 struct SoloChunk {
     unsigned long long d[K];
@@ -565,18 +576,18 @@ __device__ __forceinline__ void solo_load(SoloChunk<K> &b, const unsigned long l
     }
 }
 
-// close the next step: every wave has issued its stores of it; stamp
-__device__ __forceinline__ void solo_close(unsigned long long *ts, int &s)
+// barrier k of this rail: every wave has issued its stores of the step it closes; stamp it
+__device__ __forceinline__ void solo_close(unsigned long long *ts, const short *lcstep, int &k)
 {
     __syncthreads();
-    if (threadIdx.x == 0) ts[s] = (unsigned long long)wall_clock64();
-    ++s;
+    if (threadIdx.x == 0) ts[lcstep[k]] = (unsigned long long)wall_clock64();
+    ++k;
 }
 
 // store chunk c in row order; a row that begins new steps first closes the ones before
 // it: barrier (every wave issued their stores), stamp
 template <int K>
-__device__ __forceinline__ void solo_store(const SoloChunk<K> &b, const unsigned short *lclose,
+__device__ __forceinline__ void solo_store(const SoloChunk<K> &b, const unsigned short *lclose, const short *lcstep,
                                           unsigned long long *ts, int &s, int c, uint64_t l16, uint8_t *dst_base)
 {
 #pragma unroll
@@ -584,34 +595,42 @@ __device__ __forceinline__ void solo_store(const SoloChunk<K> &b, const unsigned
         const int n = __builtin_amdgcn_readfirstlane((int)lclose[c * K + k]);     // barriers in this row
         const int bf = __builtin_amdgcn_readfirstlane((int)(b.d[k] >> 55));      // ... before my piece
         int j = 0;
-        for (; j < bf; ++j) solo_close(ts, s);
+        for (; j < bf; ++j) solo_close(ts, lcstep, s);
         asm volatile("" ::: "memory");        // the store stays between its steps' barriers
         const unsigned long long d = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(b.d[k] >> 32)) << 32) |
                                      (unsigned)__builtin_amdgcn_readfirstlane((int)b.d[k]);
         const brsrc r = make_rsrc(dst_base + (((d >> 24) & (kSoloOffMax - 1)) << 4), (int64_t)((d >> 48) & 127) << 4);
         bstore16(r, (int)l16 * 16, b.v[k]);
         asm volatile("" ::: "memory");
-        for (; j < n; ++j) solo_close(ts, s);
+        for (; j < n; ++j) solo_close(ts, lcstep, s);
     }
 }
 
 template <int K>
 __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigned long long *__restrict__ desc,
                                                                    int npieces, const uint8_t *src_base,
-                                                                   uint8_t *dst_base,
-                                                                   const int *__restrict__ row_close, int nsteps,
-                                                                   EngineState *st,
-                                                                   unsigned long long *stamps, Doorbell *db,
-                                                                   unsigned epoch)
+                                                                   uint8_t *dst_base, const int *__restrict__ meta,
+                                                                   int nsteps, EngineState *st,
+                                                                   unsigned long long *stamps, int stride,
+                                                                   Doorbell *db, unsigned epoch)
 {
     const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    const int rail = (int)blockIdx.x, R = (int)gridDim.x;
     __shared__ unsigned long long ldesc[kSoloMaxPieces];
     __shared__ unsigned short lclose[kSoloMaxPieces / kSoloWaves + 1];
+    __shared__ short lcstep[kSoloMaxSteps];
     __shared__ unsigned long long ts[kSoloMaxSteps];
     __shared__ int give_up;
     const int nrows = npieces / kSoloWaves;
+    desc += (size_t)rail * npieces;
+    const int *row_close = meta + rail * (nrows + 1);
+    const int *cstep = meta + R * (nrows + 1) + rail * nsteps;
     for (int i = (int)threadIdx.x; i < npieces; i += kSoloThreads) ldesc[i] = desc[i];
     for (int i = (int)threadIdx.x; i <= nrows; i += kSoloThreads) lclose[i] = (unsigned short)row_close[i];
+    for (int i = (int)threadIdx.x; i < nsteps; i += kSoloThreads) {
+        lcstep[i] = (short)cstep[i];
+        ts[i] = 0;
+    }
     if (threadIdx.x == 0) give_up = db && !wait_ring(db, epoch);
     __syncthreads();
     if (give_up) {
@@ -627,26 +646,27 @@ __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigne
     // below is unconditional (a conditional one would make the compiler wait on it).
     const int nchunks = nrows / K - 1;
     SoloChunk<K> A, B;
-    int s = 0;
+    int k = 0;
     solo_load<K>(A, ldesc, 0, wave, l16, src_base);
     for (int c = 0; c < nchunks; c += 2) {
         solo_load<K>(B, ldesc, c + 1, wave, l16, src_base);
-        solo_store<K>(A, lclose, ts, s, c, l16, dst_base);
+        solo_store<K>(A, lclose, lcstep, ts, k, c, l16, dst_base);
         solo_load<K>(A, ldesc, c + 2, wave, l16, src_base);
-        solo_store<K>(B, lclose, ts, s, c + 1, l16, dst_base);
+        solo_store<K>(B, lclose, lcstep, ts, k, c + 1, l16, dst_base);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last steps: delivered
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this rail's last steps: delivered
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long t = (unsigned long long)wall_clock64();
-        for (; s < nsteps; ++s) ts[s] = t;
+        for (int s = k > 0 ? lcstep[k - 1] + 1 : 0; s < nsteps; ++s) ts[s] = t;
+        if (db) {      // the last rail to finish tells the host
+            const unsigned done = __hip_atomic_fetch_add((g_u32 *)&st->rails, 1u, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) + 1;
+            if (done % (unsigned)R == 0) ring_done(db, epoch);
+        }
     }
     __syncthreads();
-    for (int i = (int)threadIdx.x; i < nsteps; i += kSoloThreads) stamps[i] = ts[i];
-    if (db && threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        ring_done(db, epoch);
-    }
+    for (int i = (int)threadIdx.x; i < nsteps; i += kSoloThreads) stamps[(size_t)rail * stride + i] = ts[i];
 }
 
 // ---------------------------------------------------------------- displacement scan

@@ -56,8 +56,9 @@ struct xg_ctx {
     int64_t engine_max_step;   // GPU-local plans whose largest step moves <= this many bytes use the step engine
     int engine_wmax;           // at most this many (co-resident) engine workgroups
     int engine_drain;          // 1: always drain before each barrier arrival (XG_ENGINE_DRAIN=1)
-    int64_t solo_step;         // hazard-free segments averaging <= this many bytes per step run solo
-    int64_t solo_max;          // ... and moving <= this many bytes in all
+    int solo;                  // 0: never use the solo engine
+    int64_t solo_max;          // solo segments move <= this many bytes per run
+    int solo_rails;            // solo segments deal their pieces over up to this many workgroups
     int engine_arm;            // 1: xg_plan_run arms single-segment plans (doorbell)
     int split_local;           // 1: a cross-GPU step's local gather runs on the side stream
     int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
@@ -101,11 +102,13 @@ struct EngSeg {
     int s0, s1;                    // steps [s0, s1)
     int w, b;                      // workgroups; 16-B loads per lane per unit (1, 4, 16)
     int sb_off;                    // its block in d_sb: (n + 1) unit offsets, then n flags
-                                   // (solo: n + 1 row offsets)
+                                   // (solo: per rail nrows + 1 row barrier counts, then per rail
+                                   // n closed-step indices)
     int nhaz;                      // hazard points (xg_engine_hazards flag 2)
     bool solo;                     // one workgroup (solo_engine_kernel), pieces from u0
     int u0;                        // first unit / piece of the segment in d_epieces
-    int npieces;                   // solo: pieces (whole chunks of rows), from u0 in d_solo
+    int npieces;                   // solo: pieces per rail (whole chunks of rows), rail r's from u0 + r * npieces
+                                   // in d_solo; w = rails
     const uint8_t *sbase;          // solo: base pointers of the descriptors' offsets
     uint8_t *dbase;
     int64_t bytes;                 // bytes copied per run
@@ -128,7 +131,9 @@ struct xg_plan {
     std::vector<EngSeg> segs;
     int *d_sb;
     xgk::DCopy *d_epieces;         // every segment's work units, step-major
-    xgk::EngineState *d_engine;    // state (16 B, zeroed at load) followed by nsteps stamps
+    xgk::EngineState *d_engine;    // state (16 B, zeroed at load) followed by stamps: rail r's of step
+                                   // s at [r * nsteps + s] (grid segments: rail 0)
+    int stamp_rails;               // rails the stamp area holds
     unsigned engine_base;          // barrier tickets taken by earlier launches (wraps)
     bool engine_reset;             // zero the state before the next launch
     xgk::Doorbell *db;             // host-pinned doorbell of armed runs (single-segment plans), or null
@@ -236,12 +241,14 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     }
     env = getenv("XG_ENGINE_DRAIN");         // "1": drain every step even without a hazard
     c->engine_drain = env && !strcmp(env, "1");
-    c->solo_step = 64 << 10;          // see DESIGN.md (solo engine) for the measured crossover
-    c->solo_max = 8 << 20;
-    env = getenv("XG_ENGINE_SOLO_STEP");     // 0: never solo
-    if (env) c->solo_step = atol(env);
+    env = getenv("XG_ENGINE_SOLO");          // "0": never solo (the grid engine runs every segment)
+    c->solo = !(env && !strcmp(env, "0"));
+    c->solo_max = 32 << 20;
     env = getenv("XG_ENGINE_SOLO_MAX");
     if (env) c->solo_max = atol(env);
+    c->solo_rails = 8;                // see DESIGN.md (solo engine): one rail per XCD
+    env = getenv("XG_SOLO_RAILS");
+    if (env && atoi(env) > 0) c->solo_rails = std::min(atoi(env), xgk::kSoloMaxRails);
     env = getenv("XG_ENGINE_ARM");           // "0": launch latency inside the timed region
     c->engine_arm = !(env && !strcmp(env, "0"));
     env = getenv("XG_SPLIT_LOCAL");          // "0": local gather + packs in one launch
@@ -515,6 +522,20 @@ static bool engine_step(const xg_ctx *c, const StepR &st)
 // over up to one workgroup per CU with bytes enough in flight
 // (profiles/r01_engine_sweep.txt: small units starve big steps, big units leave
 // small steps on a handful of workgroups).  Barrier flags: xg_engine_hazards.
+// Solo or grid engine for a hazard-free segment of n steps (`busy` of them move
+// bytes) moving `bytes`: the cheaper by a model of the measured costs (MI355X,
+// profiles/r02/solo_probe_steps.txt, rails.txt): a rail (one CU) moves ~120 GB/s of
+// load + store traffic and closes a step in ~0.2 us; the grid engine moves at the
+// copy kernels' ~5 TB/s but pays ~1 us of device-scope barrier per step; a lone
+// busy step outside the engine is a copy launch inside the timed region (~8 us).
+static bool solo_pays(int64_t bytes, int n, int rails, int busy)
+{
+    const double traffic = 2.0 * (double)bytes;
+    const double solo = traffic / (rails * 120e9) + n * 0.2e-6;
+    const double grid = traffic / 5e12 + n * 1.0e-6 + (busy < 2 ? 8e-6 : 0.0);
+    return solo < grid;
+}
+
 static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
 {
     xg_ctx *c = p->ctx;
@@ -524,6 +545,7 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
     std::vector<int> sb;
     for (int s = 0; s < p->nsteps;) {
         int e = s;
+        const int s_run = s;
         while (e < p->nsteps && engine_step(c, p->steps[e])) ++e;
         // steps where this GPU copies nothing cost nothing as their own "launches": trim
         // them off both ends, and keep the run only if >= 2 steps copy something
@@ -532,7 +554,9 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         while (s < e && !p->steps[s].pre_n) ++s;
         while (e > s && !p->steps[e - 1].pre_n) --e;
         for (int t = s; t < e; ++t) busy += p->steps[t].pre_n > 0;
-        if (busy < 2) {
+        // one busy step is worth an (armed) engine launch only as the whole plan
+        const bool whole = s_run == 0 && run_end == p->nsteps && c->engine_arm && !c->virt;
+        if (busy < (whole ? 1 : 2)) {
             s = run_end > s ? run_end : s + 1;
             continue;
         }
@@ -580,15 +604,16 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         for (const auto &xs : xfer)
             for (const xgk::DCopy &x : xs)
                 aligned = aligned && ((((uintptr_t)x.src | (uintptr_t)x.dst | (uint64_t)x.len) & 15) == 0);
-        // solo: rows of kSoloWaves pieces of <= 1 KiB, each step padded to whole rows, the
-        // segment to whole chunks of kSoloK rows; padding pieces (len 0) move nothing
-        int64_t solo_pieces = 0;
+        // solo: each step's 1 KiB pieces dealt round-robin over R rails; per rail, rows of
+        // kSoloWaves pieces, whole chunks of kSoloK rows, an even number of them, plus the
+        // spare chunk the double-buffered loop prefetches past the end
+        int64_t total_pieces = 0;
         for (const auto &xs : xfer)
-            for (const xgk::DCopy &x : xs) solo_pieces += (x.len + xgk::kSoloPiece - 1) / xgk::kSoloPiece;
-        // whole chunks of kSoloK rows, an even number of them, plus the spare chunk the
-        // double-buffered loop prefetches past the end
+            for (const xgk::DCopy &x : xs) total_pieces += (x.len + xgk::kSoloPiece - 1) / xgk::kSoloPiece;
+        const int rails = (int)std::max<int64_t>(1, std::min<int64_t>(c->solo_rails, total_pieces / xgk::kSoloWaves));
         const int64_t chunk_pieces = (int64_t)xgk::kSoloWaves * xgk::kSoloK;
-        solo_pieces = ((solo_pieces + 2 * chunk_pieces - 1) / (2 * chunk_pieces) * 2 + 1) * chunk_pieces;
+        const int64_t per_rail = (total_pieces + rails - 1) / rails + n;     // + a row break per step at most
+        const int64_t solo_pieces = ((per_rail + 2 * chunk_pieces - 1) / (2 * chunk_pieces) * 2 + 1) * chunk_pieces;
         // the segment's source and destination base pointers (solo descriptors are offsets)
         uintptr_t slo = UINTPTR_MAX, shi = 0, dlo = UINTPTR_MAX, dhi = 0;
         for (const auto &xs : xfer)
@@ -599,40 +624,64 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
                 }
         const bool near = shi > slo && dhi > dlo && (shi - slo) / 16 < xgk::kSoloOffMax && (dhi - dlo) / 16 < xgk::kSoloOffMax;
         g.solo = g.nhaz == 0 && aligned && near && n <= xgk::kSoloMaxSteps && solo_pieces <= xgk::kSoloMaxPieces &&
-                 c->solo_step > 0 && g.bytes <= c->solo_max && g.bytes <= c->solo_step * n;
+                 c->solo && g.bytes <= c->solo_max && solo_pays(g.bytes, n, rails, busy);
+        if (!g.solo && busy < 2) {      // one busy step: an engine launch only if it runs solo
+            ep.resize(u0);
+            s = run_end;
+            continue;
+        }
         if (g.solo) {
             g.sbase = (const uint8_t *)slo;
             g.dbase = (uint8_t *)dlo;
             ep.resize(u0);
             g.u0 = (int)p->solo_desc.size();
-            g.w = 1;
-            std::vector<unsigned long long> &sd = p->solo_desc;
-            const size_t d0 = sd.size();
-            std::vector<int64_t> pend(n);          // first piece after step t (its closing barrier)
+            g.w = rails;
+            // deal: per rail its pieces in step order and, per step it has pieces in, the
+            // barrier closing that step in front of its next piece
+            std::vector<std::vector<unsigned long long>> rp(rails);
+            std::vector<std::vector<std::pair<int64_t, int>>> bar(rails);   // (in front of piece, step)
+            int cur = 0;
             for (int t = 0; t < n; ++t) {
+                std::vector<char> used(rails, 0);
                 for (const xgk::DCopy &x : xfer[t])
-                    for (int64_t o = 0; o < x.len; o += xgk::kSoloPiece)
-                        sd.push_back(xgk::solo_desc(((uintptr_t)x.src + o - slo) / 16, ((uintptr_t)x.dst + o - dlo) / 16,
-                                                    std::min<int64_t>(x.len - o, xgk::kSoloPiece) / 16, 0));
-                pend[t] = (int64_t)(sd.size() - d0);
+                    for (int64_t o = 0; o < x.len; o += xgk::kSoloPiece) {
+                        rp[cur].push_back(xgk::solo_desc(((uintptr_t)x.src + o - slo) / 16, ((uintptr_t)x.dst + o - dlo) / 16,
+                                                         std::min<int64_t>(x.len - o, xgk::kSoloPiece) / 16, 0));
+                        used[cur] = 1;
+                        cur = (cur + 1) % rails;
+                    }
+                for (int r = 0; r < rails; ++r)
+                    if (used[r]) bar[r].push_back({(int64_t)rp[r].size(), t});
             }
-            const int64_t real = (int64_t)(sd.size() - d0);
-            while ((sd.size() - d0) % (2 * chunk_pieces)) sd.push_back(0);
-            sd.insert(sd.end(), chunk_pieces, 0ull);
-            g.npieces = (int)(sd.size() - d0);
-            // the barrier closing step t sits in front of piece pend[t]: in its row, and
-            // before the pieces at or after its column; steps ending with the last piece
-            // close after the loop
-            std::vector<int> close(g.npieces / xgk::kSoloWaves + 1, 0);
-            for (int t = 0; t < n; ++t) {
-                if (pend[t] >= real) continue;
-                const int64_t row = pend[t] / xgk::kSoloWaves, col = pend[t] % xgk::kSoloWaves;
-                close[row]++;
-                for (int64_t w = col; w < xgk::kSoloWaves; ++w) sd[d0 + row * xgk::kSoloWaves + w] += 1ull << 55;
+            int64_t longest = 0;
+            for (int r = 0; r < rails; ++r) longest = std::max<int64_t>(longest, (int64_t)rp[r].size());
+            g.npieces = (int)(((longest + 2 * chunk_pieces - 1) / (2 * chunk_pieces) * 2 + 1) * chunk_pieces);
+            if (g.npieces > xgk::kSoloMaxPieces) return XG_EARG;      // cannot happen: per_rail bounds it
+            const int nrows = g.npieces / xgk::kSoloWaves;
+            std::vector<unsigned long long> &sd = p->solo_desc;
+            std::vector<int> meta((size_t)rails * (nrows + 1) + (size_t)rails * n, -1);
+            for (int r = 0; r < rails; ++r) {
+                const size_t d0 = sd.size();
+                const int64_t real = (int64_t)rp[r].size();
+                sd.insert(sd.end(), rp[r].begin(), rp[r].end());
+                sd.resize(d0 + g.npieces, 0ull);
+                // a barrier in front of piece i sits in its row, before the pieces at or
+                // after its column; those in front of the end close after the loop
+                int* close = &meta[(size_t)r * (nrows + 1)];
+                std::fill(close, close + nrows + 1, 0);
+                int* cs = &meta[(size_t)rails * (nrows + 1) + (size_t)r * n];
+                int nb = 0;
+                for (const auto &bt : bar[r]) {
+                    if (bt.first >= real) continue;
+                    const int64_t row = bt.first / xgk::kSoloWaves, col = bt.first % xgk::kSoloWaves;
+                    close[row]++;
+                    cs[nb++] = bt.second;
+                    for (int64_t w = col; w < xgk::kSoloWaves; ++w) sd[d0 + row * xgk::kSoloWaves + w] += 1ull << 55;
+                }
+                for (size_t i = d0; i < sd.size(); ++i)
+                    if ((sd[i] >> 55) > 31) return XG_EARG;      // cannot happen: <= 16 per row
             }
-            for (size_t i = d0; i < sd.size(); ++i)
-                if ((sd[i] >> 55) > 31) return XG_EARG;      // cannot happen: <= 16 per row
-            sb.insert(sb.end(), close.begin(), close.end());
+            sb.insert(sb.end(), meta.begin(), meta.end());
         } else {
             g.npieces = 0;
             g.u0 = 0;
@@ -655,8 +704,12 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         HIPCHK(hipMalloc(&p->d_solo, nb));
         HIPCHK(hipMemcpy(p->d_solo, p->solo_desc.data(), nb, hipMemcpyHostToDevice));
     }
-    HIPCHK(hipMalloc(&p->d_engine, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps));
-    HIPCHK(hipMemset(p->d_engine, 0, sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps));
+    p->stamp_rails = 1;
+    for (const EngSeg &g : p->segs)
+        if (g.solo) p->stamp_rails = std::max(p->stamp_rails, g.w);
+    const size_t eb = sizeof(xgk::EngineState) + 8 * (size_t)p->nsteps * p->stamp_rails;
+    HIPCHK(hipMalloc(&p->d_engine, eb));
+    HIPCHK(hipMemset(p->d_engine, 0, eb));
     // a plan that is ONE segment can be armed by xg_plan_run (doorbell in host memory)
     if (c->engine_arm && !c->virt && p->segs.size() == 1 && p->segs[0].s0 == 0 && p->segs[0].s1 == p->nsteps) {
         HIPCHK(hipHostMalloc((void **)&p->db, sizeof(xgk::Doorbell), hipHostMallocCoherent));
@@ -745,7 +798,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant;
     p->d_pieces = nullptr; p->d_sb = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->d_disp = nullptr;
     p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
-    p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false;
+    p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1;
     // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
     // pieces for small launches were measured no faster, and slower where they stop
     // dividing the segment size (profiles/r01_min_pieces_ab.txt)
@@ -915,6 +968,12 @@ extern "C" int xg_plan_free(xg_plan *p)
 
 extern "C" int xg_plan_nsteps(const xg_plan *p) { return p->nsteps; }
 extern "C" int xg_plan_engine(const xg_plan *p) { return p->segs.empty() ? 0 : p->segs[0].w; }
+extern "C" int xg_plan_engine_rails(const xg_plan *p)
+{
+    for (const EngSeg &g : p->segs)
+        if (g.solo) return g.w;
+    return 0;
+}
 extern "C" int xg_plan_launches(const xg_plan *p) { return p->nlaunch; }
 
 extern "C" int xg_plan_engine_steps(const xg_plan *p, int *nseg, int *nhaz)
@@ -1077,9 +1136,9 @@ static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream, bool arme
     unsigned long long *stamps = reinterpret_cast<unsigned long long *>(p->d_engine + 1) + g.s0;
     const int *sb = p->d_sb + g.sb_off;
     if (g.solo)
-        hipLaunchKernelGGL(xgk::solo_engine_kernel<xgk::kSoloK>, dim3(1), dim3(xgk::kSoloThreads), 0, stream,
-                           p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, db,
-                           epoch);
+        hipLaunchKernelGGL(xgk::solo_engine_kernel<xgk::kSoloK>, dim3(g.w), dim3(xgk::kSoloThreads), 0, stream,
+                           p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
+                           db, epoch);
     else if (g.b == 1)
         hipLaunchKernelGGL(xgk::step_engine_kernel<1>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb, n,
                            p->d_engine, stamps, base, db, epoch);
@@ -1091,6 +1150,31 @@ static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream, bool arme
                            n, p->d_engine, stamps, base, db, epoch);
     HIPCHK(hipGetLastError());
     return kt_after(c, stream, kt, g.bytes);
+}
+
+// every engine step's stamp (wall-clock ticks), after a synchronised run: grid
+// segments stamp once per step; a solo segment's rails each stamp the steps they
+// closed (0 elsewhere), so a rail's stamp of step t is its latest at or before t
+// and the step's is the MAX over rails
+static int read_stamps(const xg_plan *p, std::vector<unsigned long long> &st)
+{
+    const size_t n = (size_t)p->nsteps;
+    std::vector<unsigned long long> all(n * p->stamp_rails);
+    HIPCHK(hipMemcpy(all.data(), p->d_engine + 1, 8 * all.size(), hipMemcpyDeviceToHost));
+    st.assign(all.begin(), all.begin() + n);
+    for (const EngSeg &g : p->segs) {
+        if (!g.solo) continue;
+        for (int t = g.s0; t < g.s1; ++t) st[t] = 0;
+        for (int r = 0; r < g.w; ++r) {
+            unsigned long long carry = 0;
+            for (int t = g.s0; t < g.s1; ++t) {
+                const unsigned long long x = all[(size_t)r * n + t];
+                if (x) carry = std::max(carry, x);
+                st[t] = std::max(st[t], carry);
+            }
+        }
+    }
+    return XG_OK;
 }
 
 // after a synchronised run: did an engine workgroup give up at a grid barrier?
@@ -1157,8 +1241,8 @@ static int run_armed(xg_plan *p, double *step_done, double *step_post, double *w
         for (int s = 1; s < p->nsteps; ++s) step_post[s] = 0;
     }
     if (step_done) {
-        std::vector<unsigned long long> st(p->nsteps);
-        HIPCHK(hipMemcpy(st.data(), p->d_engine + 1, 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
+        std::vector<unsigned long long> st;
+        if ((rc = read_stamps(p, st))) return rc;
         const double total = t1 - t0;
         for (int s = 0; s < p->nsteps; ++s) {
             const double x = total - (double)(st[p->nsteps - 1] - st[s]) / c->wall_hz;
@@ -1199,10 +1283,7 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     if ((rc = xg_plan_check(p))) return rc;
     if (!step_done) return XG_OK;
     std::vector<unsigned long long> st;
-    if (!p->segs.empty()) {
-        st.resize(p->nsteps);
-        HIPCHK(hipMemcpy(st.data(), p->d_engine + 1, 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
-    }
+    if (!p->segs.empty() && (rc = read_stamps(p, st))) return rc;
     for (int s = 0; s < p->nsteps;) {
         const int gi = p->seg_of[s];
         const int e = gi >= 0 ? p->segs[gi].s1 : s + 1;

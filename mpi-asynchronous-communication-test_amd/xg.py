@@ -332,6 +332,7 @@ def device():
         d.xg_plan_run.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
         d.xg_plan_enqueue.argtypes = [vp]
         d.xg_plan_engine.argtypes = [vp]
+        d.xg_plan_engine_rails.argtypes = [vp]
         d.xg_plan_check.argtypes = [vp]
         d.xg_plan_launches.argtypes = [vp]
         d.xg_plan_engine_steps.argtypes = [vp, C.POINTER(ip), C.POINTER(ip)]
@@ -504,6 +505,7 @@ class MethodRun:
         _check(d.xg_plan_load(ctx.handle, self._r, self.view.ptr, C.byref(self._p)), "xg_plan_load")
         self.nsteps = d.xg_plan_nsteps(self._p)
         self.engine_workgroups = d.xg_plan_engine(self._p)   # 0: one launch per step
+        self.engine_rails = d.xg_plan_engine_rails(self._p)  # > 0: a solo segment on that many rails
 
     def run_timed(self):
         """barrier-free timed run; returns (step_done[], step_post[], wall)."""

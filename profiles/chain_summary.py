@@ -19,20 +19,26 @@ def parse(path):
 
 
 def main(d):
-    modes = ["solo_armed", "grid_armed", "solo_launch", "grid_launch"]
+    modes = [m for m in ["solo_armed", "solo1_armed", "grid_armed", "solo_launch", "grid_launch"]
+             if glob.glob(os.path.join(d, m + "_*.txt"))]
     runs = {m: [parse(f) for f in sorted(glob.glob(os.path.join(d, m + "_*.txt")))] for m in modes}
-    ref = parse(os.path.join(d, "ref.txt")) if os.path.exists(os.path.join(d, "ref.txt")) else []
+    refs = [parse(f) for f in sorted(glob.glob(os.path.join(d, "ref*.txt")))]   # ref.txt or ref_<r>.txt
     base = runs["solo_armed"][0]
-    print("%-36s %4s %10s %10s %10s %10s %10s %7s" % ("method", "exp", *modes, "reference", "ratio"))
+    print(("%-36s %4s" + " %11s" * len(modes) + " %10s %7s") % ("method", "exp", *modes, "reference", "ratio"))
     seen = {}
     for i, (lab, _t) in enumerate(base):
         e = seen.get(lab, 0)
         seen[lab] = e + 1
         med = [S.median(r[i][1] for r in runs[m]) * 1e6 for m in modes]
-        rf = [t for (l, t) in ref if l == lab]
-        rv = rf[e] * 1e6 if e < len(rf) else float("nan")
-        print("%-36s %4d %10.1f %10.1f %10.1f %10.1f %10.1f %7.2f" % (lab, e, *med, rv, med[0] / rv))
-    print("(us, median over %d repetitions; ratio = solo_armed / reference)" % len(runs["solo_armed"]))
+        rv = []
+        for ref in refs:
+            rf = [t for (l, t) in ref if l == lab]
+            if e < len(rf):
+                rv.append(rf[e] * 1e6)
+        rv = S.median(rv) if rv else float("nan")
+        print(("%-36s %4d" + " %11.1f" * len(modes) + " %10.1f %7.2f") % (lab, e, *med, rv, med[0] / rv))
+    print("(us, median over %d repetitions, reference median over %d runs; ratio = solo_armed / reference)"
+          % (len(runs["solo_armed"]), len(refs)))
 
 
 if __name__ == "__main__":

@@ -10,7 +10,9 @@ import __graft_entry__ as G
 xg = G.load_package().xg
 P, A, d, c = 32, 14, 2048, 3
 rl = xg.aggregator_list(P, A)
-modes = {"solo_armed": {}, "grid_armed": {"XG_ENGINE_SOLO_STEP": "0"}, "solo_launch": {"XG_ENGINE_ARM": "0"}}
+modes = {"solo_armed": {}, "solo1_armed": {"XG_SOLO_RAILS": "1"}, "solo2_armed": {"XG_SOLO_RAILS": "2"},
+         "solo4_armed": {"XG_SOLO_RAILS": "4"}, "solo16_armed": {"XG_SOLO_RAILS": "16"},
+         "grid_armed": {"XG_ENGINE_SOLO": "0"}, "solo_launch": {"XG_ENGINE_ARM": "0"}}
 for name, env in modes.items():
     os.environ.update(env)
     ctx = xg.Context(0, 1, device=0)
@@ -26,7 +28,7 @@ for name, env in modes.items():
                 best = (done, post, wall)
         done = best[0]
         steps = [done[0]] + [b - a for a, b in zip(done, done[1:])]
-        print("%-11s m%-2d steps %2d total %6.1f us  first %5.1f  mean step %5.2f  max step %5.2f  last %5.2f  post %.1f" % (
+        print("%-12s m%-2d steps %2d total %6.1f us  first %5.1f  mean step %5.2f  max step %5.2f  last %5.2f  post %.1f" % (
             name, m, len(done), done[-1] * 1e6, done[0] * 1e6, sum(steps[1:]) / max(1, len(steps) - 1) * 1e6,
             max(steps[1:]) * 1e6, steps[-1] * 1e6, best[1][0] * 1e6), flush=True)
         print("    steps us: " + " ".join("%.2f" % (x * 1e6) for x in steps), flush=True)

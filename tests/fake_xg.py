@@ -64,6 +64,7 @@ def make(real_xg):
             self.nsteps = self.view.nsteps
             self.slots = sched.verify_slots(G, g)
             self.engine_workgroups = 0
+            self.engine_rails = 0
 
         @property
         def launches(self):
