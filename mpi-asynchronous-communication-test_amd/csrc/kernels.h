@@ -336,8 +336,11 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_b(const DCopy *__restric
 struct EngineState {
     unsigned count;     // arrival tickets, cumulative over every launch of the plan
     unsigned tmo;       // != 0: some workgroup gave up waiting
-    unsigned rails;     // solo engine, armed: rails finished (cumulative; the last of a launch rings `done`)
-    unsigned pad;
+    // solo engine, armed launches (cumulative counters; a launch adds one per rail):
+    unsigned rails;     // rails finished: the last of a launch rings `done`
+    unsigned arrive;    // rails resident: the last lets rail 0 announce `ready`
+    unsigned go;        // relay: rail 0 saw the ring of this epoch
+    unsigned pad[3];
 };
 
 template <int B>
@@ -385,6 +388,20 @@ __device__ __forceinline__ bool wait_ring(Doorbell *db, unsigned epoch)
 __device__ __forceinline__ void ring_done(Doorbell *db, unsigned epoch)
 {
     __hip_atomic_store((g_u32 *)&db->done, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// lane 0: wait until *w == v (SYS: a host-memory word, else device memory) or the
+// timeout word is set; false = gave up
+template <bool SYS>
+__device__ __forceinline__ bool poll_word(g_u32 *w, unsigned v, g_u32 *tmo)
+{
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned x = SYS ? __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                               : __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (x == v) return true;
+        if (spins > kRingSpins || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
 
 // B: 16-B loads per lane per unit -> units of B * 4 KiB (the host cuts the step's
@@ -612,7 +629,7 @@ __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigne
                                                                    uint8_t *dst_base, const int *__restrict__ meta,
                                                                    int nsteps, EngineState *st,
                                                                    unsigned long long *stamps, int stride,
-                                                                   Doorbell *db, unsigned epoch)
+                                                                   Doorbell *db, unsigned epoch, int relay)
 {
     const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
     const int rail = (int)blockIdx.x, R = (int)gridDim.x;
@@ -631,12 +648,38 @@ __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigne
         lcstep[i] = (short)cstep[i];
         ts[i] = 0;
     }
-    if (threadIdx.x == 0) give_up = db && !wait_ring(db, epoch);
+    // armed: every rail resident, then rail 0 announces `ready`; the ring reaches the
+    // rails either each through its own poll of host memory, or (relay) through rail 0,
+    // which alone polls the host and passes the epoch on in device memory
+    if (threadIdx.x == 0) {
+        bool ok = true;
+        if (db) {
+            g_u32 *tmo = (g_u32 *)&st->tmo;
+            const unsigned old = __hip_atomic_fetch_add((g_u32 *)&st->arrive, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (rail == 0) {
+                const unsigned all = (old / (unsigned)R + 1) * (unsigned)R;
+                for (unsigned spins = 0; ok && (int)(__hip_atomic_load((g_u32 *)&st->arrive, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT) - all) < 0; ++spins) {
+                    __builtin_amdgcn_s_sleep(1);
+                    ok = spins < kRingSpins;
+                }
+                ok = ok && wait_ring(db, epoch);
+                if (!ok) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (relay) __hip_atomic_store((g_u32 *)&st->go, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                ok = relay ? poll_word<false>((g_u32 *)&st->go, epoch, tmo) : poll_word<true>((g_u32 *)&db->ring, epoch, tmo);
+                if (!ok) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        give_up = !ok;
+    }
     __syncthreads();
     if (give_up) {
-        if (threadIdx.x == 0) {
-            __hip_atomic_store((g_u32 *)&st->tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ring_done(db, epoch);
+        if (threadIdx.x == 0) {      // still counted, so that the launch's last rail rings `done`
+            const unsigned done = __hip_atomic_fetch_add((g_u32 *)&st->rails, 1u, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) + 1;
+            if (done % (unsigned)R == 0) ring_done(db, epoch);
         }
         return;
     }

@@ -59,6 +59,7 @@ struct xg_ctx {
     int solo;                  // 0: never use the solo engine
     int64_t solo_max;          // solo segments move <= this many bytes per run
     int solo_rails;            // solo segments deal their pieces over up to this many workgroups
+    int solo_relay;            // armed solo: rail 0 alone polls the doorbell and relays the ring
     int engine_arm;            // 1: xg_plan_run arms single-segment plans (doorbell)
     int split_local;           // 1: a cross-GPU step's local gather runs on the side stream
     int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
@@ -249,6 +250,8 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->solo_rails = 8;                // see DESIGN.md (solo engine): one rail per XCD
     env = getenv("XG_SOLO_RAILS");
     if (env && atoi(env) > 0) c->solo_rails = std::min(atoi(env), xgk::kSoloMaxRails);
+    env = getenv("XG_SOLO_RELAY");           // "0": every rail polls the doorbell itself
+    c->solo_relay = !(env && !strcmp(env, "0"));
     env = getenv("XG_ENGINE_ARM");           // "0": launch latency inside the timed region
     c->engine_arm = !(env && !strcmp(env, "0"));
     env = getenv("XG_SPLIT_LOCAL");          // "0": local gather + packs in one launch
@@ -1138,7 +1141,7 @@ static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream, bool arme
     if (g.solo)
         hipLaunchKernelGGL(xgk::solo_engine_kernel<xgk::kSoloK>, dim3(g.w), dim3(xgk::kSoloThreads), 0, stream,
                            p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
-                           db, epoch);
+                           db, epoch, c->solo_relay);
     else if (g.b == 1)
         hipLaunchKernelGGL(xgk::step_engine_kernel<1>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb, n,
                            p->d_engine, stamps, base, db, epoch);

@@ -10,9 +10,11 @@ import __graft_entry__ as G
 xg = G.load_package().xg
 P, A, d, c = 32, 14, 2048, 3
 rl = xg.aggregator_list(P, A)
-modes = {"solo_armed": {}, "solo1_armed": {"XG_SOLO_RAILS": "1"}, "solo2_armed": {"XG_SOLO_RAILS": "2"},
+modes = {"solo_armed": {}, "solo_norelay": {"XG_SOLO_RELAY": "0"}, "solo1_armed": {"XG_SOLO_RAILS": "1"},
          "solo4_armed": {"XG_SOLO_RAILS": "4"}, "solo16_armed": {"XG_SOLO_RAILS": "16"},
          "grid_armed": {"XG_ENGINE_SOLO": "0"}, "solo_launch": {"XG_ENGINE_ARM": "0"}}
+if os.environ.get("PROBE_MODES"):
+    modes = {k: v for k, v in modes.items() if k in os.environ["PROBE_MODES"].split(",")}
 for name, env in modes.items():
     os.environ.update(env)
     ctx = xg.Context(0, 1, device=0)

@@ -162,6 +162,7 @@ ENGINE_MODES = {
     "solo_armed": {},                                           # default at README sizes (8 rails)
     "solo1_armed": {"XG_SOLO_RAILS": "1"},                      # one workgroup
     "solo3_launch": {"XG_SOLO_RAILS": "3", "XG_ENGINE_ARM": "0"},
+    "solo_norelay": {"XG_SOLO_RELAY": "0"},                     # every rail polls the doorbell
     "grid_armed": {"XG_ENGINE_SOLO": "0"},
     "solo_launch": {"XG_ENGINE_ARM": "0"},
     "grid_drain": {"XG_ENGINE_SOLO": "0", "XG_ENGINE_DRAIN": "1", "XG_ENGINE_ARM": "0"},
@@ -198,7 +199,7 @@ def test_step_engine_modes(xg, method, k):
             run = xg.MethodRun(cx, s, it=it, mode=1)
             try:
                 assert run.engine_workgroups > 0
-                rails = {"solo_armed": 8, "solo1_armed": 1, "solo3_launch": 3, "solo_launch": 8}.get(name, 0)
+                rails = {"solo_armed": 8, "solo1_armed": 1, "solo3_launch": 3, "solo_launch": 8, "solo_norelay": 8}.get(name, 0)
                 assert run.engine_rails == rails, (name, run.engine_rails)
                 for _rep in range(3):
                     done, _post, wall = run.run_timed()
