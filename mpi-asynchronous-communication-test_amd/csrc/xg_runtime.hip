@@ -557,8 +557,10 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         while (s < e && !p->steps[s].pre_n) ++s;
         while (e > s && !p->steps[e - 1].pre_n) --e;
         for (int t = s; t < e; ++t) busy += p->steps[t].pre_n > 0;
-        // one busy step is worth an (armed) engine launch only as the whole plan
-        const bool whole = s_run == 0 && run_end == p->nsteps && c->engine_arm && !c->virt;
+        // one busy step is worth an (armed) engine launch only as the whole plan, and only
+        // when that plan has more steps than it (a one-step plan is one copy launch, whose
+        // event-timed ~6 us beat the armed launch's host round trip)
+        const bool whole = s_run == 0 && run_end == p->nsteps && p->nsteps >= 2 && c->engine_arm && !c->virt;
         if (busy < (whole ? 1 : 2)) {
             s = run_end > s ? run_end : s + 1;
             continue;
