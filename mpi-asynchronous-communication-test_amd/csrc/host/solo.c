@@ -1,0 +1,98 @@
+/*
+ * solo.c -- the solo step engine's tables (kernels.h solo_engine_kernel,
+ * include/xg_sched.h xg_solo_tables): a hazard-free run of steps cut into
+ * 1 KiB pieces, dealt round-robin over R rails (workgroups), and per rail laid
+ * out as rows of XG_SOLO_WAVES pieces with the step barriers placed between
+ * them.
+ *
+ * A rail closes a step with a workgroup barrier only if it had pieces in it:
+ * the barrier sits in front of the rail's next piece -- in that piece's row,
+ * counted in the `before` field of that piece and of every later piece of the
+ * row, and in the row's barrier count -- and the step it closes is listed in
+ * order; a barrier in front of the rail's end is left to the kernel's closing
+ * stamp.  Each barrier precedes a distinct piece, so a row holds at most
+ * XG_SOLO_WAVES of them (the 5-bit `before` field).  A rail's table is padded
+ * with empty pieces to an even number of chunks of XG_SOLO_K rows plus one
+ * spare chunk (the kernel's double-buffered loop loads one chunk past the
+ * last without a branch).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "xg.h"
+#include "xg_sched.h"
+
+static uint64_t desc(uint64_t src16, uint64_t dst16, uint64_t len16) { return src16 | (dst16 << 24) | (len16 << 48); }
+
+int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, uint64_t src_base,
+                   uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta)
+{
+    if (!xfer || !step_begin || !shape || nsteps < 1 || nsteps > XG_SOLO_MAX_STEPS || rails_max < 1) return XG_EARG;
+    const int nx = step_begin[nsteps];
+    int64_t total = 0;
+    for (int i = 0; i < nx; ++i) {
+        const xg_span *x = &xfer[i];
+        if ((x->src | x->dst | x->len) & 15) return XG_EARG;
+        if (x->len && (x->src < src_base || x->dst < dst_base || (x->src + x->len - src_base) / 16 > XG_SOLO_OFF_MAX ||
+                       (x->dst + x->len - dst_base) / 16 > XG_SOLO_OFF_MAX))
+            return XG_EARG;
+        total += (int64_t)((x->len + XG_SOLO_PIECE - 1) / XG_SOLO_PIECE);
+    }
+    int64_t r = total / XG_SOLO_WAVES;
+    if (r > rails_max) r = rails_max;
+    if (r < 1) r = 1;
+    const int rails = (int)r;
+    const int64_t chunk = (int64_t)XG_SOLO_WAVES * XG_SOLO_K;
+    const int64_t longest = (total + rails - 1) / rails;     /* round-robin: counts differ by <= 1 */
+    const int64_t np = ((longest + 2 * chunk - 1) / (2 * chunk) * 2 + 1) * chunk;
+    shape->rails = rails;
+    shape->npieces = (int)(np > XG_SOLO_MAX_PIECES ? XG_SOLO_MAX_PIECES + 1 : np);
+    shape->nrows = (int)(np / XG_SOLO_WAVES);
+    shape->nmeta = rails * (shape->nrows + 1) + rails * nsteps;
+    if (np > XG_SOLO_MAX_PIECES) return XG_EARG;
+    if (!descs || !meta) return XG_OK;
+
+    const int nrows = shape->nrows;
+    memset(descs, 0, sizeof(uint64_t) * (size_t)rails * np);
+    int *close = meta, *cstep = meta + (size_t)rails * (nrows + 1);
+    memset(close, 0, sizeof(int) * (size_t)rails * (nrows + 1));
+    for (int64_t i = 0; i < (int64_t)rails * nsteps; ++i) cstep[i] = -1;
+    int64_t *cnt = calloc((size_t)rails, sizeof(int64_t));    /* pieces dealt to each rail */
+    int *nb = calloc((size_t)rails, sizeof(int));              /* barriers placed on each rail */
+    char *used = calloc((size_t)rails, 1);
+    int64_t *pend = calloc((size_t)rails, sizeof(int64_t));    /* open barrier position per rail, -1 none */
+    int *pstep = calloc((size_t)rails, sizeof(int));
+    if (!cnt || !nb || !used || !pend || !pstep) {
+        free(cnt); free(nb); free(used); free(pend); free(pstep);
+        return XG_ENOMEM;
+    }
+    for (int q = 0; q < rails; ++q) pend[q] = -1;
+    int cur = 0;
+    for (int t = 0; t < nsteps; ++t) {
+        memset(used, 0, (size_t)rails);
+        for (int i = step_begin[t]; i < step_begin[t + 1]; ++i)
+            for (uint64_t o = 0; o < xfer[i].len; o += XG_SOLO_PIECE) {
+                const uint64_t len = xfer[i].len - o < XG_SOLO_PIECE ? xfer[i].len - o : XG_SOLO_PIECE;
+                /* a barrier still open on this rail goes in front of this piece */
+                if (pend[cur] >= 0) {
+                    const int64_t at = pend[cur], row = at / XG_SOLO_WAVES;
+                    close[(size_t)cur * (nrows + 1) + row]++;
+                    cstep[(size_t)cur * nsteps + nb[cur]++] = pstep[cur];
+                    for (int64_t w = at % XG_SOLO_WAVES; w < XG_SOLO_WAVES; ++w)
+                        descs[(size_t)cur * np + row * XG_SOLO_WAVES + w] += 1ull << 55;
+                    pend[cur] = -1;
+                }
+                descs[(size_t)cur * np + cnt[cur]++] +=     /* its `before` bits may be set already */
+                    desc((xfer[i].src + o - src_base) / 16, (xfer[i].dst + o - dst_base) / 16, len / 16);
+                used[cur] = 1;
+                cur = (cur + 1) % rails;
+            }
+        for (int q = 0; q < rails; ++q)
+            if (used[q]) {
+                pend[q] = cnt[q];
+                pstep[q] = t;
+            }
+    }
+    free(cnt); free(nb); free(used); free(pend); free(pstep);
+    return XG_OK;
+}

@@ -525,6 +525,11 @@ static bool engine_step(const xg_ctx *c, const StepR &st)
 // over up to one workgroup per CU with bytes enough in flight
 // (profiles/r01_engine_sweep.txt: small units starve big steps, big units leave
 // small steps on a handful of workgroups).  Barrier flags: xg_engine_hazards.
+static_assert(xgk::kSoloWaves == XG_SOLO_WAVES && xgk::kSoloPiece == XG_SOLO_PIECE && xgk::kSoloK == XG_SOLO_K &&
+                  xgk::kSoloMaxSteps == XG_SOLO_MAX_STEPS && xgk::kSoloMaxPieces == XG_SOLO_MAX_PIECES &&
+                  xgk::kSoloOffMax == XG_SOLO_OFF_MAX,
+              "solo engine constants: kernels.h and xg_sched.h disagree");
+
 // Solo or grid engine for a hazard-free segment of n steps (`busy` of them move
 // bytes) moving `bytes`: the cheaper by a model of the measured costs (MI355X,
 // profiles/r02/solo_probe_steps.txt, rails.txt): a rail (one CU) moves ~120 GB/s of
@@ -609,27 +614,18 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         for (const auto &xs : xfer)
             for (const xgk::DCopy &x : xs)
                 aligned = aligned && ((((uintptr_t)x.src | (uintptr_t)x.dst | (uint64_t)x.len) & 15) == 0);
-        // solo: each step's 1 KiB pieces dealt round-robin over R rails; per rail, rows of
-        // kSoloWaves pieces, whole chunks of kSoloK rows, an even number of them, plus the
-        // spare chunk the double-buffered loop prefetches past the end
-        int64_t total_pieces = 0;
-        for (const auto &xs : xfer)
-            for (const xgk::DCopy &x : xs) total_pieces += (x.len + xgk::kSoloPiece - 1) / xgk::kSoloPiece;
-        const int rails = (int)std::max<int64_t>(1, std::min<int64_t>(c->solo_rails, total_pieces / xgk::kSoloWaves));
-        const int64_t chunk_pieces = (int64_t)xgk::kSoloWaves * xgk::kSoloK;
-        const int64_t per_rail = (total_pieces + rails - 1) / rails + n;     // + a row break per step at most
-        const int64_t solo_pieces = ((per_rail + 2 * chunk_pieces - 1) / (2 * chunk_pieces) * 2 + 1) * chunk_pieces;
-        // the segment's source and destination base pointers (solo descriptors are offsets)
+        // solo: each step's 1 KiB pieces dealt round-robin over up to solo_rails rails, per
+        // rail rows of kSoloWaves pieces (xg_solo_tables, host/solo.c)
         uintptr_t slo = UINTPTR_MAX, shi = 0, dlo = UINTPTR_MAX, dhi = 0;
-        for (const auto &xs : xfer)
-            for (const xgk::DCopy &x : xs)
-                if (x.len > 0) {
-                    slo = std::min(slo, (uintptr_t)x.src); shi = std::max(shi, (uintptr_t)x.src + (uintptr_t)x.len);
-                    dlo = std::min(dlo, (uintptr_t)x.dst); dhi = std::max(dhi, (uintptr_t)x.dst + (uintptr_t)x.len);
-                }
-        const bool near = shi > slo && dhi > dlo && (shi - slo) / 16 < xgk::kSoloOffMax && (dhi - dlo) / 16 < xgk::kSoloOffMax;
-        g.solo = g.nhaz == 0 && aligned && near && n <= xgk::kSoloMaxSteps && solo_pieces <= xgk::kSoloMaxPieces &&
-                 c->solo && g.bytes <= c->solo_max && solo_pays(g.bytes, n, rails, busy);
+        for (const xg_span &x : spans)
+            if (x.len > 0) {
+                slo = std::min<uintptr_t>(slo, x.src); shi = std::max<uintptr_t>(shi, x.src + x.len);
+                dlo = std::min<uintptr_t>(dlo, x.dst); dhi = std::max<uintptr_t>(dhi, x.dst + x.len);
+            }
+        xg_solo_shape sh{};
+        const bool fits = aligned && shi > slo && dhi > dlo && n <= xgk::kSoloMaxSteps &&
+                          xg_solo_tables(spans.data(), tb.data(), n, c->solo_rails, slo, dlo, &sh, nullptr, nullptr) == XG_OK;
+        g.solo = g.nhaz == 0 && fits && c->solo && g.bytes <= c->solo_max && solo_pays(g.bytes, n, sh.rails, busy);
         if (!g.solo && busy < 2) {      // one busy step: an engine launch only if it runs solo
             ep.resize(u0);
             s = run_end;
@@ -640,52 +636,13 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
             g.dbase = (uint8_t *)dlo;
             ep.resize(u0);
             g.u0 = (int)p->solo_desc.size();
-            g.w = rails;
-            // deal: per rail its pieces in step order and, per step it has pieces in, the
-            // barrier closing that step in front of its next piece
-            std::vector<std::vector<unsigned long long>> rp(rails);
-            std::vector<std::vector<std::pair<int64_t, int>>> bar(rails);   // (in front of piece, step)
-            int cur = 0;
-            for (int t = 0; t < n; ++t) {
-                std::vector<char> used(rails, 0);
-                for (const xgk::DCopy &x : xfer[t])
-                    for (int64_t o = 0; o < x.len; o += xgk::kSoloPiece) {
-                        rp[cur].push_back(xgk::solo_desc(((uintptr_t)x.src + o - slo) / 16, ((uintptr_t)x.dst + o - dlo) / 16,
-                                                         std::min<int64_t>(x.len - o, xgk::kSoloPiece) / 16, 0));
-                        used[cur] = 1;
-                        cur = (cur + 1) % rails;
-                    }
-                for (int r = 0; r < rails; ++r)
-                    if (used[r]) bar[r].push_back({(int64_t)rp[r].size(), t});
-            }
-            int64_t longest = 0;
-            for (int r = 0; r < rails; ++r) longest = std::max<int64_t>(longest, (int64_t)rp[r].size());
-            g.npieces = (int)(((longest + 2 * chunk_pieces - 1) / (2 * chunk_pieces) * 2 + 1) * chunk_pieces);
-            if (g.npieces > xgk::kSoloMaxPieces) return XG_EARG;      // cannot happen: per_rail bounds it
-            const int nrows = g.npieces / xgk::kSoloWaves;
-            std::vector<unsigned long long> &sd = p->solo_desc;
-            std::vector<int> meta((size_t)rails * (nrows + 1) + (size_t)rails * n, -1);
-            for (int r = 0; r < rails; ++r) {
-                const size_t d0 = sd.size();
-                const int64_t real = (int64_t)rp[r].size();
-                sd.insert(sd.end(), rp[r].begin(), rp[r].end());
-                sd.resize(d0 + g.npieces, 0ull);
-                // a barrier in front of piece i sits in its row, before the pieces at or
-                // after its column; those in front of the end close after the loop
-                int* close = &meta[(size_t)r * (nrows + 1)];
-                std::fill(close, close + nrows + 1, 0);
-                int* cs = &meta[(size_t)rails * (nrows + 1) + (size_t)r * n];
-                int nb = 0;
-                for (const auto &bt : bar[r]) {
-                    if (bt.first >= real) continue;
-                    const int64_t row = bt.first / xgk::kSoloWaves, col = bt.first % xgk::kSoloWaves;
-                    close[row]++;
-                    cs[nb++] = bt.second;
-                    for (int64_t w = col; w < xgk::kSoloWaves; ++w) sd[d0 + row * xgk::kSoloWaves + w] += 1ull << 55;
-                }
-                for (size_t i = d0; i < sd.size(); ++i)
-                    if ((sd[i] >> 55) > 31) return XG_EARG;      // cannot happen: <= 16 per row
-            }
+            g.w = sh.rails;
+            g.npieces = sh.npieces;
+            std::vector<int> meta(sh.nmeta);
+            p->solo_desc.resize(g.u0 + (size_t)sh.rails * sh.npieces);
+            if (xg_solo_tables(spans.data(), tb.data(), n, c->solo_rails, slo, dlo, &sh,
+                               reinterpret_cast<uint64_t *>(p->solo_desc.data()) + g.u0, meta.data()) != XG_OK)
+                return XG_EARG;
             sb.insert(sb.end(), meta.begin(), meta.end());
         } else {
             g.npieces = 0;

@@ -60,6 +60,10 @@ class DevPlan(C.Structure):
                 ("remote_recv_bytes", C.c_int64)]
 
 
+class SoloShape(C.Structure):
+    _fields_ = [("rails", C.c_int32), ("npieces", C.c_int32), ("nrows", C.c_int32), ("nmeta", C.c_int32)]
+
+
 class Span(C.Structure):
     _fields_ = [("src", C.c_uint64), ("dst", C.c_uint64), ("len", C.c_uint64)]
 
@@ -133,6 +137,8 @@ def host():
         h.xg_fill_runs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(SegRun)]
         h.xg_verify_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(Slot)]
         h.xg_engine_hazards.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int)]
+        h.xg_solo_tables.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.c_uint64, C.c_uint64,
+                                     C.POINTER(SoloShape), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
         h.xg_summarize_results.argtypes = [C.c_int] * 6 + [C.c_char_p, C.c_char_p, Timer, Timer]
         _host = h
     return _host
@@ -157,6 +163,31 @@ def engine_hazards(steps, force=False):
     fl = (C.c_int * max(1, len(steps)))()
     n = host().xg_engine_hazards(arr, sb, len(steps), 1 if force else 0, fl)
     return list(fl)[:len(steps)], n
+
+
+def solo_tables(steps, rails_max, src_base, dst_base):
+    """xg_solo_tables over steps = [[(src, dst, len), ...], ...]: returns (rc, shape dict,
+    per-rail descriptor lists, per-rail row barrier counts, per-rail closed-step lists)."""
+    spans = [x for st in steps for x in st]
+    arr = (Span * max(1, len(spans)))(*[Span(*x) for x in spans])
+    beg = [0]
+    for st in steps:
+        beg.append(beg[-1] + len(st))
+    sb = (C.c_int * len(beg))(*beg)
+    sh = SoloShape()
+    rc = host().xg_solo_tables(arr, sb, len(steps), rails_max, src_base, dst_base, C.byref(sh), None, None)
+    shape = {"rails": sh.rails, "npieces": sh.npieces, "nrows": sh.nrows, "nmeta": sh.nmeta}
+    if rc:
+        return rc, shape, None, None, None
+    R, npc, nr, n = sh.rails, sh.npieces, sh.nrows, len(steps)
+    d = (C.c_uint64 * (R * npc))()
+    m = (C.c_int * sh.nmeta)()
+    rc = host().xg_solo_tables(arr, sb, n, rails_max, src_base, dst_base, C.byref(sh), d, m)
+    descs = [list(d[r * npc:(r + 1) * npc]) for r in range(R)]
+    close = [list(m[r * (nr + 1):(r + 1) * (nr + 1)]) for r in range(R)]
+    off = R * (nr + 1)
+    csteps = [list(m[off + r * n: off + (r + 1) * n]) for r in range(R)]
+    return rc, shape, descs, close, csteps
 
 
 def method_label(method):

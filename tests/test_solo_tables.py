@@ -1,0 +1,138 @@
+"""The solo engine's tables (csrc/host/solo.c xg_solo_tables) on the CPU: an interpreter
+that executes them exactly as kernels.h solo_engine_kernel does -- per rail, rows of 16
+pieces, `before` barriers ahead of each wave's store, the row's barrier count in all,
+barrier k stamping the step meta lists for it, the spare chunk never stored -- checks
+that every piece of every step is stored exactly once, by some rail, between the barrier
+closing the rail's previous step and the one closing its own, and that the rails stay
+balanced.  Random segments and the real G = 1 plans of the README-config chains."""
+import random
+
+import pytest
+
+
+WAVES, PIECE, K, MAXP = 16, 1024, 8, 4608
+
+
+def decode(d):
+    return d & 0xFFFFFF, (d >> 24) & 0xFFFFFF, (d >> 48) & 127, d >> 55
+
+
+def interpret(steps, rails_max, sbase, dbase, xg):
+    rc, shape, descs, close, csteps = xg.solo_tables(steps, rails_max, sbase, dbase)
+    assert rc == 0, (rc, shape)
+    R, npc, nr = shape["rails"], shape["npieces"], shape["nrows"]
+    n = len(steps)
+    total = sum((x[2] + PIECE - 1) // PIECE for st in steps for x in st)
+    assert R == max(1, min(rails_max, total // WAVES))
+    assert npc % (WAVES * K) == 0 and (npc // (WAVES * K)) % 2 == 1      # even chunks + the spare
+    # the steps each (src, dst) piece belongs to (the -k repetitions move identical pieces)
+    owner = {}
+    for t, st in enumerate(steps):
+        for (s, d, ln) in st:
+            for o in range(0, ln, PIECE):
+                owner.setdefault((s + o, d + o), []).append((t, min(PIECE, ln - o)))
+    left = {key: list(v) for key, v in owner.items()}
+    per_rail = []
+    for r in range(R):
+        nb = sum(close[r])
+        cs = csteps[r]
+        assert all(c >= 0 for c in cs[:nb]) and all(c == -1 for c in cs[nb:]), cs
+        assert all(a < b for a, b in zip(cs[:nb], cs[1:nb])), cs       # closed steps increase
+        assert nr - K >= 0
+        k0 = 0                       # barriers before this row
+        real = 0
+        rail_steps = []
+        for row in range(nr):
+            nrow = close[r][row]
+            assert nrow <= WAVES
+            prev_bf = 0
+            for w in range(WAVES):
+                so, do, l16, bf = decode(descs[r][row * WAVES + w])
+                assert bf <= nrow and bf >= prev_bf
+                prev_bf = bf
+                if l16 == 0:
+                    assert so == 0 and do == 0
+                    continue
+                assert row < nr - K, "a piece in the spare chunk is never stored"
+                real += 1
+                key = (sbase + so * 16, dbase + do * 16)
+                assert key in owner, key
+                kb = k0 + bf                 # barriers executed before this store
+                lo = cs[kb - 1] + 1 if kb > 0 else 0          # it must belong to a step in [lo, hi]
+                hi = cs[kb] if kb < nb else n - 1
+                fit = [x for x in left[key] if lo <= x[0] <= hi]
+                assert fit, ("stored outside its step's barriers, or twice", r, row, w, lo, hi, owner[key])
+                t, ln = fit[0]
+                left[key].remove(fit[0])
+                assert l16 * 16 == ln
+                rail_steps.append(t)
+            k0 += nrow
+        assert k0 == nb
+        assert rail_steps == sorted(rail_steps), "a rail stores its steps in order"
+        # every step the rail had pieces in is closed by a barrier, or is its last one
+        used = sorted(set(rail_steps))
+        assert used[:-1] == [c for c in cs[:nb] if c in used[:-1]] and set(cs[:nb]) == set(used[:-1])
+        per_rail.append(real)
+    assert not any(left.values()), "every piece stored"
+    assert max(per_rail) - min(per_rail) <= 1, per_rail
+    return shape
+
+
+def random_steps(rng, nsteps, sbase, dbase):
+    steps, so, do = [], 0, 0
+    for _ in range(nsteps):
+        st = []
+        for _ in range(rng.choice([0, 1, 1, 2, 3, 5])):
+            ln = 16 * rng.randint(1, 300)
+            st.append((sbase + so, dbase + do, ln))
+            so += ln + 16 * rng.randint(0, 4)
+            do += ln + 16 * rng.randint(0, 4)
+        steps.append(st)
+    return steps
+
+
+@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("rails", [1, 3, 8, 16])
+def test_random_segments(xg, seed, rails):
+    rng = random.Random(seed * 31 + rails)
+    sbase, dbase = 1 << 32, 3 << 32
+    steps = random_steps(rng, rng.randint(1, 60), sbase, dbase)
+    if not any(steps):
+        steps[0].append((sbase, dbase, 4096))
+    interpret(steps, rails, sbase, dbase, xg)
+
+
+@pytest.mark.parametrize("method", [6, 9, 10, 11, 12, 18])
+@pytest.mark.parametrize("k", [1, 3])
+def test_readme_chain_plans(xg, method, k):
+    """the G = 1 plans of the README configuration (P32 A14 d2048 c3), as build_segments
+    hands them over: one transfer per local copy, SEND and RECV at 1 GiB apart"""
+    P, A, d, c = 32, 14, 2048, 3
+    s = xg.Schedule(method, P, A, d, c, xg.aggregator_list(P, A), ntimes=k)
+    v = s.devplan(1, 0)
+    base = {b: (1 << 32) + (b << 30) for b in range(xg.NBUF)}
+    steps = []
+    for (pb, pn, _qb, _qn, _ob, _on) in v.steps:
+        steps.append([(base[sb] + so, base[db] + do, ln) for (sb, so, db, do, ln) in v.copies[pb:pb + pn]])
+    while steps and not steps[-1]:
+        steps.pop()
+    srcs = [x[0] for st in steps for x in st]
+    dsts = [x[1] for st in steps for x in st]
+    shape = interpret(steps, 8, min(srcs), min(dsts), xg)
+    assert shape["rails"] == 8
+
+
+def test_rejects(xg):
+    sb, db = 1 << 32, 3 << 32
+    rc, _s, *_ = xg.solo_tables([[(sb + 8, db, 64)]], 8, sb, db)            # misaligned
+    assert rc == 3
+    rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 8, sb + 16, db)           # below the base
+    assert rc == 3
+    rc, _s, *_ = xg.solo_tables([[(sb + (1 << 28), db, 64)]], 8, sb, db)   # past the 24-bit window
+    assert rc == 3
+    rc, shape, *_ = xg.solo_tables([[(sb, db, 1024 * MAXP * 2)]], 1, sb, db)    # too many pieces per rail
+    assert rc == 3 and shape["npieces"] > MAXP
+    rc, shape, *_ = xg.solo_tables([[(sb, db, 1024 * MAXP * 2)]], 8, sb, db)    # ... which rails spread
+    assert rc == 0 and shape["rails"] == 8
+    rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]] * 2049, 8, sb, db)         # too many steps
+    assert rc == 3
