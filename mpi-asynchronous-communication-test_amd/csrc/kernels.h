@@ -284,10 +284,15 @@ __device__ void realign_copy(const uint8_t *s, uint8_t *t, int64_t n, uint32_t (
 //   copy_kernel_g<U, NT>   global loads/stores, U-deep software pipeline; NT: non-temporal
 //   copy_kernel_b<U, AUX>  the same through buffer resources, store policy AUX
 // Pieces whose pointers or length are not 16-B aligned take realign_copy.
+// start != nullptr: workgroup 0 stamps the launch's start (wall clock) there -- in a
+// chain of back-to-back step launches that is the time the previous step completed
+// (xg_plan_run), so the steps need no timing event between them.
 template <int U, bool NT = false>
-__global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restrict__ pieces)
+__global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restrict__ pieces,
+                                                          unsigned long long *start)
 {
     __shared__ uint32_t lds[2][kTileWords];
+    if (start && blockIdx.x == 0 && threadIdx.x == 0) *start = (unsigned long long)wall_clock64();
     const DCopy c = pieces[blockIdx.x];
     if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
         pipelined_copy16<U, NT>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
@@ -304,6 +309,12 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_b(const DCopy *__restric
         pipelined_copy16_b<U, AUX>(c.src, c.dst, (int)c.len);
     else
         realign_copy(c.src, c.dst, c.len, lds);
+}
+
+// the wall clock after everything before it on the stream: closes a chain of step launches
+__global__ void clock_kernel(unsigned long long *t)
+{
+    if (threadIdx.x == 0) *t = (unsigned long long)wall_clock64();
 }
 
 // ---------------------------------------------------------------- step engine

@@ -60,6 +60,7 @@ struct xg_ctx {
     int64_t solo_max;          // solo segments move <= this many bytes per run
     int solo_rails;            // solo segments deal their pieces over up to this many workgroups
     int solo_relay;            // armed solo: rail 0 alone polls the doorbell and relays the ring
+    int step_chain;            // 1: time runs of one-launch local steps by in-kernel stamps (xg_plan_run)
     int engine_arm;            // 1: xg_plan_run arms single-segment plans (doorbell)
     int split_local;           // 1: a cross-GPU step's local gather runs on the side stream
     int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
@@ -146,7 +147,21 @@ struct xg_plan {
     int ndisp;
     int nlaunch;                   // kernel launches per run (copies + engine), RCCL's aside
     bool rec_ev;                   // xg_plan_run is recording step events (fused launches record the previous step's)
+    // chains: runs of >= 2 consecutive steps that are each ONE local copy launch (outside
+    // engine segments, no RCCL, no barrier).  xg_plan_run times them without an event
+    // between launches (an event record costs ~5 us of idle device between two launches):
+    // launch t+1 stamps its start = step t's completion, a clock kernel closes the chain,
+    // one event after it anchors the stamps.  chain_end[s] = end of s's chain (s = its
+    // first step), 0 elsewhere.
+    std::vector<int> chain_end;
+    unsigned long long *d_cstamp;  // nsteps wall-clock stamps of chained steps
 };
+
+// the copy kernel variant of a launch moving `bytes` (launch_copy)
+static int copy_variant(const xg_plan *p, int64_t bytes)
+{
+    return p->variant == 0 ? (bytes >= p->ctx->nt_min ? 6 : 1) : p->variant;
+}
 
 extern "C" double xg_now(void)
 {
@@ -250,6 +265,8 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->solo_rails = 8;                // see DESIGN.md (solo engine): one rail per XCD
     env = getenv("XG_SOLO_RAILS");
     if (env && atoi(env) > 0) c->solo_rails = std::min(atoi(env), xgk::kSoloMaxRails);
+    env = getenv("XG_STEP_CHAIN");           // "0": an event after every step launch
+    c->step_chain = !(env && !strcmp(env, "0"));
     env = getenv("XG_SOLO_RELAY");           // "0": every rail polls the doorbell itself
     c->solo_relay = !(env && !strcmp(env, "0"));
     env = getenv("XG_ENGINE_ARM");           // "0": launch latency inside the timed region
@@ -760,7 +777,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant;
     p->d_pieces = nullptr; p->d_sb = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->d_disp = nullptr;
     p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
-    p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1;
+    p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1; p->d_cstamp = nullptr;
     // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
     // pieces for small launches were measured no faster, and slower where they stop
     // dividing the segment size (profiles/r01_min_pieces_ab.txt)
@@ -900,6 +917,26 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         p->nlaunch += (st.stage_n > 0) + (st.split ? (st.local_n > 0) + (st.pack_n > 0 || st.fused) : st.pre_n > 0 || st.fused) +
                       (st.post_n > 0 && !st.deferred);
     }
+    p->chain_end.assign(p->nsteps, 0);
+    if (c->step_chain) {
+        auto one_launch = [&](int s) {
+            const StepR &st = p->steps[s];
+            const int v = copy_variant(p, st.local_bytes);
+            return p->seg_of[s] < 0 && !st.split && !st.fused && !st.deferred && !st.stage_n && !st.p2p_n && !st.pack_n &&
+                   !st.post_n && !st.sync_after && st.local_n > 0 && (v == 1 || v == 6);
+        };
+        bool any = false;
+        for (int s = 0; s < p->nsteps;) {
+            int e = s;
+            while (e < p->nsteps && one_launch(e)) ++e;
+            if (e - s >= 2) {
+                p->chain_end[s] = e;
+                any = true;
+            }
+            s = e > s ? e : s + 1;
+        }
+        if (any) HIPCHK(hipMalloc(&p->d_cstamp, 8 * (size_t)p->nsteps));
+    }
     *out = p;
     return XG_OK;
 bad:
@@ -920,6 +957,7 @@ extern "C" int xg_plan_free(xg_plan *p)
     if (p->d_disp) HIPCHK(hipFree(p->d_disp));
     if (p->db) HIPCHK(hipHostFree((void *)p->db));
     if (p->d_solo) HIPCHK(hipFree(p->d_solo));
+    if (p->d_cstamp) HIPCHK(hipFree(p->d_cstamp));
     for (auto &e : p->ev) HIPCHK(hipEventDestroy(e));
     for (auto &e : p->fork) if (e) HIPCHK(hipEventDestroy(e));
     for (auto &e : p->join) if (e) HIPCHK(hipEventDestroy(e));
@@ -963,17 +1001,19 @@ extern "C" int xg_plan_displs(const xg_plan *p, int64_t *out, int n)
 // non-temporal loads and stores (6.3 TB/s vs 5.5-5.6 plain from 256 MiB up), a smaller
 // one keeps the default policy, which re-runs serve from the cache
 // (profiles/r02/copy_nt_sizes.txt).  1..6 force one form (A/B, tests).
-static int launch_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t st)
+// start: stamp the launch's start there (variants 1 and 6 only; see copy_kernel_g)
+static int launch_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t st, unsigned long long *start = nullptr)
 {
     const xgk::DCopy *pc = p->d_pieces + b;
-    const int v = p->variant == 0 ? (bytes >= p->ctx->nt_min ? 6 : 1) : p->variant;
+    const int v = copy_variant(p, bytes);
+    if (start && v != 1 && v != 6) return XG_EARG;
     switch (v) {
     case 2: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxPlain>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 3: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxSC1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 4: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 5: hipLaunchKernelGGL((xgk::copy_kernel_b<8, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 6: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
+    case 6: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start); break;
+    default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start); break;
     }
     HIPCHK(hipGetLastError());
     return XG_OK;
@@ -1223,9 +1263,30 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     const double t0 = xg_now();
     HIPCHK(hipEventRecord(p->ev0, c->stream));
     p->rec_ev = true;
+    const bool chains = p->d_cstamp && !c->kt_mode;
     for (int s = 0; s < p->nsteps;) {
         const double tp = xg_now();
         const int gi = p->seg_of[s];
+        if (chains && p->chain_end[s]) {
+            // a chain: launch t + 1 stamps step t's completion at its start; a clock
+            // kernel stamps the last one's, one event after it anchors them all
+            const int ce = p->chain_end[s];
+            for (int t = s; t < ce; ++t) {
+                const double tq = xg_now();
+                const StepR &st = p->steps[t];
+                if ((rc = launch_copy(p, st.local_b, st.local_n, st.local_bytes, c->stream,
+                                      t > s ? p->d_cstamp + t - 1 : nullptr))) {
+                    p->rec_ev = false;
+                    return rc;
+                }
+                if (step_post) step_post[t] = xg_now() - tq;
+            }
+            hipLaunchKernelGGL(xgk::clock_kernel, dim3(1), dim3(64), 0, c->stream, p->d_cstamp + ce - 1);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(p->ev[ce - 1], c->stream));
+            s = ce;
+            continue;
+        }
         const int e = gi >= 0 ? p->segs[gi].s1 : s + 1;     // one launch posts a whole segment
         if ((rc = enqueue_unit(p, s))) {
             p->rec_ev = false;
@@ -1246,8 +1307,25 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     if (!step_done) return XG_OK;
     std::vector<unsigned long long> st;
     if (!p->segs.empty() && (rc = read_stamps(p, st))) return rc;
+    std::vector<unsigned long long> cst;
+    if (chains) {
+        cst.resize(p->nsteps);
+        HIPCHK(hipMemcpy(cst.data(), p->d_cstamp, 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
+    }
     for (int s = 0; s < p->nsteps;) {
         const int gi = p->seg_of[s];
+        if (chains && p->chain_end[s]) {
+            const int ce = p->chain_end[s];
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[ce - 1]));
+            const double end = ms * 1e-3;
+            for (int t = s; t < ce; ++t) {
+                const double x = end - (double)(cst[ce - 1] - cst[t]) / c->wall_hz;
+                step_done[t] = t == ce - 1 ? end : (x > 0 ? x : 0);
+            }
+            s = ce;
+            continue;
+        }
         const int e = gi >= 0 ? p->segs[gi].s1 : s + 1;
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[e - 1]));

@@ -94,7 +94,7 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
         switch (kind) {
         case 0: hipLaunchKernelGGL(gridstride_copy, dim3(2048), dim3(xgk::kThreads), 0, st, (const xgk::u32x4 *)a,
                                    (xgk::u32x4 *)b, n4); break;
-        case 1: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        case 1: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         case 2: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxSC1>), dim3(np), dim3(xgk::kThreads), 0, st, dp);
                 break;
         case 3: hipLaunchKernelGGL(read_only, dim3(4096), dim3(xgk::kThreads), 0, st, (const xgk::u32x4 *)a, n4, sink);
@@ -103,8 +103,8 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
         case 5: CK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, st)); break;
         case 6: hipLaunchKernelGGL(gridstride_copy_nt, dim3(2048), dim3(xgk::kThreads), 0, st, (const xgk::u32x4 *)a,
                                    (xgk::u32x4 *)b, n4); break;
-        case 9: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
-        default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        case 9: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
+        default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         }
         CK(hipGetLastError());
     }

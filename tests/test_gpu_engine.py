@@ -316,3 +316,42 @@ def test_engine_segments_in_multi_gpu_plans(xg, method):
             r.close()
         for cx in ctxs + ectxs:
             cx.close()
+
+
+@pytest.mark.parametrize("method,d", [(11, 1 << 20), (12, 1 << 20), (9, 4 << 20)])
+def test_step_chains_time_like_events(xg, method, d):
+    """Runs of one-launch local steps (large steps, outside the engine) are timed by
+    in-kernel start stamps instead of an event after every launch (XG_STEP_CHAIN):
+    same delivered bytes as the evented run, step times ordered and inside the run's
+    wall time, and no later than the evented run's by more than noise."""
+    import xg_oracle as O
+    P, A, c = 32, 14, 3
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=2)
+    exp = O.expected_recv(method, P, A, d, rl, 0, mode=1)
+    res = {}
+    for name, env in (("chain", {}), ("events", {"XG_STEP_CHAIN": "0"})):
+        cx = _ctx_env(xg, XG_ENGINE_MAX_STEP=0, **env)
+        try:
+            run = xg.MethodRun(cx, s, it=0, mode=1)
+            try:
+                best = None
+                for _rep in range(3):
+                    done, _post, wall = run.run_timed()
+                    assert all(0 <= a <= b for a, b in zip(done, done[1:])), (name, done)
+                    assert done[-1] <= wall + 1e-4
+                    best = done[-1] if best is None else min(best, done[-1])
+                chk, bad, _f = run.verify()
+                assert all(b == 0 for b in bad), name
+                for (src, seed, dst, off), ck in zip(run.slots, chk):
+                    local = off - s.recv_offset(1, dst)
+                    assert ck == O.chk64(exp[dst][local: local + d]), (name, src, dst)
+                res[name] = (chk, best)
+            finally:
+                run.close()
+        finally:
+            cx.close()
+    assert res["chain"][0] == res["events"][0]
+    print("method %d d %d: chained %.1f us, evented %.1f us" % (method, d, res["chain"][1] * 1e6,
+                                                                res["events"][1] * 1e6))
+    assert res["chain"][1] <= res["events"][1] * 1.10 + 20e-6
