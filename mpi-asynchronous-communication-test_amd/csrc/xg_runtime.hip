@@ -67,6 +67,7 @@ struct xg_ctx {
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
     int64_t nt_min;         // variant 0: launches moving >= this many bytes use non-temporal loads/stores
+    int64_t nt_stream;      // ... and in a plan streaming past the Infinity Cache, launches >= this many
     int engine_occ;            // co-resident step-engine workgroups the device admits (plan load caps W)
     // kernel timing session (xg_ktime_begin/end): 1 = an event pair around every
     // copy launch, 2 = one pair around the whole session on the main stream
@@ -128,6 +129,7 @@ struct xg_plan {
     std::vector<hipEvent_t> fork, join;   // per split step: main -> side, side -> main
     hipEvent_t ev0;
     int variant;
+    bool streaming;                // one run copies more than the Infinity Cache holds (read + write)
     // step engine segments
     std::vector<int> seg_of;       // per step: index into segs, or -1
     std::vector<EngSeg> segs;
@@ -157,10 +159,16 @@ struct xg_plan {
     unsigned long long *d_cstamp;  // nsteps wall-clock stamps of chained steps
 };
 
-// the copy kernel variant of a launch moving `bytes` (launch_copy)
+// The copy kernel variant of a launch moving `bytes` (launch_copy).  Variant 0 picks
+// non-temporal loads/stores (6) when the bytes cannot come back from the 256 MiB
+// Infinity Cache: a launch whose own source + destination exceed it, or a launch of
+// >= nt_stream bytes in a plan whose run copies more than it (every step then finds
+// its bytes evicted by the steps before); plain (1) otherwise.
 static int copy_variant(const xg_plan *p, int64_t bytes)
 {
-    return p->variant == 0 ? (bytes >= p->ctx->nt_min ? 6 : 1) : p->variant;
+    if (p->variant) return p->variant;
+    const xg_ctx *c = p->ctx;
+    return bytes >= c->nt_min || (p->streaming && c->nt_stream > 0 && bytes >= c->nt_stream) ? 6 : 1;
 }
 
 extern "C" double xg_now(void)
@@ -238,6 +246,9 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->nt_min = 128 << 20;
     env = getenv("XG_COPY_NT_MIN");
     if (env) c->nt_min = atol(env);
+    c->nt_stream = 4 << 20;           // below it nt and plain tie (profiles/r02/copy_nt_sizes.txt); 0: off
+    env = getenv("XG_COPY_NT_STREAM");
+    if (env) c->nt_stream = atol(env);
     c->engine_max_step = 16 << 20;    // crossover vs one launch per step: profiles/r01_engine_sweep.txt
     env = getenv("XG_ENGINE_MAX_STEP");      // 0: never use the step engine
     if (env) c->engine_max_step = atol(env);
@@ -774,7 +785,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         }
     HIPCHK(hipSetDevice(c->device));
     xg_plan *p = new xg_plan();
-    p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant;
+    p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant; p->streaming = false;
     p->d_pieces = nullptr; p->d_sb = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->d_disp = nullptr;
     p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
     p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1; p->d_cstamp = nullptr;
@@ -916,6 +927,11 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         }
         p->nlaunch += (st.stage_n > 0) + (st.split ? (st.local_n > 0) + (st.pack_n > 0 || st.fused) : st.pre_n > 0 || st.fused) +
                       (st.post_n > 0 && !st.deferred);
+    }
+    {
+        int64_t run = 0;
+        for (const StepR &st : p->steps) run += st.stage_bytes + st.local_bytes + st.pack_bytes + st.post_bytes;
+        p->streaming = 2 * run > ((int64_t)256 << 20);
     }
     p->chain_end.assign(p->nsteps, 0);
     if (c->step_chain) {
