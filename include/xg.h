@@ -95,10 +95,16 @@ int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_t d, int it
 int xg_plan_load(xg_ctx *ctx, xg_regions *r, const xg_devplan *dp, xg_plan **out);
 int xg_plan_free(xg_plan *p);
 int xg_plan_nsteps(const xg_plan *p);
-/* Timed run (caller barriers first): enqueues every step with a completion
- * event, waits, and returns per step the device completion time (seconds
- * since the run started) and the host enqueue time; *wall = host seconds from
- * start to the final synchronisation. */
+/* Timed run (caller barriers first): enqueues every step, waits, and returns per
+ * step the device completion time (seconds since the run started) and the host
+ * enqueue time; *wall = host seconds from start to the final synchronisation.
+ * What a step's completion time means: per-step launches -- the event after its
+ * last launch (or, in a chain of one-launch local steps, the start of the next
+ * launch), i.e. its bytes stored; engine segments -- the wall-clock stamp at the
+ * step's barrier, which for steps without a drain flag is when their stores were
+ * ISSUED (not yet performed); only drained steps (hazard points and the last step
+ * of every segment, which anchors the others) are delivery times.  A run's total
+ * is therefore always a delivered time. */
 int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall);
 /* Enqueue all steps once without events or synchronisation (bench loops).  Check
  * the step engine's timeout word with xg_plan_check after synchronising. */
