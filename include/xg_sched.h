@@ -210,7 +210,8 @@ int xg_engine_hazards(const xg_span *xfer, const int *step_begin, int nsteps, in
  * 0 = empty padding), 55-59 `before` = how many of its row's step barriers precede
  * it.  meta: [rails][nrows + 1] barriers per row (rows of XG_SOLO_WAVES pieces), then
  * [rails][nsteps] the step each barrier closes, in order, -1 past the last (a rail
- * places a barrier only after a step it had pieces in, in front of its next piece).
+ * places a barrier only after a step it had pieces in, in front of its next piece),
+ * then [rails] the rows that hold real pieces (the rest is padding, never executed).
  * descs / meta NULL: fill *shape only.  Returns 0, or XG_EARG (xg.h) for bad input or
  * npieces > XG_SOLO_MAX_PIECES (*shape still filled), XG_ENOMEM. */
 #define XG_SOLO_WAVES 16

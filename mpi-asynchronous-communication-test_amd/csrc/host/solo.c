@@ -14,7 +14,8 @@
  * XG_SOLO_WAVES of them (the 5-bit `before` field).  A rail's table is padded
  * with empty pieces to an even number of chunks of XG_SOLO_K rows plus one
  * spare chunk (the kernel's double-buffered loop loads one chunk past the
- * last without a branch).
+ * last without a branch); the kernel stops after the rows that hold real
+ * pieces (meta's last R entries), so the padding costs a table slot, not time.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -48,7 +49,7 @@ int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int r
     shape->rails = rails;
     shape->npieces = (int)(np > XG_SOLO_MAX_PIECES ? XG_SOLO_MAX_PIECES + 1 : np);
     shape->nrows = (int)(np / XG_SOLO_WAVES);
-    shape->nmeta = rails * (shape->nrows + 1) + rails * nsteps;
+    shape->nmeta = rails * (shape->nrows + 1) + rails * nsteps + rails;
     if (np > XG_SOLO_MAX_PIECES) return XG_EARG;
     if (!descs || !meta) return XG_OK;
 
@@ -93,6 +94,8 @@ int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int r
                 pstep[q] = t;
             }
     }
+    int *rows = cstep + (size_t)rails * nsteps;               /* rows holding real pieces */
+    for (int q = 0; q < rails; ++q) rows[q] = (int)((cnt[q] + XG_SOLO_WAVES - 1) / XG_SOLO_WAVES);
     free(cnt); free(nb); free(used); free(pend); free(pstep);
     return XG_OK;
 }

@@ -616,10 +616,12 @@ __device__ __forceinline__ void solo_close(unsigned long long *ts, const short *
 // it: barrier (every wave issued their stores), stamp
 template <int K>
 __device__ __forceinline__ void solo_store(const SoloChunk<K> &b, const unsigned short *lclose, const short *lcstep,
-                                          unsigned long long *ts, int &s, int c, uint64_t l16, uint8_t *dst_base)
+                                          unsigned long long *ts, int &s, int c, int rows, uint64_t l16,
+                                          uint8_t *dst_base)
 {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
+        if (c * K + k >= rows) break;         // padding rows: no piece, no barrier
         const int n = __builtin_amdgcn_readfirstlane((int)lclose[c * K + k]);     // barriers in this row
         const int bf = __builtin_amdgcn_readfirstlane((int)(b.d[k] >> 55));      // ... before my piece
         int j = 0;
@@ -653,6 +655,8 @@ __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigne
     desc += (size_t)rail * npieces;
     const int *row_close = meta + rail * (nrows + 1);
     const int *cstep = meta + R * (nrows + 1) + rail * nsteps;
+    const int rows = meta[R * (nrows + 1) + R * nsteps + rail];     // rows holding real pieces
+    const int nreal = (rows + K - 1) / K;                              // ... in that many chunks
     for (int i = (int)threadIdx.x; i < npieces; i += kSoloThreads) ldesc[i] = desc[i];
     for (int i = (int)threadIdx.x; i <= nrows; i += kSoloThreads) lclose[i] = (unsigned short)row_close[i];
     for (int i = (int)threadIdx.x; i < nsteps; i += kSoloThreads) {
@@ -696,17 +700,18 @@ __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigne
     }
     const uint64_t l16 = (uint64_t)lane;
     // double buffer: chunk c+1's loads fly while chunk c stores.  The host pads the
-    // table to an even number of chunks plus one spare empty chunk, so every load
-    // below is unconditional (a conditional one would make the compiler wait on it).
-    const int nchunks = nrows / K - 1;
+    // table to an even number of chunks plus one spare empty chunk, so the loads below
+    // need no bounds branch (a conditional one would make the compiler wait on it);
+    // the loop leaves after the last chunk that holds real pieces.
     SoloChunk<K> A, B;
     int k = 0;
     solo_load<K>(A, ldesc, 0, wave, l16, src_base);
-    for (int c = 0; c < nchunks; c += 2) {
+    for (int c = 0; c < nreal; c += 2) {
         solo_load<K>(B, ldesc, c + 1, wave, l16, src_base);
-        solo_store<K>(A, lclose, lcstep, ts, k, c, l16, dst_base);
+        solo_store<K>(A, lclose, lcstep, ts, k, c, rows, l16, dst_base);
+        if (c + 1 >= nreal) break;
         solo_load<K>(A, ldesc, c + 2, wave, l16, src_base);
-        solo_store<K>(B, lclose, lcstep, ts, k, c + 1, l16, dst_base);
+        solo_store<K>(B, lclose, lcstep, ts, k, c + 1, rows, l16, dst_base);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this rail's last steps: delivered
     __syncthreads();

@@ -167,7 +167,8 @@ def engine_hazards(steps, force=False):
 
 def solo_tables(steps, rails_max, src_base, dst_base):
     """xg_solo_tables over steps = [[(src, dst, len), ...], ...]: returns (rc, shape dict,
-    per-rail descriptor lists, per-rail row barrier counts, per-rail closed-step lists)."""
+    per-rail descriptor lists, per-rail row barrier counts, per-rail closed-step lists,
+    per-rail rows holding real pieces)."""
     spans = [x for st in steps for x in st]
     arr = (Span * max(1, len(spans)))(*[Span(*x) for x in spans])
     beg = [0]
@@ -178,7 +179,7 @@ def solo_tables(steps, rails_max, src_base, dst_base):
     rc = host().xg_solo_tables(arr, sb, len(steps), rails_max, src_base, dst_base, C.byref(sh), None, None)
     shape = {"rails": sh.rails, "npieces": sh.npieces, "nrows": sh.nrows, "nmeta": sh.nmeta}
     if rc:
-        return rc, shape, None, None, None
+        return rc, shape, None, None, None, None
     R, npc, nr, n = sh.rails, sh.npieces, sh.nrows, len(steps)
     d = (C.c_uint64 * (R * npc))()
     m = (C.c_int * sh.nmeta)()
@@ -187,7 +188,8 @@ def solo_tables(steps, rails_max, src_base, dst_base):
     close = [list(m[r * (nr + 1):(r + 1) * (nr + 1)]) for r in range(R)]
     off = R * (nr + 1)
     csteps = [list(m[off + r * n: off + (r + 1) * n]) for r in range(R)]
-    return rc, shape, descs, close, csteps
+    rows = list(m[off + R * n: off + R * n + R])
+    return rc, shape, descs, close, csteps, rows
 
 
 def method_label(method):

@@ -8,7 +8,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import __graft_entry__ as G
 
 xg = G.load_package().xg
-P, A, d, c = 32, 14, 2048, 3
+P, A, d, c = [int(x) for x in os.environ.get("PROBE_CFG", "32,14,2048,3").split(",")]
 rl = xg.aggregator_list(P, A)
 modes = {"solo_armed": {}, "solo_norelay": {"XG_SOLO_RELAY": "0"}, "solo1_armed": {"XG_SOLO_RAILS": "1"},
          "solo4_armed": {"XG_SOLO_RAILS": "4"}, "solo16_armed": {"XG_SOLO_RAILS": "16"},
@@ -20,7 +20,7 @@ for name, env in modes.items():
     ctx = xg.Context(0, 1, device=0)
     for k in env:
         del os.environ[k]
-    for m in (6, 9, 12):
+    for m in [int(x) for x in os.environ.get("PROBE_METHODS", "6,9,12").split(",")]:
         s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
         run = xg.MethodRun(ctx, s, it=0, mode=0)
         best = None

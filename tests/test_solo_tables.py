@@ -18,7 +18,7 @@ def decode(d):
 
 
 def interpret(steps, rails_max, sbase, dbase, xg):
-    rc, shape, descs, close, csteps = xg.solo_tables(steps, rails_max, sbase, dbase)
+    rc, shape, descs, close, csteps, rows = xg.solo_tables(steps, rails_max, sbase, dbase)
     assert rc == 0, (rc, shape)
     R, npc, nr = shape["rails"], shape["npieces"], shape["nrows"]
     n = len(steps)
@@ -54,6 +54,7 @@ def interpret(steps, rails_max, sbase, dbase, xg):
                     assert so == 0 and do == 0
                     continue
                 assert row < nr - K, "a piece in the spare chunk is never stored"
+                assert row < rows[r], "the kernel stops after the rows the table says are real"
                 real += 1
                 key = (sbase + so * 16, dbase + do * 16)
                 assert key in owner, key
@@ -66,8 +67,10 @@ def interpret(steps, rails_max, sbase, dbase, xg):
                 left[key].remove(fit[0])
                 assert l16 * 16 == ln
                 rail_steps.append(t)
+            assert nrow == 0 or row < rows[r], "a barrier in a row the kernel skips"
             k0 += nrow
         assert k0 == nb
+        assert rows[r] == (real + WAVES - 1) // WAVES
         assert rail_steps == sorted(rail_steps), "a rail stores its steps in order"
         # every step the rail had pieces in is closed by a barrier, or is its last one
         used = sorted(set(rail_steps))
