@@ -273,7 +273,7 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->solo_max = 32 << 20;
     env = getenv("XG_ENGINE_SOLO_MAX");
     if (env) c->solo_max = atol(env);
-    c->solo_rails = 8;                // see DESIGN.md (solo engine): one rail per XCD
+    c->solo_rails = 16;               // see DESIGN.md (solo engine): profiles/r02/rails/solo_probe.txt
     env = getenv("XG_SOLO_RAILS");
     if (env && atoi(env) > 0) c->solo_rails = std::min(atoi(env), xgk::kSoloMaxRails);
     env = getenv("XG_STEP_CHAIN");           // "0": an event after every step launch

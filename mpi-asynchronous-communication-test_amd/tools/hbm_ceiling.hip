@@ -122,3 +122,87 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipStreamDestroy(st));
     return 0;
 }
+
+// ---------------------------------------------------------------- doorbell round trip
+// How fast can the host start a waiting kernel and see its answer?  One lane polls a
+// ring word; when it reads r it writes r to a done word in host-pinned memory
+// (system scope); the host times ring store -> done seen, reps times.
+//   kind 0  ring in host-pinned coherent memory (the armed engine's doorbell)
+//   kind 1  ring in fine-grained device memory, stored by the host through its mapping
+//   kind 2  ring in uncached device memory, stored by the host through its mapping
+// Returns 4 if the device ring is not host-accessible (*us untouched).
+namespace {
+__global__ void doorbell_pingpong(unsigned *ring, unsigned *done, int reps, int dev_ring)
+{
+    if (threadIdx.x != 0) return;
+    typedef __attribute__((address_space(1))) unsigned gu;
+    for (int r = 1; r <= reps; ++r) {
+        for (unsigned spins = 0;; ++spins) {
+            const unsigned x = dev_ring ? __hip_atomic_load((gu *)ring, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                        : __hip_atomic_load((gu *)ring, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (x == (unsigned)r) break;
+            if (spins > (1u << 26)) return;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __hip_atomic_store((gu *)done, (unsigned)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+}  // namespace
+
+#include <time.h>
+static double now_s()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+extern "C" int xgt_doorbell_rtt(int device, int kind, int reps, double *us)
+{
+    if (kind < 0 || kind > 2 || reps < 1) return 3;
+    CK(hipSetDevice(device));
+    unsigned *done = nullptr, *ring = nullptr, *hring = nullptr;
+    CK(hipHostMalloc((void **)&done, 64, hipHostMallocCoherent));
+    *(volatile unsigned *)done = 0;
+    if (kind == 0) {
+        CK(hipHostMalloc((void **)&ring, 64, hipHostMallocCoherent));
+        hring = ring;
+    } else {
+        CK(hipExtMallocWithFlags((void **)&ring, 64, kind == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached));
+        CK(hipMemset(ring, 0, 64));
+        hipPointerAttribute_t at;
+        CK(hipPointerGetAttributes(&at, ring));
+        hring = (unsigned *)at.hostPointer;
+        if (!hring) {
+            CK(hipFree(ring));
+            CK(hipHostFree(done));
+            return 4;
+        }
+    }
+    *(volatile unsigned *)hring = 0;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipLaunchKernelGGL(doorbell_pingpong, dim3(1), dim3(64), 0, st, ring, done, reps + 8, kind != 0);
+    CK(hipGetLastError());
+    double tot = 0;
+    int got = 0;
+    for (int r = 1; r <= reps + 8; ++r) {
+        const double t0 = now_s();
+        __atomic_store_n(hring, (unsigned)r, __ATOMIC_SEQ_CST);
+        __builtin_ia32_sfence();
+        bool ok = true;
+        while (__atomic_load_n(done, __ATOMIC_ACQUIRE) != (unsigned)r)
+            if (now_s() - t0 > 2.0) { ok = false; break; }
+        const double t1 = now_s();
+        if (!ok) break;
+        if (r > 8) { tot += t1 - t0; ++got; }      // 8 warm-up round trips
+    }
+    CK(hipStreamSynchronize(st));
+    CK(hipStreamDestroy(st));
+    if (kind == 0) CK(hipHostFree(ring)); else CK(hipFree(ring));
+    CK(hipHostFree(done));
+    if (got != reps) return 5;
+    *us = tot / got * 1e6;
+    return 0;
+}

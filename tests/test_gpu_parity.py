@@ -159,7 +159,7 @@ def test_step_engine_matches_per_step_launches(xg, ctx, method, d):
 
 
 ENGINE_MODES = {
-    "solo_armed": {},                                           # default at README sizes (8 rails)
+    "solo_armed": {},                                           # default at README sizes (16 rails)
     "solo1_armed": {"XG_SOLO_RAILS": "1"},                      # one workgroup
     "solo3_launch": {"XG_SOLO_RAILS": "3", "XG_ENGINE_ARM": "0"},
     "solo_norelay": {"XG_SOLO_RELAY": "0"},                     # every rail polls the doorbell
@@ -172,7 +172,7 @@ ENGINE_MODES = {
 @pytest.mark.parametrize("k", [1, 3])
 @pytest.mark.parametrize("method", [6, 9, 12, 18])
 def test_step_engine_modes(xg, method, k):
-    """The README-sized chains under every engine form: solo workgroups (8, 3 or 1 rails)
+    """The README-sized chains under every engine form: solo workgroups (16, 3 or 1 rails)
     or a grid barrier per step, armed by the doorbell or launched inside the timed region, and
     the grid engine draining at every step (XG_ENGINE_DRAIN=1).  Same bytes (strong
     fingerprint, every slot against the oracle), step times ordered and within the
@@ -199,7 +199,7 @@ def test_step_engine_modes(xg, method, k):
             run = xg.MethodRun(cx, s, it=it, mode=1)
             try:
                 assert run.engine_workgroups > 0
-                rails = {"solo_armed": 8, "solo1_armed": 1, "solo3_launch": 3, "solo_launch": 8, "solo_norelay": 8}.get(name, 0)
+                rails = {"solo_armed": 16, "solo1_armed": 1, "solo3_launch": 3, "solo_launch": 16, "solo_norelay": 16}.get(name, 0)
                 assert run.engine_rails == rails, (name, run.engine_rails)
                 for _rep in range(3):
                     done, _post, wall = run.run_timed()

@@ -121,8 +121,8 @@ def test_readme_chain_plans(xg, method, k):
         steps.pop()
     srcs = [x[0] for st in steps for x in st]
     dsts = [x[1] for st in steps for x in st]
-    shape = interpret(steps, 8, min(srcs), min(dsts), xg)
-    assert shape["rails"] == 8
+    shape = interpret(steps, 16, min(srcs), min(dsts), xg)
+    assert shape["rails"] == 16
 
 
 def test_rejects(xg):
