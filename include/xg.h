@@ -117,8 +117,9 @@ int xg_plan_check(xg_plan *p);
  * launch of up to one workgroup per CU (XG_ENGINE_WG lowers it), grid barrier +
  * wall-clock stamp per step; the other steps are their own launches.
  * Small hazard-free segments run on the solo engine instead: each step's pieces
- * dealt over up to XG_SOLO_RAILS (default 16) workgroups that each keep the step
- * order with workgroup barriers and never wait for one another.
+ * dealt over up to XG_SOLO_RAILS independent rails (default 256 rails of one wave;
+ * XG_SOLO_WAVES=16: 16-wave workgroups) that each keep their own step order and
+ * never wait for one another.
  * xg_plan_engine: workgroups of the first such segment (0: none);
  * xg_plan_engine_rails: rails of the first solo segment (0: none);
  * xg_plan_engine_steps: steps inside segments (*nseg segments, *nhaz hazard

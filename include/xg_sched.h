@@ -204,25 +204,26 @@ int xg_engine_hazards(const xg_span *xfer, const int *step_begin, int nsteps, in
 /* Solo engine tables of one hazard-free run of steps (xg.h XG_SOLO_RAILS; kernels.h
  * solo_engine_kernel, whose constants must equal these).  Pieces of <= XG_SOLO_PIECE
  * bytes, every transfer 16-B aligned and within XG_SOLO_OFF_MAX 16-B units of
- * src_base / dst_base; dealt round-robin over rails = min(rails_max, pieces / 16, >= 1).
+ * src_base / dst_base; dealt round-robin over rails = min(rails_max, pieces / waves, >= 1).
  * Per rail r, npieces descriptors at descs[r * npieces]: bits 0-23 source offset,
  * 24-47 destination offset (16-B units from the bases), 48-54 length (16-B units;
  * 0 = empty padding), 55-59 `before` = how many of its row's step barriers precede
- * it.  meta: [rails][nrows + 1] barriers per row (rows of XG_SOLO_WAVES pieces), then
+ * it.  meta: [rails][nrows + 1] barriers per row (rows of `waves` pieces), then
  * [rails][nsteps] the step each barrier closes, in order, -1 past the last (a rail
  * places a barrier only after a step it had pieces in, in front of its next piece),
  * then [rails] the rows that hold real pieces (the rest is padding, never executed).
  * descs / meta NULL: fill *shape only.  Returns 0, or XG_EARG (xg.h) for bad input or
  * npieces > XG_SOLO_MAX_PIECES (*shape still filled), XG_ENOMEM. */
-#define XG_SOLO_WAVES 16
+#define XG_SOLO_WAVES 16         /* waves of a workgroup rail; `waves` = 1: every rail one wave */
+#define XG_SOLO_MAX_RAILS 512
 #define XG_SOLO_PIECE 1024
 #define XG_SOLO_K 8
 #define XG_SOLO_MAX_STEPS 2048
 #define XG_SOLO_MAX_PIECES 4608
 #define XG_SOLO_OFF_MAX (1ull << 24)
 typedef struct { int32_t rails, npieces, nrows, nmeta; } xg_solo_shape;
-int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, uint64_t src_base,
-                   uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta);
+int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, int waves,
+                   uint64_t src_base, uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta);
 
 /* fill: `nsegs` consecutive d-byte segments at `off` in the SEND region,
  * segment i = fingerprint(rank, seed0 + i, iter) (prepare_*_data loops). */

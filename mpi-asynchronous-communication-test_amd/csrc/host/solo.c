@@ -2,8 +2,8 @@
  * solo.c -- the solo step engine's tables (kernels.h solo_engine_kernel,
  * include/xg_sched.h xg_solo_tables): a hazard-free run of steps cut into
  * 1 KiB pieces, dealt round-robin over R rails (workgroups), and per rail laid
- * out as rows of XG_SOLO_WAVES pieces with the step barriers placed between
- * them.
+ * out as rows of `waves` pieces (one per wave of the rail's workgroup: 16, or
+ * 1 for rails of a single wave) with the step barriers placed between them.
  *
  * A rail closes a step with a workgroup barrier only if it had pieces in it:
  * the barrier sits in front of the rail's next piece -- in that piece's row,
@@ -11,7 +11,7 @@
  * row, and in the row's barrier count -- and the step it closes is listed in
  * order; a barrier in front of the rail's end is left to the kernel's closing
  * stamp.  Each barrier precedes a distinct piece, so a row holds at most
- * XG_SOLO_WAVES of them (the 5-bit `before` field).  A rail's table is padded
+ * `waves` of them (the 5-bit `before` field).  A rail's table is padded
  * with empty pieces to an even number of chunks of XG_SOLO_K rows plus one
  * spare chunk (the kernel's double-buffered loop loads one chunk past the
  * last without a branch); the kernel stops after the rows that hold real
@@ -25,11 +25,14 @@
 
 static uint64_t desc(uint64_t src16, uint64_t dst16, uint64_t len16) { return src16 | (dst16 << 24) | (len16 << 48); }
 
-int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, uint64_t src_base,
-                   uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta)
+int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, int waves,
+                   uint64_t src_base, uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta)
 {
-    if (!xfer || !step_begin || !shape || nsteps < 1 || nsteps > XG_SOLO_MAX_STEPS || rails_max < 1) return XG_EARG;
+    if (!xfer || !step_begin || !shape || nsteps < 1 || nsteps > XG_SOLO_MAX_STEPS || rails_max < 1 ||
+        rails_max > XG_SOLO_MAX_RAILS || (waves != 1 && waves != XG_SOLO_WAVES))
+        return XG_EARG;
     const int nx = step_begin[nsteps];
+    const int W = waves;       /* pieces per row: one per wave of a rail */
     int64_t total = 0;
     for (int i = 0; i < nx; ++i) {
         const xg_span *x = &xfer[i];
@@ -39,16 +42,16 @@ int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int r
             return XG_EARG;
         total += (int64_t)((x->len + XG_SOLO_PIECE - 1) / XG_SOLO_PIECE);
     }
-    int64_t r = total / XG_SOLO_WAVES;
+    int64_t r = total / W;
     if (r > rails_max) r = rails_max;
     if (r < 1) r = 1;
     const int rails = (int)r;
-    const int64_t chunk = (int64_t)XG_SOLO_WAVES * XG_SOLO_K;
+    const int64_t chunk = (int64_t)W * XG_SOLO_K;
     const int64_t longest = (total + rails - 1) / rails;     /* round-robin: counts differ by <= 1 */
     const int64_t np = ((longest + 2 * chunk - 1) / (2 * chunk) * 2 + 1) * chunk;
     shape->rails = rails;
     shape->npieces = (int)(np > XG_SOLO_MAX_PIECES ? XG_SOLO_MAX_PIECES + 1 : np);
-    shape->nrows = (int)(np / XG_SOLO_WAVES);
+    shape->nrows = (int)(np / W);
     shape->nmeta = rails * (shape->nrows + 1) + rails * nsteps + rails;
     if (np > XG_SOLO_MAX_PIECES) return XG_EARG;
     if (!descs || !meta) return XG_OK;
@@ -76,11 +79,11 @@ int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int r
                 const uint64_t len = xfer[i].len - o < XG_SOLO_PIECE ? xfer[i].len - o : XG_SOLO_PIECE;
                 /* a barrier still open on this rail goes in front of this piece */
                 if (pend[cur] >= 0) {
-                    const int64_t at = pend[cur], row = at / XG_SOLO_WAVES;
+                    const int64_t at = pend[cur], row = at / W;
                     close[(size_t)cur * (nrows + 1) + row]++;
                     cstep[(size_t)cur * nsteps + nb[cur]++] = pstep[cur];
-                    for (int64_t w = at % XG_SOLO_WAVES; w < XG_SOLO_WAVES; ++w)
-                        descs[(size_t)cur * np + row * XG_SOLO_WAVES + w] += 1ull << 55;
+                    for (int64_t w = at % W; w < W; ++w)
+                        descs[(size_t)cur * np + row * W + w] += 1ull << 55;
                     pend[cur] = -1;
                 }
                 descs[(size_t)cur * np + cnt[cur]++] +=     /* its `before` bits may be set already */
@@ -95,7 +98,7 @@ int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int r
             }
     }
     int *rows = cstep + (size_t)rails * nsteps;               /* rows holding real pieces */
-    for (int q = 0; q < rails; ++q) rows[q] = (int)((cnt[q] + XG_SOLO_WAVES - 1) / XG_SOLO_WAVES);
+    for (int q = 0; q < rails; ++q) rows[q] = (int)((cnt[q] + W - 1) / W);
     free(cnt); free(nb); free(used); free(pend); free(pstep);
     return XG_OK;
 }

@@ -350,9 +350,18 @@ struct EngineState {
     // solo engine, armed launches (cumulative counters; a launch adds one per rail):
     unsigned rails;     // rails finished: the last of a launch rings `done`
     unsigned arrive;    // rails resident: the last lets rail 0 announce `ready`
-    unsigned go;        // relay: rail 0 saw the ring of this epoch
-    unsigned pad[3];
+    unsigned pad[4];
+    // relay: rail 0 saw the ring of this epoch -- written to kGoLines separate 128-B lines
+    // at once (one store per lane), rail r polls line r % kGoLines, so hundreds of
+    // polling rails do not queue on one L2 line
+    unsigned go[16][32];
+    // rails finished, counted on the same 16 lines (rail r on line r % 16); the last of
+    // a line counts on `rails`, the last of those rings `done` (two short queues of
+    // atomics instead of one of R)
+    unsigned fin[16][32];
 };
+constexpr int kGoLines = 16;
+
 
 template <int B>
 __device__ __forceinline__ void burst_load16(const uint8_t *src, int64_t len, u32x4 *v)
@@ -413,6 +422,20 @@ __device__ __forceinline__ bool poll_word(g_u32 *w, unsigned v, g_u32 *tmo)
         if (spins > kRingSpins || __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
         __builtin_amdgcn_s_sleep(1);
     }
+}
+
+// lane 0 of a finished rail: count it; the launch's last rail tells the host
+__device__ __forceinline__ void rail_finished(EngineState *st, int rail, int R, Doorbell *db, unsigned epoch)
+{
+    const int L = R < kGoLines ? R : kGoLines;
+    const int line = rail % L;
+    const unsigned per_line = (unsigned)((R - line - 1) / L + 1);     // rails on this line
+    const unsigned a = __hip_atomic_fetch_add((g_u32 *)&st->fin[line][0], 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (a % per_line) return;
+    const unsigned b = __hip_atomic_fetch_add((g_u32 *)&st->rails, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (b % (unsigned)L == 0) ring_done(db, epoch);
 }
 
 // B: 16-B loads per lane per unit -> units of B * 4 KiB (the host cuts the step's
@@ -545,7 +568,10 @@ __global__ __launch_bounds__(kThreads) void step_engine_kernel(const DCopy *__re
 // nothing in step s carries its previous stamp; the host reduces).  Like flag 0 of
 // the grid engine a stamp is the time the stores were issued; the last step waits
 // for its stores (delivered time).  One CU moves ~120 GB/s of load + store
-// traffic, so R rails lift the single-workgroup bound R-fold.
+// traffic, so R rails lift the single-workgroup bound R-fold.  A rail is a
+// workgroup of WV = 16 waves (rows of 16 pieces, workgroup barriers between
+// steps) or a single wave (WV = 1: rows of one piece; a wave's stores issue in
+// program order, so its step boundaries cost no barrier at all).
 constexpr int kSoloWaves = 16;
 constexpr int kSoloThreads = kSoloWaves * 64;
 constexpr int kSoloPiece = 64 * 16;              // bytes per wave per row
@@ -565,7 +591,7 @@ __host__ __device__ constexpr unsigned long long solo_desc(uint64_t src16, uint6
     return src16 | (dst16 << 24) | (len16 << 48) | (before << 55);
 }
 constexpr uint64_t kSoloOffMax = 1ull << 24;     // offsets < 256 MiB from the bases
-constexpr int kSoloMaxRails = 16;
+constexpr int kSoloMaxRails = 512;
 
 // Host contract (build_segments), per rail r of R = gridDim.x: pieces
 // desc[r * npieces ..], every piece 16-B aligned, <= 1 KiB, within 256 MiB of the
@@ -585,13 +611,13 @@ struct SoloChunk {
     u32x4 v[K];
 };
 
-// issue the K 16-B loads of chunk c of this wave
-template <int K>
+// issue the K 16-B loads of chunk c of this wave (rows of WV pieces)
+template <int K, int WV>
 __device__ __forceinline__ void solo_load(SoloChunk<K> &b, const unsigned long long *ldesc, int c, int wave,
                                           uint64_t l16, const uint8_t *src_base)
 {
 #pragma unroll
-    for (int k = 0; k < K; ++k) b.d[k] = ldesc[(c * K + k) * kSoloWaves + wave];
+    for (int k = 0; k < K; ++k) b.d[k] = ldesc[(c * K + k) * WV + wave];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         // the descriptor is wave-uniform: a buffer resource in SGPRs whose range check
@@ -636,8 +662,8 @@ __device__ __forceinline__ void solo_store(const SoloChunk<K> &b, const unsigned
     }
 }
 
-template <int K>
-__global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigned long long *__restrict__ desc,
+template <int K, int WV>
+__global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned long long *__restrict__ desc,
                                                                    int npieces, const uint8_t *src_base,
                                                                    uint8_t *dst_base, const int *__restrict__ meta,
                                                                    int nsteps, EngineState *st,
@@ -647,27 +673,29 @@ __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigne
     const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
     const int rail = (int)blockIdx.x, R = (int)gridDim.x;
     __shared__ unsigned long long ldesc[kSoloMaxPieces];
-    __shared__ unsigned short lclose[kSoloMaxPieces / kSoloWaves + 1];
+    __shared__ unsigned short lclose[kSoloMaxPieces / WV + 1];
     __shared__ short lcstep[kSoloMaxSteps];
     __shared__ unsigned long long ts[kSoloMaxSteps];
     __shared__ int give_up;
-    const int nrows = npieces / kSoloWaves;
+    constexpr int kT = WV * 64;
+    const int nrows = npieces / WV;
     desc += (size_t)rail * npieces;
     const int *row_close = meta + rail * (nrows + 1);
     const int *cstep = meta + R * (nrows + 1) + rail * nsteps;
     const int rows = meta[R * (nrows + 1) + R * nsteps + rail];     // rows holding real pieces
     const int nreal = (rows + K - 1) / K;                              // ... in that many chunks
-    for (int i = (int)threadIdx.x; i < npieces; i += kSoloThreads) ldesc[i] = desc[i];
-    for (int i = (int)threadIdx.x; i <= nrows; i += kSoloThreads) lclose[i] = (unsigned short)row_close[i];
-    for (int i = (int)threadIdx.x; i < nsteps; i += kSoloThreads) {
+    for (int i = (int)threadIdx.x; i < npieces; i += kT) ldesc[i] = desc[i];
+    for (int i = (int)threadIdx.x; i <= nrows; i += kT) lclose[i] = (unsigned short)row_close[i];
+    for (int i = (int)threadIdx.x; i < nsteps; i += kT) {
         lcstep[i] = (short)cstep[i];
         ts[i] = 0;
     }
     // armed: every rail resident, then rail 0 announces `ready`; the ring reaches the
     // rails either each through its own poll of host memory, or (relay) through rail 0,
     // which alone polls the host and passes the epoch on in device memory
+    __shared__ int relay_now;
     if (threadIdx.x == 0) {
-        bool ok = true;
+        bool ok = true, relay_go = false;
         if (db) {
             g_u32 *tmo = (g_u32 *)&st->tmo;
             const unsigned old = __hip_atomic_fetch_add((g_u32 *)&st->arrive, 1u, __ATOMIC_RELAXED,
@@ -681,21 +709,21 @@ __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigne
                 }
                 ok = ok && wait_ring(db, epoch);
                 if (!ok) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else if (relay) __hip_atomic_store((g_u32 *)&st->go, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (relay) relay_go = true;
             } else {
-                ok = relay ? poll_word<false>((g_u32 *)&st->go, epoch, tmo) : poll_word<true>((g_u32 *)&db->ring, epoch, tmo);
+                ok = relay ? poll_word<false>((g_u32 *)&st->go[rail % kGoLines][0], epoch, tmo)
+                           : poll_word<true>((g_u32 *)&db->ring, epoch, tmo);
                 if (!ok) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         give_up = !ok;
+        relay_now = relay_go;
     }
     __syncthreads();
+    if (relay_now && threadIdx.x < kGoLines)   // one store per lane: every relay line at once
+        __hip_atomic_store((g_u32 *)&st->go[threadIdx.x][0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (give_up) {
-        if (threadIdx.x == 0) {      // still counted, so that the launch's last rail rings `done`
-            const unsigned done = __hip_atomic_fetch_add((g_u32 *)&st->rails, 1u, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT) + 1;
-            if (done % (unsigned)R == 0) ring_done(db, epoch);
-        }
+        if (threadIdx.x == 0) rail_finished(st, rail, R, db, epoch);   // still counted
         return;
     }
     const uint64_t l16 = (uint64_t)lane;
@@ -705,12 +733,12 @@ __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigne
     // the loop leaves after the last chunk that holds real pieces.
     SoloChunk<K> A, B;
     int k = 0;
-    solo_load<K>(A, ldesc, 0, wave, l16, src_base);
+    solo_load<K, WV>(A, ldesc, 0, wave, l16, src_base);
     for (int c = 0; c < nreal; c += 2) {
-        solo_load<K>(B, ldesc, c + 1, wave, l16, src_base);
+        solo_load<K, WV>(B, ldesc, c + 1, wave, l16, src_base);
         solo_store<K>(A, lclose, lcstep, ts, k, c, rows, l16, dst_base);
         if (c + 1 >= nreal) break;
-        solo_load<K>(A, ldesc, c + 2, wave, l16, src_base);
+        solo_load<K, WV>(A, ldesc, c + 2, wave, l16, src_base);
         solo_store<K>(B, lclose, lcstep, ts, k, c + 1, rows, l16, dst_base);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this rail's last steps: delivered
@@ -718,14 +746,10 @@ __global__ __launch_bounds__(kSoloThreads) void solo_engine_kernel(const unsigne
     if (threadIdx.x == 0) {
         const unsigned long long t = (unsigned long long)wall_clock64();
         for (int s = k > 0 ? lcstep[k - 1] + 1 : 0; s < nsteps; ++s) ts[s] = t;
-        if (db) {      // the last rail to finish tells the host
-            const unsigned done = __hip_atomic_fetch_add((g_u32 *)&st->rails, 1u, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT) + 1;
-            if (done % (unsigned)R == 0) ring_done(db, epoch);
-        }
+        if (db) rail_finished(st, rail, R, db, epoch);      // the last rail to finish tells the host
     }
     __syncthreads();
-    for (int i = (int)threadIdx.x; i < nsteps; i += kSoloThreads) stamps[(size_t)rail * stride + i] = ts[i];
+    for (int i = (int)threadIdx.x; i < nsteps; i += kT) stamps[(size_t)rail * stride + i] = ts[i];
 }
 
 // ---------------------------------------------------------------- displacement scan

@@ -58,7 +58,8 @@ struct xg_ctx {
     int engine_drain;          // 1: always drain before each barrier arrival (XG_ENGINE_DRAIN=1)
     int solo;                  // 0: never use the solo engine
     int64_t solo_max;          // solo segments move <= this many bytes per run
-    int solo_rails;            // solo segments deal their pieces over up to this many workgroups
+    int solo_rails;            // solo segments deal their pieces over up to this many rails
+    int solo_waves;            // waves per rail: 16 (a workgroup) or 1
     int solo_relay;            // armed solo: rail 0 alone polls the doorbell and relays the ring
     int step_chain;            // 1: time runs of one-launch local steps by in-kernel stamps (xg_plan_run)
     int engine_arm;            // 1: xg_plan_run arms single-segment plans (doorbell)
@@ -108,7 +109,8 @@ struct EngSeg {
                                    // (solo: per rail nrows + 1 row barrier counts, then per rail
                                    // n closed-step indices)
     int nhaz;                      // hazard points (xg_engine_hazards flag 2)
-    bool solo;                     // one workgroup (solo_engine_kernel), pieces from u0
+    bool solo;                     // solo engine (solo_engine_kernel), pieces from u0
+    int wv;                        // solo: waves per rail (16 or 1)
     int u0;                        // first unit / piece of the segment in d_epieces
     int npieces;                   // solo: pieces per rail (whole chunks of rows), rail r's from u0 + r * npieces
                                    // in d_solo; w = rails
@@ -273,7 +275,10 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->solo_max = 32 << 20;
     env = getenv("XG_ENGINE_SOLO_MAX");
     if (env) c->solo_max = atol(env);
-    c->solo_rails = 16;               // see DESIGN.md (solo engine): profiles/r02/rails/solo_probe.txt
+    env = getenv("XG_SOLO_WAVES");           // waves per rail: 1 (default) or 16
+    c->solo_waves = env && atoi(env) == xgk::kSoloWaves ? xgk::kSoloWaves : 1;
+    // see DESIGN.md (solo engine): profiles/r02/rails/solo_probe.txt
+    c->solo_rails = c->solo_waves == 1 ? 256 : 16;
     env = getenv("XG_SOLO_RAILS");
     if (env && atoi(env) > 0) c->solo_rails = std::min(atoi(env), xgk::kSoloMaxRails);
     env = getenv("XG_STEP_CHAIN");           // "0": an event after every step launch
@@ -553,21 +558,23 @@ static bool engine_step(const xg_ctx *c, const StepR &st)
 // over up to one workgroup per CU with bytes enough in flight
 // (profiles/r01_engine_sweep.txt: small units starve big steps, big units leave
 // small steps on a handful of workgroups).  Barrier flags: xg_engine_hazards.
-static_assert(xgk::kSoloWaves == XG_SOLO_WAVES && xgk::kSoloPiece == XG_SOLO_PIECE && xgk::kSoloK == XG_SOLO_K &&
+static_assert(xgk::kSoloWaves == XG_SOLO_WAVES && xgk::kSoloMaxRails == XG_SOLO_MAX_RAILS &&
+                  xgk::kSoloPiece == XG_SOLO_PIECE && xgk::kSoloK == XG_SOLO_K &&
                   xgk::kSoloMaxSteps == XG_SOLO_MAX_STEPS && xgk::kSoloMaxPieces == XG_SOLO_MAX_PIECES &&
                   xgk::kSoloOffMax == XG_SOLO_OFF_MAX,
               "solo engine constants: kernels.h and xg_sched.h disagree");
 
 // Solo or grid engine for a hazard-free segment of n steps (`busy` of them move
 // bytes) moving `bytes`: the cheaper by a model of the measured costs (MI355X,
-// profiles/r02/solo_probe_steps.txt, rails.txt): a rail (one CU) moves ~120 GB/s of
-// load + store traffic and closes a step in ~0.2 us; the grid engine moves at the
-// copy kernels' ~5 TB/s but pays ~1 us of device-scope barrier per step; a lone
-// busy step outside the engine is a copy launch inside the timed region (~8 us).
-static bool solo_pays(int64_t bytes, int n, int rails, int busy)
+// profiles/r02/rails/solo_probe.txt): a workgroup rail (one CU) moves ~120 GB/s of
+// load + store traffic and closes a step in ~0.2 us, a one-wave rail ~15 GB/s and
+// ~0.05 us; the grid engine moves at the copy kernels' ~5 TB/s but pays ~1 us of
+// device-scope barrier per step; a lone busy step outside the engine is a copy
+// launch inside the timed region (~8 us).
+static bool solo_pays(int64_t bytes, int n, int rails, int wv, int busy)
 {
     const double traffic = 2.0 * (double)bytes;
-    const double solo = traffic / (rails * 120e9) + n * 0.2e-6;
+    const double solo = wv == 1 ? traffic / (rails * 15e9) + n * 0.05e-6 : traffic / (rails * 120e9) + n * 0.2e-6;
     const double grid = traffic / 5e12 + n * 1.0e-6 + (busy < 2 ? 8e-6 : 0.0);
     return solo < grid;
 }
@@ -652,8 +659,11 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
             }
         xg_solo_shape sh{};
         const bool fits = aligned && shi > slo && dhi > dlo && n <= xgk::kSoloMaxSteps &&
-                          xg_solo_tables(spans.data(), tb.data(), n, c->solo_rails, slo, dlo, &sh, nullptr, nullptr) == XG_OK;
-        g.solo = g.nhaz == 0 && fits && c->solo && g.bytes <= c->solo_max && solo_pays(g.bytes, n, sh.rails, busy);
+                          xg_solo_tables(spans.data(), tb.data(), n, c->solo_rails, c->solo_waves, slo, dlo, &sh, nullptr,
+                                         nullptr) == XG_OK;
+        g.solo = g.nhaz == 0 && fits && c->solo && g.bytes <= c->solo_max &&
+                 solo_pays(g.bytes, n, sh.rails, c->solo_waves, busy);
+        g.wv = c->solo_waves;
         if (!g.solo && busy < 2) {      // one busy step: an engine launch only if it runs solo
             ep.resize(u0);
             s = run_end;
@@ -668,7 +678,7 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
             g.npieces = sh.npieces;
             std::vector<int> meta(sh.nmeta);
             p->solo_desc.resize(g.u0 + (size_t)sh.rails * sh.npieces);
-            if (xg_solo_tables(spans.data(), tb.data(), n, c->solo_rails, slo, dlo, &sh,
+            if (xg_solo_tables(spans.data(), tb.data(), n, c->solo_rails, c->solo_waves, slo, dlo, &sh,
                                reinterpret_cast<uint64_t *>(p->solo_desc.data()) + g.u0, meta.data()) != XG_OK)
                 return XG_EARG;
             sb.insert(sb.end(), meta.begin(), meta.end());
@@ -1153,9 +1163,13 @@ static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream, bool arme
     if ((rc = kt_before(c, stream, &kt))) return rc;
     unsigned long long *stamps = reinterpret_cast<unsigned long long *>(p->d_engine + 1) + g.s0;
     const int *sb = p->d_sb + g.sb_off;
-    if (g.solo)
-        hipLaunchKernelGGL(xgk::solo_engine_kernel<xgk::kSoloK>, dim3(g.w), dim3(xgk::kSoloThreads), 0, stream,
+    if (g.solo && g.wv == 1)
+        hipLaunchKernelGGL((xgk::solo_engine_kernel<xgk::kSoloK, 1>), dim3(g.w), dim3(64), 0, stream,
                            p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
+                           db, epoch, c->solo_relay);
+    else if (g.solo)
+        hipLaunchKernelGGL((xgk::solo_engine_kernel<xgk::kSoloK, xgk::kSoloWaves>), dim3(g.w), dim3(xgk::kSoloThreads), 0,
+                           stream, p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
                            db, epoch, c->solo_relay);
     else if (g.b == 1)
         hipLaunchKernelGGL(xgk::step_engine_kernel<1>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb, n,

@@ -10,8 +10,10 @@ import __graft_entry__ as G
 xg = G.load_package().xg
 P, A, d, c = [int(x) for x in os.environ.get("PROBE_CFG", "32,14,2048,3").split(",")]
 rl = xg.aggregator_list(P, A)
-modes = {"solo_armed": {}, "solo_norelay": {"XG_SOLO_RELAY": "0"}, "solo1_armed": {"XG_SOLO_RAILS": "1"},
-         "solo4_armed": {"XG_SOLO_RAILS": "4"}, "solo8_armed": {"XG_SOLO_RAILS": "8"},
+modes = {"solo_armed": {}, "solo64_armed": {"XG_SOLO_RAILS": "64"}, "solo512_armed": {"XG_SOLO_RAILS": "512"},
+         "solo1_armed": {"XG_SOLO_RAILS": "1"}, "solo_norelay": {"XG_SOLO_RELAY": "0", "XG_SOLO_RAILS": "16"},
+         "wg16_armed": {"XG_SOLO_WAVES": "16"}, "wg4_armed": {"XG_SOLO_WAVES": "16", "XG_SOLO_RAILS": "4"},
+         "wg1_armed": {"XG_SOLO_WAVES": "16", "XG_SOLO_RAILS": "1"},
          "grid_armed": {"XG_ENGINE_SOLO": "0"}, "solo_launch": {"XG_ENGINE_ARM": "0"}}
 if os.environ.get("PROBE_MODES"):
     modes = {k: v for k, v in modes.items() if k in os.environ["PROBE_MODES"].split(",")}

@@ -159,10 +159,12 @@ def test_step_engine_matches_per_step_launches(xg, ctx, method, d):
 
 
 ENGINE_MODES = {
-    "solo_armed": {},                                           # default at README sizes (16 rails)
-    "solo1_armed": {"XG_SOLO_RAILS": "1"},                      # one workgroup
-    "solo3_launch": {"XG_SOLO_RAILS": "3", "XG_ENGINE_ARM": "0"},
-    "solo_norelay": {"XG_SOLO_RELAY": "0"},                     # every rail polls the doorbell
+    "solo_armed": {},                                           # default at README sizes: 256 one-wave rails
+    "solo64_armed": {"XG_SOLO_RAILS": "64"},
+    "solo37_launch": {"XG_SOLO_RAILS": "37", "XG_ENGINE_ARM": "0"},
+    "solo_norelay": {"XG_SOLO_RELAY": "0", "XG_SOLO_RAILS": "16"},   # every rail polls the doorbell
+    "wg_armed": {"XG_SOLO_WAVES": "16"},                        # 16 workgroup rails of 16 waves
+    "wg1_launch": {"XG_SOLO_WAVES": "16", "XG_SOLO_RAILS": "1", "XG_ENGINE_ARM": "0"},
     "grid_armed": {"XG_ENGINE_SOLO": "0"},
     "solo_launch": {"XG_ENGINE_ARM": "0"},
     "grid_drain": {"XG_ENGINE_SOLO": "0", "XG_ENGINE_DRAIN": "1", "XG_ENGINE_ARM": "0"},
@@ -172,7 +174,7 @@ ENGINE_MODES = {
 @pytest.mark.parametrize("k", [1, 3])
 @pytest.mark.parametrize("method", [6, 9, 12, 18])
 def test_step_engine_modes(xg, method, k):
-    """The README-sized chains under every engine form: solo workgroups (16, 3 or 1 rails)
+    """The README-sized chains under every engine form: solo rails (one-wave or 16-wave)
     or a grid barrier per step, armed by the doorbell or launched inside the timed region, and
     the grid engine draining at every step (XG_ENGINE_DRAIN=1).  Same bytes (strong
     fingerprint, every slot against the oracle), step times ordered and within the
@@ -199,7 +201,8 @@ def test_step_engine_modes(xg, method, k):
             run = xg.MethodRun(cx, s, it=it, mode=1)
             try:
                 assert run.engine_workgroups > 0
-                rails = {"solo_armed": 16, "solo1_armed": 1, "solo3_launch": 3, "solo_launch": 16, "solo_norelay": 16}.get(name, 0)
+                rails = {"solo_armed": 256, "solo64_armed": 64, "solo37_launch": 37, "solo_norelay": 16, "wg_armed": 16,
+                         "wg1_launch": 1, "solo_launch": 256}.get(name, 0)
                 assert run.engine_rails == rails, (name, run.engine_rails)
                 for _rep in range(3):
                     done, _post, wall = run.run_timed()

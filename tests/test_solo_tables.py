@@ -10,15 +10,16 @@ import random
 import pytest
 
 
-WAVES, PIECE, K, MAXP = 16, 1024, 8, 4608
+PIECE, K, MAXP = 1024, 8, 4608
 
 
 def decode(d):
     return d & 0xFFFFFF, (d >> 24) & 0xFFFFFF, (d >> 48) & 127, d >> 55
 
 
-def interpret(steps, rails_max, sbase, dbase, xg):
-    rc, shape, descs, close, csteps, rows = xg.solo_tables(steps, rails_max, sbase, dbase)
+def interpret(steps, rails_max, sbase, dbase, xg, WAVES=16):
+    """WAVES: pieces per row = waves per rail (16: a workgroup; 1: a single wave)"""
+    rc, shape, descs, close, csteps, rows = xg.solo_tables(steps, rails_max, sbase, dbase, waves=WAVES)
     assert rc == 0, (rc, shape)
     R, npc, nr = shape["rails"], shape["npieces"], shape["nrows"]
     n = len(steps)
@@ -95,19 +96,20 @@ def random_steps(rng, nsteps, sbase, dbase):
 
 
 @pytest.mark.parametrize("seed", range(12))
-@pytest.mark.parametrize("rails", [1, 3, 8, 16])
-def test_random_segments(xg, seed, rails):
-    rng = random.Random(seed * 31 + rails)
+@pytest.mark.parametrize("rails,waves", [(1, 16), (3, 16), (8, 16), (16, 16), (1, 1), (7, 1), (64, 1), (256, 1)])
+def test_random_segments(xg, seed, rails, waves):
+    rng = random.Random(seed * 31 + rails + waves)
     sbase, dbase = 1 << 32, 3 << 32
     steps = random_steps(rng, rng.randint(1, 60), sbase, dbase)
     if not any(steps):
         steps[0].append((sbase, dbase, 4096))
-    interpret(steps, rails, sbase, dbase, xg)
+    interpret(steps, rails, sbase, dbase, xg, WAVES=waves)
 
 
 @pytest.mark.parametrize("method", [6, 9, 10, 11, 12, 18])
 @pytest.mark.parametrize("k", [1, 3])
-def test_readme_chain_plans(xg, method, k):
+@pytest.mark.parametrize("rails,waves", [(16, 16), (256, 1)])
+def test_readme_chain_plans(xg, method, k, rails, waves):
     """the G = 1 plans of the README configuration (P32 A14 d2048 c3), as build_segments
     hands them over: one transfer per local copy, SEND and RECV at 1 GiB apart"""
     P, A, d, c = 32, 14, 2048, 3
@@ -121,8 +123,8 @@ def test_readme_chain_plans(xg, method, k):
         steps.pop()
     srcs = [x[0] for st in steps for x in st]
     dsts = [x[1] for st in steps for x in st]
-    shape = interpret(steps, 16, min(srcs), min(dsts), xg)
-    assert shape["rails"] == 16
+    shape = interpret(steps, rails, min(srcs), min(dsts), xg, WAVES=waves)
+    assert shape["rails"] == rails
 
 
 def test_rejects(xg):
@@ -138,4 +140,8 @@ def test_rejects(xg):
     rc, shape, *_ = xg.solo_tables([[(sb, db, 1024 * MAXP * 2)]], 8, sb, db)    # ... which rails spread
     assert rc == 0 and shape["rails"] == 8
     rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]] * 2049, 8, sb, db)         # too many steps
+    assert rc == 3
+    rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 8, sb, db, waves=4)       # rails are 16 waves or 1
+    assert rc == 3
+    rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 513, sb, db, waves=1)     # at most 512 rails
     assert rc == 3
