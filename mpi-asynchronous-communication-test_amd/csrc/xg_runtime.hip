@@ -165,12 +165,14 @@ struct xg_plan {
 // non-temporal loads/stores (6) when the bytes cannot come back from the 256 MiB
 // Infinity Cache: a launch whose own source + destination exceed it, or a launch of
 // >= nt_stream bytes in a plan whose run copies more than it (every step then finds
-// its bytes evicted by the steps before); plain (1) otherwise.
-static int copy_variant(const xg_plan *p, int64_t bytes)
+// its bytes evicted by the steps before) -- unless what it writes is read again at
+// once (`reread`: packs feeding RCCL, TAM stage copies), which then may still find
+// it in the cache; plain (1) otherwise.
+static int copy_variant(const xg_plan *p, int64_t bytes, bool reread = false)
 {
     if (p->variant) return p->variant;
     const xg_ctx *c = p->ctx;
-    return bytes >= c->nt_min || (p->streaming && c->nt_stream > 0 && bytes >= c->nt_stream) ? 6 : 1;
+    return bytes >= c->nt_min || (!reread && p->streaming && c->nt_stream > 0 && bytes >= c->nt_stream) ? 6 : 1;
 }
 
 extern "C" double xg_now(void)
@@ -1028,10 +1030,11 @@ extern "C" int xg_plan_displs(const xg_plan *p, int64_t *out, int n)
 // one keeps the default policy, which re-runs serve from the cache
 // (profiles/r02/copy_nt_sizes.txt).  1..6 force one form (A/B, tests).
 // start: stamp the launch's start there (variants 1 and 6 only; see copy_kernel_g)
-static int launch_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t st, unsigned long long *start = nullptr)
+static int launch_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t st, unsigned long long *start = nullptr,
+                       bool reread = false)
 {
     const xgk::DCopy *pc = p->d_pieces + b;
-    const int v = copy_variant(p, bytes);
+    const int v = copy_variant(p, bytes, reread);
     if (start && v != 1 && v != 6) return XG_EARG;
     switch (v) {
     case 2: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxPlain>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
@@ -1067,12 +1070,12 @@ static int kt_after(xg_ctx *c, hipStream_t stream, bool kt, int64_t bytes)
 }
 
 // one copy launch, bracketed by kernel-timing events when a per-launch session is on
-static int timed_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t stream)
+static int timed_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t stream, bool reread = false)
 {
     int rc;
     bool kt;
     if ((rc = kt_before(p->ctx, stream, &kt))) return rc;
-    if ((rc = launch_copy(p, b, n, bytes, stream))) return rc;
+    if ((rc = launch_copy(p, b, n, bytes, stream, nullptr, reread))) return rc;
     return kt_after(p->ctx, stream, kt, bytes);
 }
 
@@ -1086,10 +1089,11 @@ static int enqueue_pre(xg_plan *p, int s, hipStream_t stream, hipStream_t side)
 {
     const StepR &st = p->steps[s];
     int rc;
-    if (st.stage_n && (rc = timed_copy(p, st.stage_b, st.stage_n, st.stage_bytes, stream))) return rc;
+    if (st.stage_n && (rc = timed_copy(p, st.stage_b, st.stage_n, st.stage_bytes, stream, true))) return rc;
     if (st.fused) {
         const StepR &pv = p->steps[s - 1];
-        if ((rc = timed_copy(p, pv.post_b, pv.post_n + st.pack_n, pv.post_bytes + st.pack_bytes, stream))) return rc;
+        if ((rc = timed_copy(p, pv.post_b, pv.post_n + st.pack_n, pv.post_bytes + st.pack_bytes, stream, true)))
+            return rc;
         if (p->rec_ev) HIPCHK(hipEventRecord(p->ev[s - 1], stream));
     }
     if (st.split) {
@@ -1097,9 +1101,9 @@ static int enqueue_pre(xg_plan *p, int s, hipStream_t stream, hipStream_t side)
         HIPCHK(hipStreamWaitEvent(side, p->fork[s], 0));
         if ((rc = timed_copy(p, st.local_b, st.local_n, st.local_bytes, side))) return rc;
         HIPCHK(hipEventRecord(p->join[s], side));
-        if (!st.fused && st.pack_n && (rc = timed_copy(p, st.pack_b, st.pack_n, st.pack_bytes, stream))) return rc;
+        if (!st.fused && st.pack_n && (rc = timed_copy(p, st.pack_b, st.pack_n, st.pack_bytes, stream, true))) return rc;
     } else if (!st.fused && st.pre_n &&
-               (rc = timed_copy(p, st.local_b, st.pre_n, st.local_bytes + st.pack_bytes, stream))) {
+               (rc = timed_copy(p, st.local_b, st.pre_n, st.local_bytes + st.pack_bytes, stream, st.pack_n > 0))) {
         return rc;
     }
     return XG_OK;
