@@ -12,6 +12,9 @@
 //   kind 7  one 256 KiB span per workgroup, 4 x 16-B loads in flight per lane
 //   kind 8  copy_kernel_g<4> over 64 KiB pieces
 //   kind 9  copy_kernel_g<4, nt> over 32 KiB pieces (non-temporal loads and stores)
+//   kind 10 read-only stream, non-temporal loads      kind 11 write-only stream, non-temporal stores
+//   kind 12 grid-stride copy, nt loads + plain stores   kind 13 grid-stride copy, plain loads + nt stores
+//   kind 14 copy_kernel_g<8, nt> over 32 KiB pieces   kind 15 copy_kernel_g<2, nt> over 32 KiB pieces
 // *gbps = counted bytes / average launch time (a copy counts read + write).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -54,6 +57,34 @@ __global__ __launch_bounds__(xgk::kThreads) void gridstride_copy_nt(const xgk::u
         __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), t + i);
 }
 
+__global__ __launch_bounds__(xgk::kThreads) void read_only_nt(const xgk::u32x4 *__restrict__ s, int64_t n4, unsigned *sink)
+{
+    unsigned x = 0;
+    for (int64_t i = (int64_t)blockIdx.x * xgk::kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * xgk::kThreads) {
+        const xgk::u32x4 v = __builtin_nontemporal_load(s + i);
+        x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (x == 0x9e3779b9u) atomicAdd(sink, 1u);
+}
+
+__global__ __launch_bounds__(xgk::kThreads) void write_only_nt(xgk::u32x4 *__restrict__ t, int64_t n4)
+{
+    const xgk::u32x4 v = {1u, 2u, 3u, 4u};
+    for (int64_t i = (int64_t)blockIdx.x * xgk::kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * xgk::kThreads)
+        __builtin_nontemporal_store(v, t + i);
+}
+
+template <bool NTL, bool NTS>
+__global__ __launch_bounds__(xgk::kThreads) void gridstride_copy_mix(const xgk::u32x4 *__restrict__ s,
+                                                                     xgk::u32x4 *__restrict__ t, int64_t n4)
+{
+    for (int64_t i = (int64_t)blockIdx.x * xgk::kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * xgk::kThreads) {
+        const xgk::u32x4 v = NTL ? __builtin_nontemporal_load(s + i) : s[i];
+        if (NTS) __builtin_nontemporal_store(v, t + i);
+        else t[i] = v;
+    }
+}
+
 }  // namespace
 
 #define CK(x)                                                                                             \
@@ -68,7 +99,7 @@ __global__ __launch_bounds__(xgk::kThreads) void gridstride_copy_nt(const xgk::u
 extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, double *gbps)
 {
     bytes &= ~(int64_t)32767;
-    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 9) return 3;
+    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 15) return 3;
     CK(hipSetDevice(device));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -104,6 +135,15 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
         case 6: hipLaunchKernelGGL(gridstride_copy_nt, dim3(2048), dim3(xgk::kThreads), 0, st, (const xgk::u32x4 *)a,
                                    (xgk::u32x4 *)b, n4); break;
         case 9: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
+        case 10: hipLaunchKernelGGL(read_only_nt, dim3(4096), dim3(xgk::kThreads), 0, st, (const xgk::u32x4 *)a, n4, sink);
+                 break;
+        case 11: hipLaunchKernelGGL(write_only_nt, dim3(4096), dim3(xgk::kThreads), 0, st, (xgk::u32x4 *)b, n4); break;
+        case 12: hipLaunchKernelGGL((gridstride_copy_mix<true, false>), dim3(2048), dim3(xgk::kThreads), 0, st,
+                                    (const xgk::u32x4 *)a, (xgk::u32x4 *)b, n4); break;
+        case 13: hipLaunchKernelGGL((gridstride_copy_mix<false, true>), dim3(2048), dim3(xgk::kThreads), 0, st,
+                                    (const xgk::u32x4 *)a, (xgk::u32x4 *)b, n4); break;
+        case 14: hipLaunchKernelGGL((xgk::copy_kernel_g<8, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
+        case 15: hipLaunchKernelGGL((xgk::copy_kernel_g<2, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         }
         CK(hipGetLastError());
@@ -112,7 +152,7 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    *gbps = (kind == 3 || kind == 4 ? 1.0 : 2.0) * (double)bytes * reps / (ms * 1e-3) / 1e9;
+    *gbps = (kind == 3 || kind == 4 || kind == 10 || kind == 11 ? 1.0 : 2.0) * (double)bytes * reps / (ms * 1e-3) / 1e9;
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
     CK(hipFree(a));
