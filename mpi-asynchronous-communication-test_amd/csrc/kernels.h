@@ -743,13 +743,15 @@ __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned lon
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this rail's last steps: delivered
     __syncthreads();
+    __shared__ unsigned long long t_end;                // the steps after its last barrier end here
+    __shared__ int s_end;
     if (threadIdx.x == 0) {
-        const unsigned long long t = (unsigned long long)wall_clock64();
-        for (int s = k > 0 ? lcstep[k - 1] + 1 : 0; s < nsteps; ++s) ts[s] = t;
+        t_end = (unsigned long long)wall_clock64();
+        s_end = k > 0 ? lcstep[k - 1] + 1 : 0;
         if (db) rail_finished(st, rail, R, db, epoch);      // the last rail to finish tells the host
     }
     __syncthreads();
-    for (int i = (int)threadIdx.x; i < nsteps; i += kT) stamps[(size_t)rail * stride + i] = ts[i];
+    for (int i = (int)threadIdx.x; i < nsteps; i += kT) stamps[(size_t)rail * stride + i] = i >= s_end ? t_end : ts[i];
 }
 
 // ---------------------------------------------------------------- displacement scan
