@@ -224,6 +224,9 @@ int xg_engine_hazards(const xg_span *xfer, const int *step_begin, int nsteps, in
 typedef struct { int32_t rails, npieces, nrows, nmeta; } xg_solo_shape;
 int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, int waves,
                    uint64_t src_base, uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta);
+/* Step times of a solo segment [s0, s1) from its rails' stamps (stamps[r * stride + t], 0 =
+ * the rail closed nothing there): out[t] = max over rails of the rail's latest stamp <= t. */
+void xg_solo_reduce_stamps(const uint64_t *stamps, int rails, int64_t stride, int s0, int s1, uint64_t *out);
 
 /* fill: `nsegs` consecutive d-byte segments at `off` in the SEND region,
  * segment i = fingerprint(rank, seed0 + i, iter) (prepare_*_data loops). */

@@ -102,3 +102,21 @@ int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int r
     free(cnt); free(nb); free(used); free(pend); free(pstep);
     return XG_OK;
 }
+
+/* Step times of a solo segment from its rails' stamps (kernels.h solo_engine_kernel):
+ * rail r's stamp of step t is stamps[r * stride + t], 0 where the rail closed nothing;
+ * a rail with nothing in step t is done with it when it closed its previous step, so
+ * its value for t is its latest nonzero stamp at or before t; step t is over when every
+ * rail is: out[t] = max over rails, for t in [s0, s1). */
+void xg_solo_reduce_stamps(const uint64_t *stamps, int rails, int64_t stride, int s0, int s1, uint64_t *out)
+{
+    for (int t = s0; t < s1; ++t) out[t] = 0;
+    for (int r = 0; r < rails; ++r) {
+        uint64_t carry = 0;
+        for (int t = s0; t < s1; ++t) {
+            const uint64_t x = stamps[(int64_t)r * stride + t];
+            if (x > carry) carry = x;
+            if (carry > out[t]) out[t] = carry;
+        }
+    }
+}

@@ -1233,18 +1233,10 @@ static int read_stamps(const xg_plan *p, std::vector<unsigned long long> &st)
     std::vector<unsigned long long> all(n * p->stamp_rails);
     HIPCHK(hipMemcpy(all.data(), p->d_engine + 1, 8 * all.size(), hipMemcpyDeviceToHost));
     st.assign(all.begin(), all.begin() + n);
-    for (const EngSeg &g : p->segs) {
-        if (!g.solo) continue;
-        for (int t = g.s0; t < g.s1; ++t) st[t] = 0;
-        for (int r = 0; r < g.w; ++r) {
-            unsigned long long carry = 0;
-            for (int t = g.s0; t < g.s1; ++t) {
-                const unsigned long long x = all[(size_t)r * n + t];
-                if (x) carry = std::max(carry, x);
-                st[t] = std::max(st[t], carry);
-            }
-        }
-    }
+    for (const EngSeg &g : p->segs)
+        if (g.solo)
+            xg_solo_reduce_stamps(reinterpret_cast<const uint64_t *>(all.data()), g.w, (int64_t)n, g.s0, g.s1,
+                                  reinterpret_cast<uint64_t *>(st.data()));
     return XG_OK;
 }
 

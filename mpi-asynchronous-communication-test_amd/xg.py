@@ -137,6 +137,9 @@ def host():
         h.xg_fill_runs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(SegRun)]
         h.xg_verify_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(Slot)]
         h.xg_engine_hazards.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int)]
+        h.xg_solo_reduce_stamps.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.c_int64, C.c_int, C.c_int,
+                                            C.POINTER(C.c_uint64)]
+        h.xg_solo_reduce_stamps.restype = None
         h.xg_solo_tables.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int, C.c_uint64,
                                      C.c_uint64, C.POINTER(SoloShape), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
         h.xg_summarize_results.argtypes = [C.c_int] * 6 + [C.c_char_p, C.c_char_p, Timer, Timer]
@@ -190,6 +193,15 @@ def solo_tables(steps, rails_max, src_base, dst_base, waves=16):
     csteps = [list(m[off + r * n: off + (r + 1) * n]) for r in range(R)]
     rows = list(m[off + R * n: off + R * n + R])
     return rc, shape, descs, close, csteps, rows
+
+
+def solo_reduce_stamps(stamps, s0, s1):
+    """xg_solo_reduce_stamps over stamps = [rail][step] (ints, 0 = nothing closed)"""
+    R, n = len(stamps), len(stamps[0])
+    arr = (C.c_uint64 * (R * n))(*[x for row in stamps for x in row])
+    out = (C.c_uint64 * n)()
+    host().xg_solo_reduce_stamps(arr, R, n, s0, s1, out)
+    return list(out)
 
 
 def method_label(method):

@@ -145,3 +145,29 @@ def test_rejects(xg):
     assert rc == 3
     rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 513, sb, db, waves=1)     # at most 512 rails
     assert rc == 3
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_reduce_stamps(xg, seed):
+    """step t of a solo segment is over when every rail is: each rail's latest stamp at or
+    before t (0 = the rail closed nothing there), MAX over rails; steps outside [s0, s1)
+    untouched (0)"""
+    rng = random.Random(seed)
+    R, n = rng.randint(1, 20), rng.randint(1, 50)
+    stamps = [[0] * n for _ in range(R)]
+    for r in range(R):
+        t0 = rng.randint(1000, 2000)
+        for t in range(n):
+            t0 += rng.randint(1, 50)
+            if rng.random() < 0.3:
+                stamps[r][t] = t0
+    s0 = rng.randint(0, n - 1)
+    s1 = rng.randint(s0 + 1, n)
+    got = xg.solo_reduce_stamps(stamps, s0, s1)
+    for t in range(n):
+        if not s0 <= t < s1:
+            assert got[t] == 0
+            continue
+        exp = max(max([x for x in stamps[r][s0:t + 1] if x] or [0]) for r in range(R))
+        assert got[t] == exp, (t, got[t], exp)
+    assert all(a <= b for a, b in zip(got[s0:s1], got[s0 + 1:s1]))
