@@ -15,6 +15,9 @@
 //   kind 10 read-only stream, non-temporal loads      kind 11 write-only stream, non-temporal stores
 //   kind 12 grid-stride copy, nt loads + plain stores   kind 13 grid-stride copy, plain loads + nt stores
 //   kind 14 copy_kernel_g<8, nt> over 32 KiB pieces   kind 15 copy_kernel_g<2, nt> over 32 KiB pieces
+//   kind 16 many-to-all gather, copy_kernel_g<4, nt>: 14 source blocks of 32 x 1 MiB segments at a
+//           32 MiB stride, destination segment (r, a) at (r * 14 + a) MiB, pieces in destination order
+//   kind 17 the same with the source blocks 32 MiB + 64 KiB apart (stride off a power of two)
 // *gbps = counted bytes / average launch time (a copy counts read + write).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(xgk::kThreads) void gridstride_copy_mix(const xgk::
 extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, double *gbps)
 {
     bytes &= ~(int64_t)32767;
-    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 15) return 3;
+    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 17) return 3;
     CK(hipSetDevice(device));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -111,7 +114,16 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipMemsetAsync(a, 1, bytes, st));
     const int64_t piece = kind == 7 ? 262144 : (kind == 8 ? 65536 : 32768);
     std::vector<xgk::DCopy> pieces;
-    for (int64_t o = 0; o < bytes; o += piece) pieces.push_back({a + o, b + o, std::min<int64_t>(piece, bytes - o)});
+    if (kind == 16 || kind == 17) {            // bytes ignored: 14 x 32 one-MiB segments
+        const int64_t seg = 1 << 20, stride = 32 * seg + (kind == 17 ? 65536 : 0);
+        if (14 * stride > bytes) return 3;
+        for (int r = 0; r < 32; ++r)
+            for (int g = 0; g < 14; ++g)
+                for (int64_t o = 0; o < seg; o += piece)
+                    pieces.push_back({a + g * stride + r * seg + o, b + (int64_t)(r * 14 + g) * seg + o, piece});
+    } else {
+        for (int64_t o = 0; o < bytes; o += piece) pieces.push_back({a + o, b + o, std::min<int64_t>(piece, bytes - o)});
+    }
     xgk::DCopy *dp;
     CK(hipMalloc(&dp, sizeof(xgk::DCopy) * pieces.size()));
     CK(hipMemcpy(dp, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
@@ -144,6 +156,8 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
                                     (const xgk::u32x4 *)a, (xgk::u32x4 *)b, n4); break;
         case 14: hipLaunchKernelGGL((xgk::copy_kernel_g<8, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         case 15: hipLaunchKernelGGL((xgk::copy_kernel_g<2, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
+        case 16:
+        case 17: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         }
         CK(hipGetLastError());
@@ -152,7 +166,8 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    *gbps = (kind == 3 || kind == 4 || kind == 10 || kind == 11 ? 1.0 : 2.0) * (double)bytes * reps / (ms * 1e-3) / 1e9;
+    const double moved = kind == 16 || kind == 17 ? 448.0 * (1 << 20) : (double)bytes;
+    *gbps = (kind == 3 || kind == 4 || kind == 10 || kind == 11 ? 1.0 : 2.0) * moved * reps / (ms * 1e-3) / 1e9;
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
     CK(hipFree(a));
