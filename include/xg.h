@@ -117,7 +117,7 @@ int xg_plan_check(xg_plan *p);
  * launch of up to one workgroup per CU (XG_ENGINE_WG lowers it), grid barrier +
  * wall-clock stamp per step; the other steps are their own launches.
  * Small hazard-free segments run on the solo engine instead: each step's pieces
- * dealt over up to XG_SOLO_RAILS independent rails (default 256 rails of one wave;
+ * dealt over up to XG_SOLO_RAILS independent rails (default 512 rails of one wave;
  * XG_SOLO_WAVES=16: 16-wave workgroups) that each keep their own step order and
  * never wait for one another.
  * xg_plan_engine: workgroups of the first such segment (0: none);

@@ -275,13 +275,13 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->engine_drain = env && !strcmp(env, "1");
     env = getenv("XG_ENGINE_SOLO");          // "0": never solo (the grid engine runs every segment)
     c->solo = !(env && !strcmp(env, "0"));
-    c->solo_max = 32 << 20;
+    c->solo_max = (int64_t)256 << 20;     // the descriptors' 24-bit offset window bounds it anyway
     env = getenv("XG_ENGINE_SOLO_MAX");
     if (env) c->solo_max = atol(env);
     env = getenv("XG_SOLO_WAVES");           // waves per rail: 1 (default) or 16
     c->solo_waves = env && atoi(env) == xgk::kSoloWaves ? xgk::kSoloWaves : 1;
     // see DESIGN.md (solo engine): profiles/r02/rails/solo_probe.txt
-    c->solo_rails = c->solo_waves == 1 ? 256 : 16;
+    c->solo_rails = c->solo_waves == 1 ? 512 : 16;     // 512 one-wave rails: 2 per CU by LDS
     env = getenv("XG_SOLO_RAILS");
     if (env && atoi(env) > 0) c->solo_rails = std::min(atoi(env), xgk::kSoloMaxRails);
     env = getenv("XG_PIECE_ORDER");          // profiles/r02/piece_order/: by destination is fastest
@@ -571,15 +571,16 @@ static_assert(xgk::kSoloWaves == XG_SOLO_WAVES && xgk::kSoloMaxRails == XG_SOLO_
 
 // Solo or grid engine for a hazard-free segment of n steps (`busy` of them move
 // bytes) moving `bytes`: the cheaper by a model of the measured costs (MI355X,
-// profiles/r02/rails/solo_probe.txt): a workgroup rail (one CU) moves ~120 GB/s of
-// load + store traffic and closes a step in ~0.2 us, a one-wave rail ~15 GB/s and
-// ~0.05 us; the grid engine moves at the copy kernels' ~5 TB/s but pays ~1 us of
-// device-scope barrier per step; a lone busy step outside the engine is a copy
-// launch inside the timed region (~8 us).
+// profiles/r02/rails/solo_probe*.txt): a workgroup rail (one CU) moves ~120 GB/s of
+// load + store traffic and closes a step in ~0.2 us, a one-wave rail ~15 GB/s (up to
+// the ~6 TB/s HBM copy rate) and ~0.05 us; the grid engine moves at the copy kernels'
+// ~5 TB/s but pays >= 1 us of device-scope barrier per step; a lone busy step outside
+// the engine is a copy launch inside the timed region (~8 us).
 static bool solo_pays(int64_t bytes, int n, int rails, int wv, int busy)
 {
     const double traffic = 2.0 * (double)bytes;
-    const double solo = wv == 1 ? traffic / (rails * 15e9) + n * 0.05e-6 : traffic / (rails * 120e9) + n * 0.2e-6;
+    const double solo = wv == 1 ? traffic / std::min(rails * 15e9, 6e12) + n * 0.05e-6
+                                : traffic / (rails * 120e9) + n * 0.2e-6;
     const double grid = traffic / 5e12 + n * 1.0e-6 + (busy < 2 ? 8e-6 : 0.0);
     return solo < grid;
 }

@@ -14,7 +14,11 @@ modes = {"solo_armed": {}, "solo64_armed": {"XG_SOLO_RAILS": "64"}, "solo512_arm
          "solo1_armed": {"XG_SOLO_RAILS": "1"}, "solo_norelay": {"XG_SOLO_RELAY": "0", "XG_SOLO_RAILS": "16"},
          "wg16_armed": {"XG_SOLO_WAVES": "16"}, "wg4_armed": {"XG_SOLO_WAVES": "16", "XG_SOLO_RAILS": "4"},
          "wg1_armed": {"XG_SOLO_WAVES": "16", "XG_SOLO_RAILS": "1"},
-         "grid_armed": {"XG_ENGINE_SOLO": "0"}, "solo_launch": {"XG_ENGINE_ARM": "0"}}
+         "grid_armed": {"XG_ENGINE_SOLO": "0"}, "solo_launch": {"XG_ENGINE_ARM": "0"},
+         "solo_big": {"XG_ENGINE_SOLO_MAX": "268435456", "XG_ENGINE_MAX_STEP": "268435456"},
+         "solo512_big": {"XG_ENGINE_SOLO_MAX": "268435456", "XG_ENGINE_MAX_STEP": "268435456", "XG_SOLO_RAILS": "512"},
+         "grid_big": {"XG_ENGINE_SOLO": "0", "XG_ENGINE_MAX_STEP": "268435456"},
+         "chained": {"XG_ENGINE_MAX_STEP": "0"}}
 if os.environ.get("PROBE_MODES"):
     modes = {k: v for k, v in modes.items() if k in os.environ["PROBE_MODES"].split(",")}
 for name, env in modes.items():

@@ -159,7 +159,7 @@ def test_step_engine_matches_per_step_launches(xg, ctx, method, d):
 
 
 ENGINE_MODES = {
-    "solo_armed": {},                                           # default at README sizes: 256 one-wave rails
+    "solo_armed": {},                                           # default at README sizes: 512 one-wave rails
     "solo64_armed": {"XG_SOLO_RAILS": "64"},
     "solo37_launch": {"XG_SOLO_RAILS": "37", "XG_ENGINE_ARM": "0"},
     "solo_norelay": {"XG_SOLO_RELAY": "0", "XG_SOLO_RAILS": "16"},   # every rail polls the doorbell
@@ -201,8 +201,8 @@ def test_step_engine_modes(xg, method, k):
             run = xg.MethodRun(cx, s, it=it, mode=1)
             try:
                 assert run.engine_workgroups > 0
-                rails = {"solo_armed": 256, "solo64_armed": 64, "solo37_launch": 37, "solo_norelay": 16, "wg_armed": 16,
-                         "wg1_launch": 1, "solo_launch": 256}.get(name, 0)
+                rails = {"solo_armed": 512, "solo64_armed": 64, "solo37_launch": 37, "solo_norelay": 16, "wg_armed": 16,
+                         "wg1_launch": 1, "solo_launch": 512}.get(name, 0)
                 assert run.engine_rails == rails, (name, run.engine_rails)
                 for _rep in range(3):
                     done, _post, wall = run.run_timed()
