@@ -77,3 +77,38 @@ def test_real_plans_have_no_hazards(xg, method, k):
     base = {b: (b + 1) << 40 for b in range(xg.NBUF)}
     flags, n = xg.engine_hazards(_spans(v, base))
     assert n == 0 and flags[-1] == 1 and all(f == 0 for f in flags[:-1]), (method, k, flags)
+
+
+@pytest.mark.parametrize("method", [15, 16])
+def test_tam_plans_have_hazards_where_scratch_is_read_back(xg, method):
+    """TAM stages rank data in SCRATCH and reads it back later.  With each plan step cut
+    into its stage copies, then its local copies, the scan puts a hazard barrier before
+    every step that reads SCRATCH written since the previous hazard point (checked
+    against a direct interval walk).  Those barriers are why TAM plans stay outside the
+    engine: in the grid engine they cost 59-61 us at the README size against 29 us for
+    per-step launches (profiles/r02/tam_engine/)."""
+    P, A, d, c = 32, 14, 2048, 3
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=2, proc_node=4)
+    v = s.devplan(1, 0)
+    base = {b: (b + 1) << 40 for b in range(xg.NBUF)}
+    steps = []
+    for i, (pb, pc, _q, _n, _b, _c) in enumerate(v.steps):
+        cp = [(base[sb] + so, base[db] + do, ln) for (sb, so, db, do, ln) in v.copies[pb:pb + pc]]
+        ns = v.stage_count[i]
+        if ns:
+            steps.append(cp[:ns])
+        if pc > ns or not ns:
+            steps.append(cp[ns:])
+    flags, n = xg.engine_hazards(steps)
+    assert n > 0 and flags[-1] >= 1
+    # reference walk: pending written bytes since the last flag-2 barrier
+    pend = []
+    for t, st in enumerate(steps):
+        if t and any(lo < sa + ln and sa < hi for (sa, _da, ln) in st if ln for (lo, hi) in pend):
+            assert flags[t - 1] == 2, (t, flags)
+            pend = []
+        if flags[t] == 2:
+            pend = []
+        else:
+            pend += [(da, da + ln) for (_sa, da, ln) in st if ln]
