@@ -68,7 +68,35 @@ def parse():
     ap.add_argument("--child-timeout", type=float, default=0,
                     help="parent mode: seconds before the children are stopped (0: none)")
     ap.add_argument("--cpu-reps", type=int, default=10, help="-k of the reference CPU run")
+    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 900)),
+                    help="rank process: seconds before a rank that is still running reports the phase it is "
+                         "stuck in and exits 124 (0: off) -- a lost peer leaves RCCL waiting forever")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------- watchdog (rank processes)
+PHASE = ["start"]
+
+
+def phase(name):
+    PHASE[0] = name
+
+
+def start_watchdog(seconds, rank):
+    """A rank whose peers died (or never came) waits in RCCL with no timeout of its own:
+    after `seconds` this thread names the phase the rank is in and ends the process
+    (os._exit: no exec, nothing else runs in its place)."""
+    if seconds <= 0:
+        return
+
+    def fire():
+        sys.stderr.write("bench: rank %d still in phase '%s' after %.0f s; exiting\n" % (rank, PHASE[0], seconds))
+        sys.stderr.flush()
+        os._exit(124)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
 
 
 # ---------------------------------------------------------------- CPU baseline (reference)
@@ -257,19 +285,23 @@ def main():
     if world != a.gpus:
         raise SystemExit("WORLD_SIZE=%d but --gpus %d" % (world, a.gpus))
     methods = [int(x) for x in a.methods.split(",")]
+    start_watchdog(a.watchdog, rank)
 
     # host-MPI baseline first, before this process touches the GPU (rank 0; a parent
     # process of an N-GPU job runs it itself and passes --no-cpu-baseline)
     cpu = None
     if rank == 0 and not a.no_cpu_baseline:
+        phase("cpu baseline")
         cpu = cpu_baseline(a, methods)
 
     import __graft_entry__ as G
     xg = G.load_package().xg
     uid, rdzv = (None, None)
     if world > 1:
+        phase("rendezvous (RCCL id file)")
         uid, rdzv = rendezvous_uid(xg, rank, world)
     dev = int(os.environ.get("XG_DEVICE", local))   # XG_DEVICE: test hook (several ranks on one GPU)
+    phase("RCCL communicator init (ncclCommInitRank, %d ranks)" % world)
     ctx = xg.Context(rank=rank, nranks=world, device=dev, uid=uid)
     ctx.barrier()
     if rdzv:
@@ -298,6 +330,7 @@ def main():
     tune_on = a.tune_pack == 1 or (a.tune_pack < 0 and world > 1 and a.pack_max_seg == 4 << 20)
     cands = [0, 4 << 20] if tune_on else [a.pack_max_seg]
     for m in methods:
+        phase("method %d: verify + plan choice" % m)
         s = xg.Schedule(m, a.procs, a.aggs, a.size, a.comm_size, rl, ntimes=1)
         best = None
         for pk in cands:
@@ -341,6 +374,7 @@ def main():
         for r in runs:
             r.check()
 
+    phase("warm-up")
     for _ in range(a.warmup):
         step()
     ctx.device_sync()
@@ -351,6 +385,7 @@ def main():
     # mode): with nothing but copy launches in it (N = 1) its device time over the
     # number of launches is the copy kernel's average launch duration, gaps between
     # back-to-back launches included.
+    phase("timed steps")
     launches_per_step = sum(r.launches for r in runs)
     region = world == 1 and not any(r.view.p2p for r in runs)
     ctx.barrier()
@@ -396,6 +431,7 @@ def main():
     # N > 1: cross-GPU (xGMI) bytes of the timed region vs the measured RCCL all-pairs ceiling
     xgmi = None
     if world > 1:
+        phase("xGMI ceiling (RCCL all-pairs send/recv)")
         cross_step = 0      # every rank derives every GPU's plan (deterministic, cheap)
         for r in runs:
             for g in range(world):

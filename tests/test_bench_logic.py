@@ -73,3 +73,12 @@ def test_bench_single_gpu_line(tmp_path):
     assert out["n_gpus"] == 1 and out["xgmi"] is None
     assert out["roofline"]["measured"].startswith("one HIP event pair")
     assert out["roofline"]["avg_launch_us"] * out["roofline"]["launches_per_step"] <= out["ms_per_step"] * 1e3 * 1.001
+
+
+def test_watchdog_ends_a_rank_whose_peers_never_come(tmp_path):
+    """rank 1 of a 2-GPU job whose rank 0 never writes the RCCL id: instead of waiting in
+    the rendezvous (or, on hardware, in ncclCommInitRank) forever, the watchdog names the
+    phase and exits 124"""
+    p = _run(2, 1, ["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--watchdog", "3"], tmp_path)
+    assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
+    assert "rank 1 still in phase 'rendezvous" in p.stderr
