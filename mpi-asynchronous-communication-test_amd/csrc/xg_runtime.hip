@@ -152,8 +152,8 @@ struct xg_plan {
     int ndisp;
     int nlaunch;                   // kernel launches per run (copies + engine), RCCL's aside
     bool rec_ev;                   // xg_plan_run is recording step events (fused launches record the previous step's)
-    // chains: runs of >= 2 consecutive steps that are each ONE local copy launch (outside
-    // engine segments, no RCCL, no barrier).  xg_plan_run times them without an event
+    // chains: runs of >= 2 consecutive steps that are each ONE local copy launch, or a TAM
+    // stage launch and/or a local launch (outside engine segments, no RCCL, no barrier).  xg_plan_run times them without an event
     // between launches (an event record costs ~5 us of idle device between two launches):
     // launch t+1 stamps its start = step t's completion, a clock kernel closes the chain,
     // one event after it anchors the stamps.  chain_end[s] = end of s's chain (s = its
@@ -983,11 +983,17 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     }
     p->chain_end.assign(p->nsteps, 0);
     if (c->step_chain) {
+        // a chain step: its stage copies (TAM) and/or its local copies, each one launch
+        // of a variant that can stamp its start, and nothing else
         auto one_launch = [&](int s) {
             const StepR &st = p->steps[s];
-            const int v = copy_variant(p, st.local_bytes);
-            return p->seg_of[s] < 0 && !st.split && !st.fused && !st.deferred && !st.stage_n && !st.p2p_n && !st.pack_n &&
-                   !st.post_n && !st.sync_after && st.local_n > 0 && (v == 1 || v == 6);
+            auto stamps = [&](int64_t bytes, bool reread) {
+                const int v = copy_variant(p, bytes, reread);
+                return v == 1 || v == 6;
+            };
+            return p->seg_of[s] < 0 && !st.split && !st.fused && !st.deferred && !st.p2p_n && !st.pack_n &&
+                   !st.post_n && !st.sync_after && (st.local_n > 0 || st.stage_n > 0) &&
+                   (!st.local_n || stamps(st.local_bytes, false)) && (!st.stage_n || stamps(st.stage_bytes, true));
         };
         bool any = false;
         for (int s = 0; s < p->nsteps;) {
@@ -1336,8 +1342,15 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
             for (int t = s; t < ce; ++t) {
                 const double tq = xg_now();
                 const StepR &st = p->steps[t];
-                if ((rc = launch_copy(p, st.local_b, st.local_n, st.local_bytes, c->stream,
-                                      t > s ? p->d_cstamp + t - 1 : nullptr))) {
+                // the step's first launch stamps the previous step's completion
+                unsigned long long *start = t > s ? p->d_cstamp + t - 1 : nullptr;
+                rc = XG_OK;
+                if (st.stage_n) {
+                    rc = launch_copy(p, st.stage_b, st.stage_n, st.stage_bytes, c->stream, start, true);
+                    start = nullptr;
+                }
+                if (!rc && st.local_n) rc = launch_copy(p, st.local_b, st.local_n, st.local_bytes, c->stream, start);
+                if (rc) {
                     p->rec_ev = false;
                     return rc;
                 }

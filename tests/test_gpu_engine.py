@@ -318,10 +318,12 @@ def test_engine_segments_in_multi_gpu_plans(xg, method):
             cx.close()
 
 
-@pytest.mark.parametrize("method,d", [(11, 1 << 20), (12, 1 << 20), (9, 4 << 20)])
+@pytest.mark.parametrize("method,d", [(11, 1 << 20), (12, 1 << 20), (9, 4 << 20), (15, 2048), (16, 2048),
+                                      (16, 1000), (15, 1 << 20)])
 def test_step_chains_time_like_events(xg, method, d):
-    """Runs of one-launch local steps (large steps, outside the engine) are timed by
-    in-kernel start stamps instead of an event after every launch (XG_STEP_CHAIN):
+    """Runs of one-launch local steps (large steps, outside the engine; TAM steps: a stage
+    launch and/or a local launch) are timed by in-kernel start stamps of each step's
+    first launch instead of an event after every step (XG_STEP_CHAIN):
     same delivered bytes as the evented run, step times ordered and inside the run's
     wall time, and no later than the evented run's by more than noise."""
     import xg_oracle as O
