@@ -2,7 +2,9 @@
 CPU (tests/test_bench_logic.py).  Schedules, device plans, fill/verify descriptors and
 timers are the REAL host library (libxghost.so); only what needs a GPU -- contexts,
 RCCL, kernels -- is replaced by plausible no-ops.  Never imported by the product."""
+import os
 import sys
+import time
 import types
 
 
@@ -22,9 +24,25 @@ def make(real_xg):
             assert nranks == 1 or (uid is not None and len(uid) == 128)
             self.rank, self.nranks = rank, nranks
             self._kt = None
+            self._nbar = 0
+            # like ncclCommInitRank, returns once every rank has joined (file barrier
+            # when the test gives one: XG_FAKE_BARRIER_DIR)
+            self.barrier()
 
         def barrier(self):
-            pass
+            """XG_FAKE_BARRIER_DIR set: a real barrier across the job's processes (one
+            marker file per rank and barrier); otherwise a no-op"""
+            d = os.environ.get("XG_FAKE_BARRIER_DIR")
+            if not d or self.nranks == 1:
+                return
+            i = self._nbar
+            self._nbar += 1
+            open(os.path.join(d, "b%d_r%d" % (i, self.rank)), "w").close()
+            t0 = time.time()
+            while not all(os.path.exists(os.path.join(d, "b%d_r%d" % (i, r))) for r in range(self.nranks)):
+                if time.time() - t0 > 120:
+                    raise RuntimeError("fake barrier %d: peers missing" % i)
+                time.sleep(0.01)
 
         def device_sync(self):
             pass

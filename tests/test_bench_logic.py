@@ -82,3 +82,27 @@ def test_watchdog_ends_a_rank_whose_peers_never_come(tmp_path):
     p = _run(2, 1, ["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--watchdog", "3"], tmp_path)
     assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
     assert "rank 1 still in phase 'rendezvous" in p.stderr
+
+
+def test_bench_under_torchrun_launch_form(tmp_path):
+    """The driver's N > 1 command form: torch.distributed.run starts the ranks (RANK /
+    WORLD_SIZE / MASTER_PORT / TORCHELASTIC_RUN_ID set, no XG_RDZV_KEY), so the RCCL id
+    travels through the launcher-keyed file; fake device layer, real host scheduler.
+    Rank 0 prints the one JSON line, the other rank nothing, both exit 0."""
+    import socket
+    script = tmp_path / "bench_fake.py"
+    script.write_text(DRIVER.format(repo=REPO, argv=["--gpus", "2", "--steps", "2", "--warmup", "1",
+                                                     "--no-cpu-baseline", "--watchdog", "120"]))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "XG_RDZV_KEY")}
+    env["XG_FAKE_BARRIER_DIR"] = str(tmp_path)      # barriers (and the comm init) really wait for the peer
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["xgmi"]["cross_gpu_bytes_per_step"] > 0
