@@ -100,6 +100,30 @@ def start_watchdog(seconds, rank):
 
 
 # ---------------------------------------------------------------- CPU baseline (reference)
+def host_cpus():
+    """CPUs this process may actually use: affinity mask, capped by a cgroup v2 CPU quota
+    (cpu.max), which os.cpu_count() does not see -- (cpus, how it was found)"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    how = "%d in the affinity mask" % n
+    quota = period = None
+    try:                                               # cgroup v2
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+    except (OSError, ValueError):
+        try:                                           # cgroup v1
+            quota = open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read().strip()
+            period = open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().strip()
+        except OSError:
+            pass
+    try:
+        if quota not in (None, "max", "-1") and int(period) > 0:
+            q = max(1, int(int(quota) / int(period)))
+            if q < n:
+                n, how = q, "cgroup CPU quota %s/%s of %d in the affinity mask" % (quota, period, n)
+    except ValueError:
+        pass
+    return n, how
+
+
 def cpu_baseline(a, methods):
     """The reference ./test (oracle/_ref/test, built from /root/reference by oracle/Makefile)
     under MPICH on this box's host cores, same P/A/d/methods, bounded -k."""
@@ -125,13 +149,14 @@ def cpu_baseline(a, methods):
         per[m] = float(mt[0])
         tot_time += float(mt[0])
         tot_bytes += float(a.procs) * a.aggs * a.size * a.cpu_reps
-    ncpu = os.cpu_count()
-    return {"value": round(tot_bytes / tot_time / 1e9, 4), "unit": "GB/s", "cores": a.procs,
+    ncpu, how = host_cpus()
+    return {"value": round(tot_bytes / tot_time / 1e9, 4), "unit": "GB/s", "cores": min(a.procs, ncpu),
             "kind": "reference",
             "sample": "reference ./test via MPICH 3.3.2 ch3:nemesis, mpiexec -n %d (one process per logical "
-                      "rank, %d host CPUs visible), -a %d -d %d -k %d, methods %s, aggregate = sum(P*A*d*k) / "
-                      "sum(max total time); %.1f s wall" % (a.procs, ncpu, a.aggs, a.size, a.cpu_reps,
-                                                            ",".join(map(str, methods)), time.time() - t0),
+                      "rank) on %d usable host CPUs (%s)%s, -a %d -d %d -k %d, methods %s, aggregate = "
+                      "sum(P*A*d*k) / sum(max total time); %.1f s wall"
+                      % (a.procs, ncpu, how, ", oversubscribed: MPICH busy-polls" if a.procs > ncpu else "",
+                         a.aggs, a.size, a.cpu_reps, ",".join(map(str, methods)), time.time() - t0),
             "max_total_time_s": per}
 
 
