@@ -1,0 +1,111 @@
+"""GPU: seeded random configurations beyond the golden set, every method, against the
+oracle's closed form (oracle/xg_oracle.py expected_recv + chk64) with the collision-free
+fingerprint.
+
+The golden configurations pin the schedules to the real reference; this sweep widens
+the shapes the device path sees -- odd and prime P, A up to P, every placement type,
+-c from 1 to past P, 1..3 repetitions, segment sizes from 1 byte to 1 MiB at every
+alignment, barrier types, proc_node -- on one GPU (every engine form the plan picks:
+solo rails, grid engine, chains, single launches) and as virtual 2/3/4/8-GPU jobs
+(packed and direct cross-GPU segments).  Schedules the step compiler proves deadlocked
+under the reference's MPI (XG_ESCHED) are skipped, as the reference would hang there.
+"""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _configs(seed, n):
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        P = rng.choice([1, 2, 3, 5, 7, 8, 11, 13, 16, 17, 24, 31, 32, 37])
+        A = rng.randint(1, P)
+        d = rng.choice([1, 3, 16, 24, 100, 1000, 2048, 4096, 4100, 12288, 65536, 98304, 1 << 20])
+        c = rng.choice([1, 2, 3, 4, 7, 16, 200000000])
+        k = rng.randint(1, 3)
+        t = rng.randint(0, 3)
+        pn = rng.choice([1, 2, 3, 4])
+        b = rng.randint(0, 2)
+        m = rng.randint(1, 20)
+        it = rng.randint(0, 2)
+        out.append((m, P, A, d, c, k, t, pn, b, it))
+    return out
+
+
+def _schedule(xg, cfg):
+    m, P, A, d, c, k, t, pn, b, it = cfg
+    rl = xg.aggregator_list(P, A, pn, t)
+    try:
+        return xg.Schedule(m, P, A, d, c, rl, ntimes=k, proc_node=pn, barrier_type=b, iteration=it), rl
+    except xg.XGError as e:          # a schedule the reference's MPI would deadlock on
+        pytest.skip("refused schedule: %s" % e)
+
+
+def _check(xg, s, rl, cfg, results, G):
+    import xg_oracle as O
+    m, P, A, d, c, k, t, pn, b, it = cfg
+    exp = O.expected_recv(m, P, A, d, rl, it, mode=1)
+    n = 0
+    for (src, seed, dst, off), ck, nb, fb in results:
+        assert nb == 0, "cfg %s G%d: %d->%d %d bad bytes from %d" % (cfg, G, src, dst, nb, fb)
+        local = off - s.recv_offset(G, dst)
+        assert ck == O.chk64(exp[dst][local: local + d]), (cfg, G, src, dst)
+        n += 1
+    assert n == P * A, (cfg, G, n)
+
+
+@pytest.fixture(scope="module")
+def ctx(xg):
+    c = xg.Context(rank=0, nranks=1, device=0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("cfg", _configs(2026, 120), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
+def test_random_config_one_gpu(xg, ctx, cfg):
+    s, rl = _schedule(xg, cfg)
+    run = xg.MethodRun(ctx, s, it=cfg[-1], mode=1)
+    try:
+        for _rep in range(2):
+            done, _post, wall = run.run_timed()
+            assert all(0 <= x <= y for x, y in zip(done, done[1:])) and (not done or done[-1] <= wall + 1e-4)
+        chk, bad, first = run.verify()
+        _check(xg, s, rl, cfg, list(zip(run.slots, chk, bad, first)), 1)
+    finally:
+        run.close()
+
+
+@pytest.fixture(scope="module")
+def worlds(xg):
+    w = {G: [xg.Context.virtual(g, G, device=0) for g in range(G)] for G in (2, 3, 4, 8)}
+    yield w
+    for ctxs in w.values():
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("cfg", _configs(7, 60), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
+def test_random_config_virtual_gpus(xg, worlds, cfg):
+    rng = random.Random(hash(cfg) & 0xffff)
+    G = rng.choice([2, 3, 4, 8])
+    if G > cfg[1]:
+        G = 2 if cfg[1] >= 2 else 1
+    if G == 1:
+        pytest.skip("one rank: no cross-GPU job")
+    s, rl = _schedule(xg, cfg)
+    for pack in (0, 1 << 30):
+        runs = [xg.MethodRun(c, s, it=cfg[-1], mode=1, pack_max_seg=pack) for c in worlds[G]]
+        try:
+            done = xg.run_virtual(runs, rccl=rng.random() < 0.5)
+            assert all(y >= x for x, y in zip(done, done[1:]))
+            res = []
+            for r in runs:
+                chk, bad, first = r.verify()
+                res += list(zip(r.slots, chk, bad, first))
+            _check(xg, s, rl, cfg, res, G)
+        finally:
+            for r in runs:
+                r.close()
