@@ -66,3 +66,31 @@ def test_region_sizes(xg):
             tot_send = sum(s.region_bytes(G, g, 0) for g in range(G))
             tot_recv = sum(s.region_bytes(G, g, 1) for g in range(G))
             assert tot_send == tot_recv == P * A * d
+
+
+def _random_cases(seed, n):
+    import random
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        P = rng.choice([2, 3, 5, 7, 9, 12, 16, 19, 24])
+        out.append((rng.randint(1, 20), P, rng.randint(1, P), rng.choice([1, 5, 16, 24, 40]),
+                    rng.choice([1, 2, 3, 5, 200000000]), rng.randint(1, 3), rng.randint(0, 3),
+                    rng.choice([1, 2, 3, 4]), rng.randint(0, 2), rng.choice([2, 3, 4, 8])))
+    return out
+
+
+@pytest.mark.parametrize("case", _random_cases(11, 200), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d_G%d" % c)
+def test_random_plans_deliver_every_byte(xg, case):
+    """Seeded random shapes (every method, placement type, barrier type, -c, -k, proc_node)
+    as G-GPU jobs, packed and direct, through the race-checked executor."""
+    m, P, A, d, c, k, t, pn, b, G = case
+    G = min(G, P)
+    rl = xg.aggregator_list(P, A, pn, t)
+    try:
+        s = xg.Schedule(m, P, A, d, c, rl, ntimes=k, proc_node=pn, barrier_type=b, iteration=2)
+    except xg.XGError as e:
+        pytest.skip("refused schedule: %s" % e)
+    for pack in (0, 1 << 20):
+        _views, regs = simulate(s, G, it=2, mode=1, pack=pack)
+        check_recv(s, G, regs, it=2, mode=1)
