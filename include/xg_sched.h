@@ -224,6 +224,14 @@ int xg_engine_hazards(const xg_span *xfer, const int *step_begin, int nsteps, in
 typedef struct { int32_t rails, npieces, nrows, nmeta; } xg_solo_shape;
 int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, int waves,
                    uint64_t src_base, uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta);
+/* The same with offsets and lengths in units of `granule` bytes (16, 4 or 1; 4 and 1 only
+ * for one-wave rails): every transfer granule-aligned, offsets within XG_SOLO_OFF_MAX
+ * granules of the bases; bits 0-23 source, 24-47 destination offset, then the length
+ * (7, 9 or 11 bits: up to XG_SOLO_PIECE bytes), then `before` at XG_SOLO_BEFORE_SHIFT.
+ * Segment sizes that are not multiples of 16 (any -d) run on 4-B or 1-B accesses. */
+#define XG_SOLO_BEFORE_SHIFT(g) ((g) == 16 ? 55 : (g) == 4 ? 57 : 59)
+int xg_solo_tables_g(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, int waves, int granule,
+                     uint64_t src_base, uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta);
 /* Step times of a solo segment [s0, s1) from its rails' stamps (stamps[r * stride + t], 0 =
  * the rail closed nothing there): out[t] = max over rails of the rail's latest stamp <= t. */
 void xg_solo_reduce_stamps(const uint64_t *stamps, int rails, int64_t stride, int s0, int s1, uint64_t *out);

@@ -16,6 +16,11 @@
  * spare chunk (the kernel's double-buffered loop loads one chunk past the
  * last without a branch); the kernel stops after the rows that hold real
  * pieces (meta's last R entries), so the padding costs a table slot, not time.
+ *
+ * Granule G (16, 4 or 1 bytes): the unit of the offsets and lengths, i.e. the
+ * alignment every transfer must have -- 16 for the 16-B loads/stores of aligned
+ * segments, 4 and 1 for segment sizes that are not multiples of 16 (any -d); the
+ * kernel then moves a piece with 4-B or 1-B accesses (xg_solo_tables_g).
  */
 #include <stdlib.h>
 #include <string.h>
@@ -23,22 +28,31 @@
 #include "xg.h"
 #include "xg_sched.h"
 
-static uint64_t desc(uint64_t src16, uint64_t dst16, uint64_t len16) { return src16 | (dst16 << 24) | (len16 << 48); }
+static uint64_t desc(uint64_t src, uint64_t dst, uint64_t len) { return src | (dst << 24) | (len << 48); }
 
 int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, int waves,
                    uint64_t src_base, uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta)
 {
+    return xg_solo_tables_g(xfer, step_begin, nsteps, rails_max, waves, 16, src_base, dst_base, shape, descs, meta);
+}
+
+int xg_solo_tables_g(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, int waves, int granule,
+                     uint64_t src_base, uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta)
+{
     if (!xfer || !step_begin || !shape || nsteps < 1 || nsteps > XG_SOLO_MAX_STEPS || rails_max < 1 ||
-        rails_max > XG_SOLO_MAX_RAILS || (waves != 1 && waves != XG_SOLO_WAVES))
+        rails_max > XG_SOLO_MAX_RAILS || (waves != 1 && waves != XG_SOLO_WAVES) ||
+        (granule != 16 && granule != 4 && granule != 1) || (granule != 16 && waves != 1))
         return XG_EARG;
     const int nx = step_begin[nsteps];
     const int W = waves;       /* pieces per row: one per wave of a rail */
+    const uint64_t G = (uint64_t)granule;
+    const int bshift = XG_SOLO_BEFORE_SHIFT(granule);
     int64_t total = 0;
     for (int i = 0; i < nx; ++i) {
         const xg_span *x = &xfer[i];
-        if ((x->src | x->dst | x->len) & 15) return XG_EARG;
-        if (x->len && (x->src < src_base || x->dst < dst_base || (x->src + x->len - src_base) / 16 > XG_SOLO_OFF_MAX ||
-                       (x->dst + x->len - dst_base) / 16 > XG_SOLO_OFF_MAX))
+        if ((x->src | x->dst | x->len) & (G - 1)) return XG_EARG;
+        if (x->len && (x->src < src_base || x->dst < dst_base || (x->src + x->len - src_base) / G > XG_SOLO_OFF_MAX ||
+                       (x->dst + x->len - dst_base) / G > XG_SOLO_OFF_MAX))
             return XG_EARG;
         total += (int64_t)((x->len + XG_SOLO_PIECE - 1) / XG_SOLO_PIECE);
     }
@@ -83,11 +97,11 @@ int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int r
                     close[(size_t)cur * (nrows + 1) + row]++;
                     cstep[(size_t)cur * nsteps + nb[cur]++] = pstep[cur];
                     for (int64_t w = at % W; w < W; ++w)
-                        descs[(size_t)cur * np + row * W + w] += 1ull << 55;
+                        descs[(size_t)cur * np + row * W + w] += 1ull << bshift;
                     pend[cur] = -1;
                 }
                 descs[(size_t)cur * np + cnt[cur]++] +=     /* its `before` bits may be set already */
-                    desc((xfer[i].src + o - src_base) / 16, (xfer[i].dst + o - dst_base) / 16, len / 16);
+                    desc((xfer[i].src + o - src_base) / G, (xfer[i].dst + o - dst_base) / G, len / G);
                 used[cur] = 1;
                 cur = (cur + 1) % rails;
             }

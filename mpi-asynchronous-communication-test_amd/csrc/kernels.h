@@ -581,17 +581,26 @@ constexpr int kSoloMaxPieces = 4608;             // descriptors per rail kept in
 
 // One solo piece in 64 bits: source and destination offsets (16-B units, 24 bits)
 // from the segment's two base pointers, the length (16-B units, <= 64, 7 bits) and
-// `before` (5 bits): how many of its row's step barriers come before this piece.
-// Steps are packed back to back, so a row may hold the end of one step and the
-// start of the next: every wave executes all of the row's barriers, its store
-// after the first `before` of them.
-__host__ __device__ constexpr unsigned long long solo_desc(uint64_t src16, uint64_t dst16, uint64_t len16,
-                                                           uint64_t before)
-{
-    return src16 | (dst16 << 24) | (len16 << 48) | (before << 55);
-}
+// `before` (5 bits, from bit 55): how many of its row's step barriers come before this
+// piece.  Steps are packed back to back, so a row may hold the end of one step and the
+// start of the next: every wave executes all of the row's barriers, its store after
+// the first `before` of them.  (Other granules: SoloFmt below.)
 constexpr uint64_t kSoloOffMax = 1ull << 24;     // offsets < 256 MiB from the bases
 constexpr int kSoloMaxRails = 512;
+
+// Granule G of a segment's descriptors (xg_solo_tables_g): offsets and lengths in units of
+// G bytes.  G = 16: one 16-B access per lane per piece (the form above); G = 4 / 1, for
+// segment sizes that are not multiples of 16: 4 dword / 16 byte accesses per lane, access
+// j of lane l at G * (l + 64 j) -- each instruction covers 64 consecutive granules of the
+// piece -- and the range check drops the granules past its end exactly.  The length field
+// widens (7 / 9 / 11 bits for up to 1 KiB), so `before` moves up (55 / 57 / 59).
+template <int G>
+struct SoloFmt {
+    static constexpr int kShift = G == 16 ? 4 : G == 4 ? 2 : 0;       // log2 G
+    static constexpr int kLenBits = G == 16 ? 7 : G == 4 ? 9 : 11;
+    static constexpr int kBefore = 48 + kLenBits;
+    static constexpr int kNV = G == 1 ? 16 : 4;                       // registers per lane per piece
+};
 
 // Host contract (build_segments), per rail r of R = gridDim.x: pieces
 // desc[r * npieces ..], every piece 16-B aligned, <= 1 KiB, within 256 MiB of the
@@ -605,17 +614,25 @@ constexpr int kSoloMaxRails = 512;
 // drops the lanes past its end (an empty padding piece moves nothing), so the body
 // has no branch but the step barriers.  stamps[r * stride + t]: rail r's stamp of
 // step t, 0 where it closed nothing (the host carries and reduces).
-template <int K>
+template <int K, int G = 16>
 struct SoloChunk {
     unsigned long long d[K];
-    u32x4 v[K];
+    uint32_t v[K][SoloFmt<G>::kNV];
 };
 
-// issue the K 16-B loads of chunk c of this wave (rows of WV pieces)
-template <int K, int WV>
-__device__ __forceinline__ void solo_load(SoloChunk<K> &b, const unsigned long long *ldesc, int c, int wave,
+// the wave-uniform descriptor of a piece (SGPRs)
+__device__ __forceinline__ unsigned long long solo_uniform(unsigned long long d)
+{
+    return ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(d >> 32)) << 32) |
+           (unsigned)__builtin_amdgcn_readfirstlane((int)d);
+}
+
+// issue the loads of chunk c of this wave (rows of WV pieces)
+template <int K, int WV, int G>
+__device__ __forceinline__ void solo_load(SoloChunk<K, G> &b, const unsigned long long *ldesc, int c, int wave,
                                           uint64_t l16, const uint8_t *src_base)
 {
+    using F = SoloFmt<G>;
 #pragma unroll
     for (int k = 0; k < K; ++k) b.d[k] = ldesc[(c * K + k) * WV + wave];
 #pragma unroll
@@ -623,10 +640,19 @@ __device__ __forceinline__ void solo_load(SoloChunk<K> &b, const unsigned long l
         // the descriptor is wave-uniform: a buffer resource in SGPRs whose range check
         // (num_records = the piece's bytes) drops the lanes past its end -- an empty
         // padding piece moves nothing
-        const unsigned long long d = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(b.d[k] >> 32)) << 32) |
-                                     (unsigned)__builtin_amdgcn_readfirstlane((int)b.d[k]);
-        const brsrc r = make_rsrc(src_base + ((d & (kSoloOffMax - 1)) << 4), (int64_t)((d >> 48) & 127) << 4);
-        b.v[k] = bload16(r, (int)l16 * 16);
+        const unsigned long long d = solo_uniform(b.d[k]);
+        const brsrc r = make_rsrc(src_base + ((d & (kSoloOffMax - 1)) << F::kShift),
+                                  (int64_t)((d >> 48) & ((1u << F::kLenBits) - 1)) << F::kShift);
+        if constexpr (G == 16) {
+            const u32x4 x = bload16(r, (int)l16 * 16);
+            b.v[k][0] = x.x; b.v[k][1] = x.y; b.v[k][2] = x.z; b.v[k][3] = x.w;
+        } else if constexpr (G == 4) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b.v[k][j] = __builtin_amdgcn_raw_buffer_load_b32(r, 4 * ((int)l16 + 64 * j), 0, 0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) b.v[k][j] = __builtin_amdgcn_raw_buffer_load_b8(r, (int)l16 + 64 * j, 0, 0);
+        }
     }
 }
 
@@ -640,29 +666,41 @@ __device__ __forceinline__ void solo_close(unsigned long long *ts, const short *
 
 // store chunk c in row order; a row that begins new steps first closes the ones before
 // it: barrier (every wave issued their stores), stamp
-template <int K>
-__device__ __forceinline__ void solo_store(const SoloChunk<K> &b, const unsigned short *lclose, const short *lcstep,
+template <int K, int G>
+__device__ __forceinline__ void solo_store(const SoloChunk<K, G> &b, const unsigned short *lclose, const short *lcstep,
                                           unsigned long long *ts, int &s, int c, int rows, uint64_t l16,
                                           uint8_t *dst_base)
 {
+    using F = SoloFmt<G>;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         if (c * K + k >= rows) break;         // padding rows: no piece, no barrier
         const int n = __builtin_amdgcn_readfirstlane((int)lclose[c * K + k]);     // barriers in this row
-        const int bf = __builtin_amdgcn_readfirstlane((int)(b.d[k] >> 55));      // ... before my piece
+        const int bf = __builtin_amdgcn_readfirstlane((int)(b.d[k] >> F::kBefore));  // ... before my piece
         int j = 0;
         for (; j < bf; ++j) solo_close(ts, lcstep, s);
         asm volatile("" ::: "memory");        // the store stays between its steps' barriers
-        const unsigned long long d = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(b.d[k] >> 32)) << 32) |
-                                     (unsigned)__builtin_amdgcn_readfirstlane((int)b.d[k]);
-        const brsrc r = make_rsrc(dst_base + (((d >> 24) & (kSoloOffMax - 1)) << 4), (int64_t)((d >> 48) & 127) << 4);
-        bstore16(r, (int)l16 * 16, b.v[k]);
+        const unsigned long long d = solo_uniform(b.d[k]);
+        const brsrc r = make_rsrc(dst_base + (((d >> 24) & (kSoloOffMax - 1)) << F::kShift),
+                                  (int64_t)((d >> 48) & ((1u << F::kLenBits) - 1)) << F::kShift);
+        if constexpr (G == 16) {
+            u32x4 x;
+            x.x = b.v[k][0]; x.y = b.v[k][1]; x.z = b.v[k][2]; x.w = b.v[k][3];
+            bstore16(r, (int)l16 * 16, x);
+        } else if constexpr (G == 4) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) __builtin_amdgcn_raw_buffer_store_b32(b.v[k][q], r, 4 * ((int)l16 + 64 * q), 0, 0);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)b.v[k][q], r, (int)l16 + 64 * q, 0, 0);
+        }
         asm volatile("" ::: "memory");
         for (; j < n; ++j) solo_close(ts, lcstep, s);
     }
 }
 
-template <int K, int WV>
+template <int K, int WV, int G = 16>
 __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned long long *__restrict__ desc,
                                                                    int npieces, const uint8_t *src_base,
                                                                    uint8_t *dst_base, const int *__restrict__ meta,
@@ -731,15 +769,15 @@ __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned lon
     // table to an even number of chunks plus one spare empty chunk, so the loads below
     // need no bounds branch (a conditional one would make the compiler wait on it);
     // the loop leaves after the last chunk that holds real pieces.
-    SoloChunk<K> A, B;
+    SoloChunk<K, G> A, B;
     int k = 0;
-    solo_load<K, WV>(A, ldesc, 0, wave, l16, src_base);
+    solo_load<K, WV, G>(A, ldesc, 0, wave, l16, src_base);
     for (int c = 0; c < nreal; c += 2) {
-        solo_load<K, WV>(B, ldesc, c + 1, wave, l16, src_base);
-        solo_store<K>(A, lclose, lcstep, ts, k, c, rows, l16, dst_base);
+        solo_load<K, WV, G>(B, ldesc, c + 1, wave, l16, src_base);
+        solo_store<K, G>(A, lclose, lcstep, ts, k, c, rows, l16, dst_base);
         if (c + 1 >= nreal) break;
-        solo_load<K, WV>(A, ldesc, c + 2, wave, l16, src_base);
-        solo_store<K>(B, lclose, lcstep, ts, k, c + 1, rows, l16, dst_base);
+        solo_load<K, WV, G>(A, ldesc, c + 2, wave, l16, src_base);
+        solo_store<K, G>(B, lclose, lcstep, ts, k, c + 1, rows, l16, dst_base);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this rail's last steps: delivered
     __syncthreads();

@@ -112,6 +112,7 @@ struct EngSeg {
     int nhaz;                      // hazard points (xg_engine_hazards flag 2)
     bool solo;                     // solo engine (solo_engine_kernel), pieces from u0
     int wv;                        // solo: waves per rail (16 or 1)
+    int gran;                      // solo: descriptor granule in bytes (16, or 4 / 1 for segments not 16-B aligned)
     int u0;                        // first unit / piece of the segment in d_epieces
     int npieces;                   // solo: pieces per rail (whole chunks of rows), rail r's from u0 + r * npieces
                                    // in d_solo; w = rails
@@ -576,10 +577,12 @@ static_assert(xgk::kSoloWaves == XG_SOLO_WAVES && xgk::kSoloMaxRails == XG_SOLO_
 // the ~6 TB/s HBM copy rate) and ~0.05 us; the grid engine moves at the copy kernels'
 // ~5 TB/s but pays >= 1 us of device-scope barrier per step; a lone busy step outside
 // the engine is a copy launch inside the timed region (~8 us).
-static bool solo_pays(int64_t bytes, int n, int rails, int wv, int busy)
+static bool solo_pays(int64_t bytes, int n, int rails, int wv, int busy, int gran = 16)
 {
     const double traffic = 2.0 * (double)bytes;
-    const double solo = wv == 1 ? traffic / std::min(rails * 15e9, 6e12) + n * 0.05e-6
+    // one-wave rails on 4-B / 1-B accesses move a quarter / a sixteenth of the 16-B rate
+    const double rail = 15e9 * gran / 16.0;
+    const double solo = wv == 1 ? traffic / std::min(rails * rail, 6e12 * gran / 16.0) + n * 0.05e-6
                                 : traffic / (rails * 120e9) + n * 0.2e-6;
     const double grid = traffic / 5e12 + n * 1.0e-6 + (busy < 2 ? 8e-6 : 0.0);
     return solo < grid;
@@ -651,10 +654,12 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         g.nhaz = xg_engine_hazards(spans.data(), tb.data(), n, c->engine_drain, fl.data());
         g.w = std::max(1, std::min(maxu, c->engine_wmax));
         g.sb_off = (int)sb.size();
-        bool aligned = true;
+        // solo granule: the largest of 16 / 4 / 1 every transfer is aligned to (segment sizes
+        // that are not multiples of 16 move on 4-B or 1-B accesses, one-wave rails only)
+        uint64_t bits = 0;
         for (const auto &xs : xfer)
-            for (const xgk::DCopy &x : xs)
-                aligned = aligned && ((((uintptr_t)x.src | (uintptr_t)x.dst | (uint64_t)x.len) & 15) == 0);
+            for (const xgk::DCopy &x : xs) bits |= (uintptr_t)x.src | (uintptr_t)x.dst | (uint64_t)x.len;
+        const int gran = (bits & 15) == 0 ? 16 : (bits & 3) == 0 ? 4 : 1;
         // solo: each step's 1 KiB pieces dealt round-robin over up to solo_rails rails, per
         // rail rows of kSoloWaves pieces (xg_solo_tables, host/solo.c)
         uintptr_t slo = UINTPTR_MAX, shi = 0, dlo = UINTPTR_MAX, dhi = 0;
@@ -664,12 +669,13 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
                 dlo = std::min<uintptr_t>(dlo, x.dst); dhi = std::max<uintptr_t>(dhi, x.dst + x.len);
             }
         xg_solo_shape sh{};
-        const bool fits = aligned && shi > slo && dhi > dlo && n <= xgk::kSoloMaxSteps &&
-                          xg_solo_tables(spans.data(), tb.data(), n, c->solo_rails, c->solo_waves, slo, dlo, &sh, nullptr,
-                                         nullptr) == XG_OK;
+        const bool fits = (gran == 16 || c->solo_waves == 1) && shi > slo && dhi > dlo && n <= xgk::kSoloMaxSteps &&
+                          xg_solo_tables_g(spans.data(), tb.data(), n, c->solo_rails, c->solo_waves, gran, slo, dlo, &sh,
+                                           nullptr, nullptr) == XG_OK;
         g.solo = g.nhaz == 0 && fits && c->solo && g.bytes <= c->solo_max &&
-                 solo_pays(g.bytes, n, sh.rails, c->solo_waves, busy);
+                 solo_pays(g.bytes, n, sh.rails, c->solo_waves, busy, gran);
         g.wv = c->solo_waves;
+        g.gran = gran;
         if (!g.solo && busy < 2) {      // one busy step: an engine launch only if it runs solo
             ep.resize(u0);
             s = run_end;
@@ -684,7 +690,7 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
             g.npieces = sh.npieces;
             std::vector<int> meta(sh.nmeta);
             p->solo_desc.resize(g.u0 + (size_t)sh.rails * sh.npieces);
-            if (xg_solo_tables(spans.data(), tb.data(), n, c->solo_rails, c->solo_waves, slo, dlo, &sh,
+            if (xg_solo_tables_g(spans.data(), tb.data(), n, c->solo_rails, c->solo_waves, gran, slo, dlo, &sh,
                                reinterpret_cast<uint64_t *>(p->solo_desc.data()) + g.u0, meta.data()) != XG_OK)
                 return XG_EARG;
             sb.insert(sb.end(), meta.begin(), meta.end());
@@ -1209,8 +1215,16 @@ static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream, bool arme
     if ((rc = kt_before(c, stream, &kt))) return rc;
     unsigned long long *stamps = reinterpret_cast<unsigned long long *>(p->d_engine + 1) + g.s0;
     const int *sb = p->d_sb + g.sb_off;
-    if (g.solo && g.wv == 1)
+    if (g.solo && g.wv == 1 && g.gran == 16)
         hipLaunchKernelGGL((xgk::solo_engine_kernel<xgk::kSoloK, 1>), dim3(g.w), dim3(64), 0, stream,
+                           p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
+                           db, epoch, c->solo_relay);
+    else if (g.solo && g.wv == 1 && g.gran == 4)
+        hipLaunchKernelGGL((xgk::solo_engine_kernel<xgk::kSoloK, 1, 4>), dim3(g.w), dim3(64), 0, stream,
+                           p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
+                           db, epoch, c->solo_relay);
+    else if (g.solo && g.wv == 1)      // granule 1: 16 registers per piece and lane, half the rows per chunk
+        hipLaunchKernelGGL((xgk::solo_engine_kernel<xgk::kSoloK / 2, 1, 1>), dim3(g.w), dim3(64), 0, stream,
                            p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
                            db, epoch, c->solo_relay);
     else if (g.solo)

@@ -142,6 +142,9 @@ def host():
         h.xg_solo_reduce_stamps.restype = None
         h.xg_solo_tables.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int, C.c_uint64,
                                      C.c_uint64, C.POINTER(SoloShape), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
+        h.xg_solo_tables_g.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.c_uint64, C.c_uint64, C.POINTER(SoloShape), C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_int)]
         h.xg_summarize_results.argtypes = [C.c_int] * 6 + [C.c_char_p, C.c_char_p, Timer, Timer]
         _host = h
     return _host
@@ -168,8 +171,8 @@ def engine_hazards(steps, force=False):
     return list(fl)[:len(steps)], n
 
 
-def solo_tables(steps, rails_max, src_base, dst_base, waves=16):
-    """xg_solo_tables over steps = [[(src, dst, len), ...], ...]: returns (rc, shape dict,
+def solo_tables(steps, rails_max, src_base, dst_base, waves=16, granule=16):
+    """xg_solo_tables_g over steps = [[(src, dst, len), ...], ...]: returns (rc, shape dict,
     per-rail descriptor lists, per-rail row barrier counts, per-rail closed-step lists,
     per-rail rows holding real pieces)."""
     spans = [x for st in steps for x in st]
@@ -179,14 +182,15 @@ def solo_tables(steps, rails_max, src_base, dst_base, waves=16):
         beg.append(beg[-1] + len(st))
     sb = (C.c_int * len(beg))(*beg)
     sh = SoloShape()
-    rc = host().xg_solo_tables(arr, sb, len(steps), rails_max, waves, src_base, dst_base, C.byref(sh), None, None)
+    rc = host().xg_solo_tables_g(arr, sb, len(steps), rails_max, waves, granule, src_base, dst_base, C.byref(sh),
+                                 None, None)
     shape = {"rails": sh.rails, "npieces": sh.npieces, "nrows": sh.nrows, "nmeta": sh.nmeta}
     if rc:
         return rc, shape, None, None, None, None
     R, npc, nr, n = sh.rails, sh.npieces, sh.nrows, len(steps)
     d = (C.c_uint64 * (R * npc))()
     m = (C.c_int * sh.nmeta)()
-    rc = host().xg_solo_tables(arr, sb, n, rails_max, waves, src_base, dst_base, C.byref(sh), d, m)
+    rc = host().xg_solo_tables_g(arr, sb, n, rails_max, waves, granule, src_base, dst_base, C.byref(sh), d, m)
     descs = [list(d[r * npc:(r + 1) * npc]) for r in range(R)]
     close = [list(m[r * (nr + 1):(r + 1) * (nr + 1)]) for r in range(R)]
     off = R * (nr + 1)

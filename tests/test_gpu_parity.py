@@ -219,3 +219,46 @@ def test_step_engine_modes(xg, method, k):
         finally:
             cx.close()
     assert all(v == res["solo_armed"] for v in res.values())
+
+
+@pytest.mark.parametrize("k", [1, 3])
+@pytest.mark.parametrize("d", [1000, 100, 24, 33, 1])
+@pytest.mark.parametrize("method", [6, 9, 12, 18, 1, 4])
+def test_solo_engine_fine_granules(xg, method, d, k):
+    """Segment sizes that are not multiples of 16 run on the solo engine's 4-B (d = 1000,
+    100, 24) or 1-B (d = 33, 1) granules: armed one-wave rails, the same bytes as one
+    launch per step, every slot against the oracle with the strong fingerprint."""
+    import os
+    import xg_oracle as O
+    P, A, c, it = 32, 14, 3, 1
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, iteration=it)
+    exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
+    res = {}
+    for name, env in (("solo", {}), ("eager", {"XG_ENGINE_MAX_STEP": "0"})):
+        os.environ.update(env)
+        try:
+            cx = xg.Context(rank=0, nranks=1, device=0)
+        finally:
+            for key in env:
+                del os.environ[key]
+        try:
+            run = xg.MethodRun(cx, s, it=it, mode=1)
+            try:
+                if name == "solo" and run.nsteps >= 2:
+                    assert run.engine_rails > 0, (method, d, k, run.nsteps)
+                for _rep in range(3):
+                    done, _post, wall = run.run_timed()
+                    assert all(0 <= a <= b for a, b in zip(done, done[1:])), (name, done)
+                    assert done[-1] <= wall + 1e-4
+                chk, bad, _f = run.verify()
+                assert all(b == 0 for b in bad), (name, method, d)
+                for (src, seed, dst, off), ck in zip(run.slots, chk):
+                    local = off - s.recv_offset(1, dst)
+                    assert ck == O.chk64(exp[dst][local: local + d]), (name, method, d, src, dst)
+                res[name] = chk
+            finally:
+                run.close()
+        finally:
+            cx.close()
+    assert res["solo"] == res["eager"]

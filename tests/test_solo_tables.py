@@ -11,15 +11,18 @@ import pytest
 
 
 PIECE, K, MAXP = 1024, 8, 4608
+LEN_BITS = {16: 7, 4: 9, 1: 11}      # kernels.h SoloFmt
 
 
-def decode(d):
-    return d & 0xFFFFFF, (d >> 24) & 0xFFFFFF, (d >> 48) & 127, d >> 55
+def decode(d, G=16):
+    L = LEN_BITS[G]
+    return d & 0xFFFFFF, (d >> 24) & 0xFFFFFF, (d >> 48) & ((1 << L) - 1), d >> (48 + L)
 
 
-def interpret(steps, rails_max, sbase, dbase, xg, WAVES=16):
-    """WAVES: pieces per row = waves per rail (16: a workgroup; 1: a single wave)"""
-    rc, shape, descs, close, csteps, rows = xg.solo_tables(steps, rails_max, sbase, dbase, waves=WAVES)
+def interpret(steps, rails_max, sbase, dbase, xg, WAVES=16, G=16):
+    """WAVES: pieces per row = waves per rail (16: a workgroup; 1: a single wave);
+    G: the descriptors' granule (offsets and lengths in G-byte units)"""
+    rc, shape, descs, close, csteps, rows = xg.solo_tables(steps, rails_max, sbase, dbase, waves=WAVES, granule=G)
     assert rc == 0, (rc, shape)
     R, npc, nr = shape["rails"], shape["npieces"], shape["nrows"]
     n = len(steps)
@@ -48,7 +51,7 @@ def interpret(steps, rails_max, sbase, dbase, xg, WAVES=16):
             assert nrow <= WAVES
             prev_bf = 0
             for w in range(WAVES):
-                so, do, l16, bf = decode(descs[r][row * WAVES + w])
+                so, do, l16, bf = decode(descs[r][row * WAVES + w], G)
                 assert bf <= nrow and bf >= prev_bf
                 prev_bf = bf
                 if l16 == 0:
@@ -57,16 +60,20 @@ def interpret(steps, rails_max, sbase, dbase, xg, WAVES=16):
                 assert row < nr - K, "a piece in the spare chunk is never stored"
                 assert row < rows[r], "the kernel stops after the rows the table says are real"
                 real += 1
-                key = (sbase + so * 16, dbase + do * 16)
+                key = (sbase + so * G, dbase + do * G)
                 assert key in owner, key
                 kb = k0 + bf                 # barriers executed before this store
                 lo = cs[kb - 1] + 1 if kb > 0 else 0          # it must belong to a step in [lo, hi]
                 hi = cs[kb] if kb < nb else n - 1
-                fit = [x for x in left[key] if lo <= x[0] <= hi]
+                # a barrier closes the step of every piece stored since the one before it; the
+                # -k repetitions hold identical pieces in several steps, so pick by that rule
+                # (after the rail's last barrier: its final step, the latest candidate)
+                fit = [x for x in left[key] if (x[0] == hi if kb < nb else lo <= x[0] <= hi)]
                 assert fit, ("stored outside its step's barriers, or twice", r, row, w, lo, hi, owner[key])
-                t, ln = fit[0]
-                left[key].remove(fit[0])
-                assert l16 * 16 == ln
+                pick = fit[0] if kb < nb else max(fit)
+                t, ln = pick
+                left[key].remove(pick)
+                assert l16 * G == ln
                 rail_steps.append(t)
             assert nrow == 0 or row < rows[r], "a barrier in a row the kernel skips"
             k0 += nrow
@@ -82,17 +89,31 @@ def interpret(steps, rails_max, sbase, dbase, xg, WAVES=16):
     return shape
 
 
-def random_steps(rng, nsteps, sbase, dbase):
+def random_steps(rng, nsteps, sbase, dbase, G=16):
     steps, so, do = [], 0, 0
     for _ in range(nsteps):
         st = []
         for _ in range(rng.choice([0, 1, 1, 2, 3, 5])):
-            ln = 16 * rng.randint(1, 300)
+            ln = G * rng.randint(1, 300 * 16 // G)
             st.append((sbase + so, dbase + do, ln))
-            so += ln + 16 * rng.randint(0, 4)
-            do += ln + 16 * rng.randint(0, 4)
+            so += ln + G * rng.randint(0, 4)
+            do += ln + G * rng.randint(0, 4)
         steps.append(st)
     return steps
+
+
+@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("G", [4, 1])
+@pytest.mark.parametrize("rails", [1, 7, 64, 512])
+def test_random_segments_fine_granules(xg, seed, G, rails):
+    """segments whose sizes are not multiples of 16 (any -d): descriptors in 4-B or 1-B
+    units on one-wave rails, executed by the same interpreter"""
+    rng = random.Random(seed * 131 + G * 7 + rails)
+    sbase, dbase = (1 << 32) + G * 3, (3 << 32) + G
+    steps = random_steps(rng, rng.randint(1, 60), sbase, dbase, G)
+    if not any(steps):
+        steps[0].append((sbase, dbase, 1000))
+    interpret(steps, rails, sbase, dbase, xg, WAVES=1, G=G)
 
 
 @pytest.mark.parametrize("seed", range(12))
@@ -108,11 +129,13 @@ def test_random_segments(xg, seed, rails, waves):
 
 @pytest.mark.parametrize("method", [6, 9, 10, 11, 12, 18])
 @pytest.mark.parametrize("k", [1, 3])
-@pytest.mark.parametrize("rails,waves", [(16, 16), (256, 1)])
-def test_readme_chain_plans(xg, method, k, rails, waves):
-    """the G = 1 plans of the README configuration (P32 A14 d2048 c3), as build_segments
-    hands them over: one transfer per local copy, SEND and RECV at 1 GiB apart"""
-    P, A, d, c = 32, 14, 2048, 3
+@pytest.mark.parametrize("rails,waves,d", [(16, 16, 2048), (256, 1, 2048), (512, 1, 1000), (512, 1, 33)])
+def test_readme_chain_plans(xg, method, k, rails, waves, d):
+    """the G = 1 plans of the README configuration (P32 A14 c3; d = 2048, and d = 1000 / 33
+    on 4-B / 1-B granules), as build_segments hands them over: one transfer per local
+    copy, SEND and RECV at 1 GiB apart"""
+    P, A, c = 32, 14, 3
+    G = 16 if d % 16 == 0 else 4 if d % 4 == 0 else 1
     s = xg.Schedule(method, P, A, d, c, xg.aggregator_list(P, A), ntimes=k)
     v = s.devplan(1, 0)
     base = {b: (1 << 32) + (b << 30) for b in range(xg.NBUF)}
@@ -123,8 +146,8 @@ def test_readme_chain_plans(xg, method, k, rails, waves):
         steps.pop()
     srcs = [x[0] for st in steps for x in st]
     dsts = [x[1] for st in steps for x in st]
-    shape = interpret(steps, rails, min(srcs), min(dsts), xg, WAVES=waves)
-    assert shape["rails"] == rails
+    shape = interpret(steps, rails, min(srcs), min(dsts), xg, WAVES=waves, G=G)
+    assert shape["rails"] == min(rails, sum((x[2] + PIECE - 1) // PIECE for st in steps for x in st))
 
 
 def test_rejects(xg):
@@ -144,6 +167,18 @@ def test_rejects(xg):
     rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 8, sb, db, waves=4)       # rails are 16 waves or 1
     assert rc == 3
     rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 513, sb, db, waves=1)     # at most 512 rails
+    assert rc == 3
+    rc, _s, *_ = xg.solo_tables([[(sb + 2, db, 64)]], 8, sb, db, waves=1, granule=4)   # not 4-B aligned
+    assert rc == 3
+    rc, _s, *_ = xg.solo_tables([[(sb + 4, db, 68)]], 8, sb, db, waves=1, granule=4)
+    assert rc == 0
+    rc, _s, *_ = xg.solo_tables([[(sb + 3, db + 1, 1001)]], 8, sb, db, waves=1, granule=1)
+    assert rc == 0
+    rc, _s, *_ = xg.solo_tables([[(sb + (1 << 24), db, 64)]], 8, sb, db, waves=1, granule=1)   # 16 MiB window
+    assert rc == 3
+    rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 8, sb, db, waves=16, granule=4)   # fine granules: one-wave rails
+    assert rc == 3
+    rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 8, sb, db, waves=1, granule=8)    # 16, 4 or 1
     assert rc == 3
 
 
