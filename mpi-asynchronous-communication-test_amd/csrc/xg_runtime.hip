@@ -60,6 +60,7 @@ struct xg_ctx {
     int64_t solo_max;          // solo segments move <= this many bytes per run
     int solo_rails;            // solo segments deal their pieces over up to this many rails
     int solo_waves;            // waves per rail: 16 (a workgroup) or 1
+    int solo_min_steps;        // a whole plan of fewer steps stays a copy launch
     int solo_relay;            // armed solo: rail 0 alone polls the doorbell and relays the ring
     int step_chain;            // 1: time runs of one-launch local steps by in-kernel stamps (xg_plan_run)
     int piece_order;           // local pieces of a launch: 0 message order, 1 by destination, 2 by source
@@ -285,6 +286,8 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->solo_rails = c->solo_waves == 1 ? 512 : 16;     // 512 one-wave rails: 2 per CU by LDS
     env = getenv("XG_SOLO_RAILS");
     if (env && atoi(env) > 0) c->solo_rails = std::min(atoi(env), xgk::kSoloMaxRails);
+    env = getenv("XG_SOLO_MIN_STEPS");       // plans of fewer steps never run as an armed solo launch
+    c->solo_min_steps = env ? atoi(env) : 1;  // profiles/r02/one_step/: armed beats the event-timed launch
     env = getenv("XG_PIECE_ORDER");          // profiles/r02/piece_order/: by destination is fastest
     c->piece_order = env ? atoi(env) : 1;
     env = getenv("XG_STEP_CHAIN");           // "0": an event after every step launch
@@ -606,10 +609,11 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         while (s < e && !p->steps[s].pre_n) ++s;
         while (e > s && !p->steps[e - 1].pre_n) --e;
         for (int t = s; t < e; ++t) busy += p->steps[t].pre_n > 0;
-        // one busy step is worth an (armed) engine launch only as the whole plan, and only
-        // when that plan has more steps than it (a one-step plan is one copy launch, whose
-        // event-timed ~6 us beat the armed launch's host round trip)
-        const bool whole = s_run == 0 && run_end == p->nsteps && p->nsteps >= 2 && c->engine_arm && !c->virt;
+        // one busy step is worth an (armed) engine launch only as the whole plan: a small
+        // one-step plan armed on rails takes 5 us against 6 us (10-24 us cold) as an
+        // event-timed copy launch (profiles/r02/one_step/; XG_SOLO_MIN_STEPS=2 restores it)
+        const bool whole = s_run == 0 && run_end == p->nsteps && p->nsteps >= c->solo_min_steps && c->engine_arm &&
+                           !c->virt;
         if (busy < (whole ? 1 : 2)) {
             s = run_end > s ? run_end : s + 1;
             continue;

@@ -141,7 +141,8 @@ def test_step_engine_matches_per_step_launches(xg, ctx, method, d):
         for name, cx in (("engine", ctx), ("eager", ctx_eager)):
             run = xg.MethodRun(cx, s, it=it, mode=1)
             try:
-                assert (run.engine_workgroups > 0) == (name != "eager" and run.nsteps >= 2), (name, run.nsteps)
+                if name == "eager" or run.nsteps >= 2:     # one-step plans: armed solo when small enough
+                    assert (run.engine_workgroups > 0) == (name != "eager"), (name, run.nsteps)
                 done, post, wall = run.run_timed()
                 assert all(0 <= a <= b for a, b in zip(done, done[1:])), done
                 assert done[-1] <= wall + 1e-4
