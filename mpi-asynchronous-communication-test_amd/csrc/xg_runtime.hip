@@ -591,6 +591,163 @@ static bool solo_pays(int64_t bytes, int n, int rails, int wv, int busy, int gra
     return solo < grid;
 }
 
+// One engine segment candidate: steps [s0, s1) with their transfers (chunk-sized pieces
+// re-joined), hazard flags, solo granule and shape.  Nothing is committed to the plan.
+struct SegCand {
+    int s0, s1, n;
+    std::vector<std::vector<xgk::DCopy>> xfer;
+    std::vector<xg_span> spans;
+    std::vector<int> tb, fl;
+    int64_t bytes, maxstep;
+    int nhaz, gran;
+    uintptr_t slo, shi, dlo, dhi;
+    xg_solo_shape sh;
+    bool fits;                     // the solo tables can be built (limits, alignment, window)
+};
+
+static SegCand seg_candidate(const xg_plan *p, const std::vector<xgk::DCopy> &pieces, int s0, int s1)
+{
+    const xg_ctx *c = p->ctx;
+    SegCand k{};
+    k.s0 = s0; k.s1 = s1; k.n = s1 - s0;
+    k.xfer.resize(k.n);
+    for (int t = s0; t < s1; ++t) {
+        const StepR &st = p->steps[t];
+        for (int i = st.local_b; i < st.local_b + st.local_n;) {     // eligible steps hold no packs
+            const uint8_t *src = pieces[i].src;
+            uint8_t *dst = pieces[i].dst;
+            int64_t len = pieces[i].len;
+            for (++i; i < st.local_b + st.local_n && pieces[i].src == src + len && pieces[i].dst == dst + len; ++i)
+                len += pieces[i].len;
+            k.xfer[t - s0].push_back({src, dst, len});
+        }
+        k.bytes += st.local_bytes + st.pack_bytes;
+        k.maxstep = std::max(k.maxstep, st.local_bytes + st.pack_bytes);
+    }
+    k.tb.assign(k.n + 1, 0);
+    for (int t = 0; t < k.n; ++t) {
+        k.tb[t + 1] = k.tb[t] + (int)k.xfer[t].size();
+        for (const xgk::DCopy &x : k.xfer[t])
+            k.spans.push_back({(uint64_t)(uintptr_t)x.src, (uint64_t)(uintptr_t)x.dst, (uint64_t)x.len});
+    }
+    // hazards over whole transfers (host scan)
+    k.fl.assign(k.n, 0);
+    k.nhaz = xg_engine_hazards(k.spans.data(), k.tb.data(), k.n, c->engine_drain, k.fl.data());
+    // solo granule: the largest of 16 / 4 / 1 every transfer is aligned to (segment sizes
+    // that are not multiples of 16 move on 4-B or 1-B accesses, one-wave rails only)
+    uint64_t bits = 0;
+    for (const xg_span &x : k.spans) bits |= x.src | x.dst | x.len;
+    k.gran = (bits & 15) == 0 ? 16 : (bits & 3) == 0 ? 4 : 1;
+    // solo: each step's 1 KiB pieces dealt round-robin over up to solo_rails rails, per
+    // rail rows of kSoloWaves pieces (xg_solo_tables_g, host/solo.c)
+    k.slo = k.dlo = UINTPTR_MAX;
+    k.shi = k.dhi = 0;
+    for (const xg_span &x : k.spans)
+        if (x.len > 0) {
+            k.slo = std::min<uintptr_t>(k.slo, x.src); k.shi = std::max<uintptr_t>(k.shi, x.src + x.len);
+            k.dlo = std::min<uintptr_t>(k.dlo, x.dst); k.dhi = std::max<uintptr_t>(k.dhi, x.dst + x.len);
+        }
+    k.fits = (k.gran == 16 || c->solo_waves == 1) && k.shi > k.slo && k.dhi > k.dlo && k.n <= xgk::kSoloMaxSteps &&
+             k.bytes <= c->solo_max &&
+             xg_solo_tables_g(k.spans.data(), k.tb.data(), k.n, c->solo_rails, c->solo_waves, k.gran, k.slo, k.dlo,
+                              &k.sh, nullptr, nullptr) == XG_OK;
+    return k;
+}
+
+// Cut a hazard-free run [s0, s1) that is too long for one solo launch (steps, bytes, pieces
+// per rail, the descriptors' offset window) into consecutive sub-runs that each fit, greedily
+// from per-step totals; empty if some single step does not fit on its own.
+static std::vector<std::pair<int, int>> solo_split(const xg_plan *p, const SegCand &k)
+{
+    const xg_ctx *c = p->ctx;
+    std::vector<std::pair<int, int>> out;
+    const int64_t rows_cap = xgk::kSoloMaxPieces - 3 * xgk::kSoloK * c->solo_waves;   // padding headroom
+    const int64_t pieces_cap = (int64_t)c->solo_rails * rows_cap;
+    const uint64_t window = (uint64_t)xgk::kSoloOffMax * (uint64_t)k.gran;
+    int a = k.s0;
+    int64_t bytes = 0, np = 0;
+    uintptr_t slo = UINTPTR_MAX, shi = 0, dlo = UINTPTR_MAX, dhi = 0;
+    for (int t = k.s0; t < k.s1; ++t) {
+        int64_t tb = 0, tp = 0;
+        uintptr_t tsl = UINTPTR_MAX, tsh = 0, tdl = UINTPTR_MAX, tdh = 0;
+        for (const xgk::DCopy &x : k.xfer[t - k.s0]) {
+            if (x.len <= 0) continue;
+            tb += x.len;
+            tp += (x.len + xgk::kSoloPiece - 1) / xgk::kSoloPiece;
+            tsl = std::min<uintptr_t>(tsl, (uintptr_t)x.src); tsh = std::max<uintptr_t>(tsh, (uintptr_t)x.src + x.len);
+            tdl = std::min<uintptr_t>(tdl, (uintptr_t)x.dst); tdh = std::max<uintptr_t>(tdh, (uintptr_t)x.dst + x.len);
+        }
+        auto ok = [&](int steps, int64_t b, int64_t q, uintptr_t sl, uintptr_t sh, uintptr_t dl, uintptr_t dh) {
+            return steps <= xgk::kSoloMaxSteps && b <= c->solo_max && q <= pieces_cap &&
+                   (sh <= sl || sh - sl <= window) && (dh <= dl || dh - dl <= window);
+        };
+        if (!ok(1, tb, tp, tsl, tsh, tdl, tdh)) return {};
+        if (!ok(t + 1 - a, bytes + tb, np + tp, std::min(slo, tsl), std::max(shi, tsh), std::min(dlo, tdl),
+                std::max(dhi, tdh))) {
+            out.push_back({a, t});
+            a = t;
+            bytes = np = 0;
+            slo = dlo = UINTPTR_MAX;
+            shi = dhi = 0;
+        }
+        bytes += tb;
+        np += tp;
+        slo = std::min(slo, tsl); shi = std::max(shi, tsh);
+        dlo = std::min(dlo, tdl); dhi = std::max(dhi, tdh);
+    }
+    out.push_back({a, k.s1});
+    return out;
+}
+
+// Commit a candidate as an engine segment (solo tables or grid units) to the plan.
+static int commit_seg(xg_plan *p, SegCand &k, bool solo, std::vector<xgk::DCopy> &ep, std::vector<int> &sb)
+{
+    xg_ctx *c = p->ctx;
+    EngSeg g;
+    g.s0 = k.s0; g.s1 = k.s1; g.bytes = k.bytes; g.nhaz = k.nhaz;
+    g.solo = solo;
+    g.wv = c->solo_waves;
+    g.gran = k.gran;
+    g.b = k.maxstep <= (1 << 20) ? 1 : (k.maxstep <= (4 << 20) ? 4 : 16);
+    g.sb_off = (int)sb.size();
+    const int n = k.n;
+    if (solo) {
+        g.sbase = (const uint8_t *)k.slo;
+        g.dbase = (uint8_t *)k.dlo;
+        g.u0 = (int)p->solo_desc.size();
+        g.w = k.sh.rails;
+        g.npieces = k.sh.npieces;
+        std::vector<int> meta(k.sh.nmeta);
+        p->solo_desc.resize(g.u0 + (size_t)k.sh.rails * k.sh.npieces);
+        if (xg_solo_tables_g(k.spans.data(), k.tb.data(), n, c->solo_rails, c->solo_waves, k.gran, k.slo, k.dlo, &k.sh,
+                             reinterpret_cast<uint64_t *>(p->solo_desc.data()) + g.u0, meta.data()) != XG_OK)
+            return XG_EARG;
+        sb.insert(sb.end(), meta.begin(), meta.end());
+    } else {
+        // grid units: the step's transfers cut to B * 4 KiB, one burst of B 16-B loads per lane
+        const int64_t unit = (int64_t)g.b * xgk::kThreads * 16;
+        const int u0 = (int)ep.size();
+        std::vector<int> beg(n + 1);
+        int maxu = 0;
+        for (int t = 0; t < n; ++t) {
+            beg[t] = (int)ep.size() - u0;
+            for (const xgk::DCopy &x : k.xfer[t])
+                for (int64_t o = 0; o < x.len; o += unit)
+                    ep.push_back({x.src + o, x.dst + o, x.len - o < unit ? x.len - o : unit});
+            maxu = std::max(maxu, (int)ep.size() - u0 - beg[t]);
+        }
+        beg[n] = (int)ep.size() - u0;
+        g.w = std::max(1, std::min(maxu, c->engine_wmax));
+        g.npieces = 0;
+        g.u0 = 0;
+        for (int t = 0; t <= n; ++t) sb.push_back(u0 + beg[t]);
+        sb.insert(sb.end(), k.fl.begin(), k.fl.end());
+    }
+    for (int t = k.s0; t < k.s1; ++t) p->seg_of[t] = (int)p->segs.size();
+    p->segs.push_back(g);
+    return XG_OK;
+}
+
 static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
 {
     xg_ctx *c = p->ctx;
@@ -598,6 +755,7 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
     if (c->engine_max_step <= 0) return XG_OK;
     std::vector<xgk::DCopy> ep;
     std::vector<int> sb;
+    int rc;
     for (int s = 0; s < p->nsteps;) {
         int e = s;
         const int s_run = s;
@@ -618,94 +776,35 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
             s = run_end > s ? run_end : s + 1;
             continue;
         }
-        EngSeg g;
-        g.s0 = s; g.s1 = e; g.bytes = 0;
-        int64_t maxstep = 0;
-        std::vector<std::vector<xgk::DCopy>> xfer(e - s);
-        for (int t = s; t < e; ++t) {
-            const StepR &st = p->steps[t];
-            for (int i = st.local_b; i < st.local_b + st.local_n;) {     // eligible steps hold no packs
-                const uint8_t *src = pieces[i].src;
-                uint8_t *dst = pieces[i].dst;
-                int64_t len = pieces[i].len;
-                for (++i; i < st.local_b + st.local_n && pieces[i].src == src + len && pieces[i].dst == dst + len; ++i)
-                    len += pieces[i].len;
-                xfer[t - s].push_back({src, dst, len});
+        SegCand k = seg_candidate(p, pieces, s, e);
+        const bool solo = k.nhaz == 0 && k.fits && c->solo &&
+                          solo_pays(k.bytes, k.n, k.sh.rails, c->solo_waves, busy, k.gran);
+        if (!solo && k.nhaz == 0 && c->solo && !k.fits && k.n >= 2) {
+            // too long for one solo launch (more than kSoloMaxSteps steps -- e.g. a large -k --,
+            // more bytes or pieces per rail than one launch holds): consecutive solo launches,
+            // each a kernel boundary, when that beats one grid launch's barrier per step
+            std::vector<std::pair<int, int>> cut = solo_split(p, k);
+            std::vector<SegCand> parts;
+            bool all = !cut.empty() && cut.size() > 1;
+            for (size_t i = 0; all && i < cut.size(); ++i) {
+                parts.push_back(seg_candidate(p, pieces, cut[i].first, cut[i].second));
+                all = parts.back().fits && parts.back().nhaz == 0;
             }
-            g.bytes += st.local_bytes + st.pack_bytes;
-            maxstep = std::max(maxstep, st.local_bytes + st.pack_bytes);
+            const double traffic = 2.0 * (double)k.bytes;
+            const double grid = traffic / 5e12 + k.n * 1.0e-6;
+            const double split = (double)cut.size() * 6e-6 + traffic / (6e12 * k.gran / 16.0) + k.n * 0.05e-6;
+            if (all && split < grid) {
+                for (SegCand &q : parts)
+                    if ((rc = commit_seg(p, q, true, ep, sb))) return rc;
+                s = e;
+                continue;
+            }
         }
-        g.b = maxstep <= (1 << 20) ? 1 : (maxstep <= (4 << 20) ? 4 : 16);
-        const int64_t unit = (int64_t)g.b * xgk::kThreads * 16;
-        const int n = e - s, u0 = (int)ep.size();
-        std::vector<int> beg(n + 1);
-        std::vector<xg_span> spans;
-        int maxu = 0;
-        for (int t = 0; t < n; ++t) {
-            beg[t] = (int)ep.size() - u0;
-            for (const xgk::DCopy &x : xfer[t]) {
-                spans.push_back({(uint64_t)(uintptr_t)x.src, (uint64_t)(uintptr_t)x.dst, (uint64_t)x.len});
-                for (int64_t o = 0; o < x.len; o += unit)
-                    ep.push_back({x.src + o, x.dst + o, x.len - o < unit ? x.len - o : unit});
-            }
-            maxu = std::max(maxu, (int)ep.size() - u0 - beg[t]);
-        }
-        beg[n] = (int)ep.size() - u0;
-        // hazards over whole transfers: re-cut beg in transfer units for the host scan
-        std::vector<int> tb(n + 1, 0);
-        for (int t = 0; t < n; ++t) tb[t + 1] = tb[t] + (int)xfer[t].size();
-        std::vector<int> fl(n);
-        g.nhaz = xg_engine_hazards(spans.data(), tb.data(), n, c->engine_drain, fl.data());
-        g.w = std::max(1, std::min(maxu, c->engine_wmax));
-        g.sb_off = (int)sb.size();
-        // solo granule: the largest of 16 / 4 / 1 every transfer is aligned to (segment sizes
-        // that are not multiples of 16 move on 4-B or 1-B accesses, one-wave rails only)
-        uint64_t bits = 0;
-        for (const auto &xs : xfer)
-            for (const xgk::DCopy &x : xs) bits |= (uintptr_t)x.src | (uintptr_t)x.dst | (uint64_t)x.len;
-        const int gran = (bits & 15) == 0 ? 16 : (bits & 3) == 0 ? 4 : 1;
-        // solo: each step's 1 KiB pieces dealt round-robin over up to solo_rails rails, per
-        // rail rows of kSoloWaves pieces (xg_solo_tables, host/solo.c)
-        uintptr_t slo = UINTPTR_MAX, shi = 0, dlo = UINTPTR_MAX, dhi = 0;
-        for (const xg_span &x : spans)
-            if (x.len > 0) {
-                slo = std::min<uintptr_t>(slo, x.src); shi = std::max<uintptr_t>(shi, x.src + x.len);
-                dlo = std::min<uintptr_t>(dlo, x.dst); dhi = std::max<uintptr_t>(dhi, x.dst + x.len);
-            }
-        xg_solo_shape sh{};
-        const bool fits = (gran == 16 || c->solo_waves == 1) && shi > slo && dhi > dlo && n <= xgk::kSoloMaxSteps &&
-                          xg_solo_tables_g(spans.data(), tb.data(), n, c->solo_rails, c->solo_waves, gran, slo, dlo, &sh,
-                                           nullptr, nullptr) == XG_OK;
-        g.solo = g.nhaz == 0 && fits && c->solo && g.bytes <= c->solo_max &&
-                 solo_pays(g.bytes, n, sh.rails, c->solo_waves, busy, gran);
-        g.wv = c->solo_waves;
-        g.gran = gran;
-        if (!g.solo && busy < 2) {      // one busy step: an engine launch only if it runs solo
-            ep.resize(u0);
+        if (!solo && busy < 2) {      // one busy step: an engine launch only if it runs solo
             s = run_end;
             continue;
         }
-        if (g.solo) {
-            g.sbase = (const uint8_t *)slo;
-            g.dbase = (uint8_t *)dlo;
-            ep.resize(u0);
-            g.u0 = (int)p->solo_desc.size();
-            g.w = sh.rails;
-            g.npieces = sh.npieces;
-            std::vector<int> meta(sh.nmeta);
-            p->solo_desc.resize(g.u0 + (size_t)sh.rails * sh.npieces);
-            if (xg_solo_tables_g(spans.data(), tb.data(), n, c->solo_rails, c->solo_waves, gran, slo, dlo, &sh,
-                               reinterpret_cast<uint64_t *>(p->solo_desc.data()) + g.u0, meta.data()) != XG_OK)
-                return XG_EARG;
-            sb.insert(sb.end(), meta.begin(), meta.end());
-        } else {
-            g.npieces = 0;
-            g.u0 = 0;
-            for (int t = 0; t <= n; ++t) sb.push_back(u0 + beg[t]);
-            sb.insert(sb.end(), fl.begin(), fl.end());
-        }
-        for (int t = s; t < e; ++t) p->seg_of[t] = (int)p->segs.size();
-        p->segs.push_back(g);
+        if ((rc = commit_seg(p, k, solo, ep, sb))) return rc;
         s = e;
     }
     if (p->segs.empty()) return XG_OK;

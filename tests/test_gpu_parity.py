@@ -263,3 +263,49 @@ def test_solo_engine_fine_granules(xg, method, d, k):
         finally:
             cx.close()
     assert res["solo"] == res["eager"]
+
+
+@pytest.mark.parametrize("method,k,env", [(6, 60, {}), (9, 70, {}), (12, 2, {"XG_ENGINE_SOLO_MAX": "262144"}),
+                                          (18, 3, {"XG_ENGINE_SOLO_MAX": "1048576"}), (1, 200, {})])
+def test_long_runs_split_into_solo_launches(xg, method, k, env):
+    """A hazard-free run too long for one solo launch (more than 2048 steps at a large -k,
+    or more bytes than XG_ENGINE_SOLO_MAX) becomes consecutive solo launches instead of
+    one grid launch with a barrier per step: same bytes as per-step launches, step times
+    ordered, every slot against the oracle."""
+    import os
+    import xg_oracle as O
+    P, A, d, c, it = 32, 14, 2048, 3, 0
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, iteration=it)
+    exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
+    res = {}
+    for name, extra in (("split", env), ("grid", {"XG_ENGINE_SOLO": "0"}), ("eager", {"XG_ENGINE_MAX_STEP": "0"})):
+        os.environ.update(extra)
+        try:
+            cx = xg.Context(rank=0, nranks=1, device=0)
+        finally:
+            for key in extra:
+                del os.environ[key]
+        try:
+            run = xg.MethodRun(cx, s, it=it, mode=1)
+            try:
+                if name == "split":
+                    n_eng, nseg, nhaz = run.engine_steps()
+                    assert nseg >= 2 and nhaz == 0 and run.engine_rails > 0, (n_eng, nseg, nhaz, run.nsteps)
+                for _rep in range(2):
+                    done, _post, wall = run.run_timed()
+                    assert all(0 <= a <= b for a, b in zip(done, done[1:])), name
+                    assert done[-1] <= wall + 1e-4
+                chk, bad, _f = run.verify()
+                assert all(b == 0 for b in bad), name
+                for (src, seed, dst, off), ck in zip(run.slots, chk):
+                    local = off - s.recv_offset(1, dst)
+                    assert ck == O.chk64(exp[dst][local: local + d]), (name, method, src, dst)
+                res[name] = (chk, done[-1])
+            finally:
+                run.close()
+        finally:
+            cx.close()
+    assert res["split"][0] == res["eager"][0] == res["grid"][0]
+    print("method %d -k %d: split solo %.1f us, grid engine %.1f us, per-step launches %.1f us"
+          % (method, k, res["split"][1] * 1e6, res["grid"][1] * 1e6, res["eager"][1] * 1e6))
