@@ -221,6 +221,10 @@ int xg_engine_hazards(const xg_span *xfer, const int *step_begin, int nsteps, in
 #define XG_SOLO_MAX_STEPS 2048
 #define XG_SOLO_MAX_PIECES 4608
 #define XG_SOLO_OFF_MAX (1ull << 24)
+/* waves = 1 (one-wave rails): the WIDE form -- descriptor = src | dst << 32 (granules, so
+ * windows of XG_SOLO_WIDE_OFF_MAX granules), and each row's meta word = barrier count (bits
+ * 0-7, all preceding the row's one piece) | the piece's length in granules << 8. */
+#define XG_SOLO_WIDE_OFF_MAX (1ull << 32)
 typedef struct { int32_t rails, npieces, nrows, nmeta; } xg_solo_shape;
 int xg_solo_tables(const xg_span *xfer, const int *step_begin, int nsteps, int rails_max, int waves,
                    uint64_t src_base, uint64_t dst_base, xg_solo_shape *shape, uint64_t *descs, int *meta);

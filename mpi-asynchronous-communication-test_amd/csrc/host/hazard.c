@@ -55,12 +55,57 @@ static int meets(const ivl *v, int n, uint64_t a, uint64_t b, int want, int64_t 
     return 0;
 }
 
+/* Fast path, O(N log N) once: when no transfer reads bytes that any transfer writes (the
+ * source and destination hulls are disjoint, as for every SEND -> RECV plan) and no two
+ * writes of the same bytes carry different data (one sort of every write by address),
+ * there is no hazard anywhere.  Returns 1 when that holds. */
+static int hazard_free(const xg_span *xfer, int n)
+{
+    uint64_t slo = UINT64_MAX, shi = 0, dlo = UINT64_MAX, dhi = 0;
+    int i, m = 0, ok = 1;
+    for (i = 0; i < n; ++i)
+        if (xfer[i].len) {
+            if (xfer[i].src < slo) slo = xfer[i].src;
+            if (xfer[i].src + xfer[i].len > shi) shi = xfer[i].src + xfer[i].len;
+            if (xfer[i].dst < dlo) dlo = xfer[i].dst;
+            if (xfer[i].dst + xfer[i].len > dhi) dhi = xfer[i].dst + xfer[i].len;
+            m++;
+        }
+    if (!m) return 1;
+    if (slo < dhi && dlo < shi) return 0;            /* a read may meet a write: full scan */
+    ivl *w = (ivl *)malloc(sizeof(ivl) * (size_t)m);
+    if (!w) return 0;
+    for (i = 0, m = 0; i < n; ++i)
+        if (xfer[i].len) {
+            w[m].lo = xfer[i].dst;
+            w[m].hi = xfer[i].dst + xfer[i].len;
+            w[m].delta = (int64_t)(xfer[i].dst - xfer[i].src);
+            m++;
+        }
+    qsort(w, (size_t)m, sizeof(ivl), cmp_ivl);
+    uint64_t reach = 0;                               /* end of the writes seen so far ... */
+    int64_t rdelta = 0;                               /* ... and the delta of the one reaching it */
+    for (i = 0; i < m && ok; ++i) {
+        if (i && w[i].lo < reach && w[i].delta != rdelta) ok = 0;   /* overlap, other bytes */
+        if (w[i].hi > reach) {
+            reach = w[i].hi;
+            rdelta = w[i].delta;
+        }
+    }
+    free(w);
+    return ok;
+}
+
 int xg_engine_hazards(const xg_span *xfer, const int *step_begin, int nsteps, int force, int *flags)
 {
     ivl *pend = NULL, *tmp = NULL;
     int npend = 0, cap = 0, s, k, nhaz = 0;
     if (nsteps <= 0) return 0;
     for (s = 0; s < nsteps; ++s) flags[s] = force ? 1 : 0;
+    if (hazard_free(xfer, step_begin[nsteps])) {
+        if (flags[nsteps - 1] < 1) flags[nsteps - 1] = 1;
+        return 0;
+    }
     for (s = 0; s < nsteps; ++s) {
         const int b = step_begin[s], e = step_begin[s + 1];
         int hazard = 0, nnew = 0, n, m;

@@ -21,6 +21,11 @@
  * alignment every transfer must have -- 16 for the 16-B loads/stores of aligned
  * segments, 4 and 1 for segment sizes that are not multiples of 16 (any -d); the
  * kernel then moves a piece with 4-B or 1-B accesses (xg_solo_tables_g).
+ *
+ * One-wave rails (waves = 1) use the WIDE form: a row is one piece, so the row's
+ * barrier word carries the piece's length (bits 8-19) beside the barrier count
+ * (bits 0-7, all of which precede the piece), and the descriptor is two 32-bit
+ * offsets in granules (src | dst << 32): 4-64 GiB windows instead of 16-256 MiB.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -47,12 +52,14 @@ int xg_solo_tables_g(const xg_span *xfer, const int *step_begin, int nsteps, int
     const int W = waves;       /* pieces per row: one per wave of a rail */
     const uint64_t G = (uint64_t)granule;
     const int bshift = XG_SOLO_BEFORE_SHIFT(granule);
+    const int wide = W == 1;
+    const uint64_t offmax = wide ? XG_SOLO_WIDE_OFF_MAX : XG_SOLO_OFF_MAX;
     int64_t total = 0;
     for (int i = 0; i < nx; ++i) {
         const xg_span *x = &xfer[i];
         if ((x->src | x->dst | x->len) & (G - 1)) return XG_EARG;
-        if (x->len && (x->src < src_base || x->dst < dst_base || (x->src + x->len - src_base) / G > XG_SOLO_OFF_MAX ||
-                       (x->dst + x->len - dst_base) / G > XG_SOLO_OFF_MAX))
+        if (x->len && (x->src < src_base || x->dst < dst_base || (x->src + x->len - src_base) / G > offmax ||
+                       (x->dst + x->len - dst_base) / G > offmax))
             return XG_EARG;
         total += (int64_t)((x->len + XG_SOLO_PIECE - 1) / XG_SOLO_PIECE);
     }
@@ -96,12 +103,19 @@ int xg_solo_tables_g(const xg_span *xfer, const int *step_begin, int nsteps, int
                     const int64_t at = pend[cur], row = at / W;
                     close[(size_t)cur * (nrows + 1) + row]++;
                     cstep[(size_t)cur * nsteps + nb[cur]++] = pstep[cur];
-                    for (int64_t w = at % W; w < W; ++w)
-                        descs[(size_t)cur * np + row * W + w] += 1ull << bshift;
+                    if (!wide)                                   /* wide: `before` = the row's count */
+                        for (int64_t w = at % W; w < W; ++w)
+                            descs[(size_t)cur * np + row * W + w] += 1ull << bshift;
                     pend[cur] = -1;
                 }
-                descs[(size_t)cur * np + cnt[cur]++] +=     /* its `before` bits may be set already */
-                    desc((xfer[i].src + o - src_base) / G, (xfer[i].dst + o - dst_base) / G, len / G);
+                if (wide) {
+                    close[(size_t)cur * (nrows + 1) + cnt[cur]] |= (int)((len / G) << 8);
+                    descs[(size_t)cur * np + cnt[cur]++] =
+                        ((xfer[i].src + o - src_base) / G) | (((xfer[i].dst + o - dst_base) / G) << 32);
+                } else {
+                    descs[(size_t)cur * np + cnt[cur]++] +=     /* its `before` bits may be set already */
+                        desc((xfer[i].src + o - src_base) / G, (xfer[i].dst + o - dst_base) / G, len / G);
+                }
                 used[cur] = 1;
                 cur = (cur + 1) % rails;
             }

@@ -26,6 +26,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace xgk {
 
@@ -594,6 +595,14 @@ constexpr int kSoloMaxRails = 512;
 // j of lane l at G * (l + 64 j) -- each instruction covers 64 consecutive granules of the
 // piece -- and the range check drops the granules past its end exactly.  The length field
 // widens (7 / 9 / 11 bits for up to 1 KiB), so `before` moves up (55 / 57 / 59).
+// One-wave rails (WV = 1) use the WIDE form instead: a row is one piece, so the row's
+// barrier word carries the piece's length (bits 8-19, granules) beside its barrier count
+// (bits 0-7; every barrier of the row precedes its one piece, so `before` = the count),
+// and the 64-bit descriptor holds two 32-bit offsets in granules: windows of 4 GiB (G = 1)
+// to 64 GiB (G = 16) instead of 16-256 MiB, so a run whose sources or destinations span
+// a whole large region (16384 logical ranks on one GPU) still fits one table.
+constexpr uint64_t kSoloWideOffMax = 1ull << 32;
+
 template <int G>
 struct SoloFmt {
     static constexpr int kShift = G == 16 ? 4 : G == 4 ? 2 : 0;       // log2 G
@@ -627,10 +636,31 @@ __device__ __forceinline__ unsigned long long solo_uniform(unsigned long long d)
            (unsigned)__builtin_amdgcn_readfirstlane((int)d);
 }
 
+// a piece's source / destination offsets and length in granules, from its descriptor and
+// (wide form, WV = 1) its row's barrier word
+template <int WV, int G>
+__device__ __forceinline__ uint64_t solo_src(unsigned long long d)
+{
+    return WV == 1 ? (d & 0xFFFFFFFFull) : (d & (kSoloOffMax - 1));
+}
+template <int WV, int G>
+__device__ __forceinline__ uint64_t solo_dst(unsigned long long d)
+{
+    return WV == 1 ? (d >> 32) : ((d >> 24) & (kSoloOffMax - 1));
+}
+template <int WV, int G>
+__device__ __forceinline__ int64_t solo_len(unsigned long long d, unsigned row_word)
+{
+    return WV == 1 ? (int64_t)((row_word >> 8) & 0xFFF) : (int64_t)((d >> 48) & ((1u << SoloFmt<G>::kLenBits) - 1));
+}
+template <int WV>
+using SoloRowT = typename std::conditional<WV == 1, unsigned, unsigned short>::type;
+
 // issue the loads of chunk c of this wave (rows of WV pieces)
 template <int K, int WV, int G>
-__device__ __forceinline__ void solo_load(SoloChunk<K, G> &b, const unsigned long long *ldesc, int c, int wave,
-                                          uint64_t l16, const uint8_t *src_base)
+__device__ __forceinline__ void solo_load(SoloChunk<K, G> &b, const unsigned long long *ldesc,
+                                          const SoloRowT<WV> *lclose, int c, int wave, uint64_t l16,
+                                          const uint8_t *src_base)
 {
     using F = SoloFmt<G>;
 #pragma unroll
@@ -641,8 +671,8 @@ __device__ __forceinline__ void solo_load(SoloChunk<K, G> &b, const unsigned lon
         // (num_records = the piece's bytes) drops the lanes past its end -- an empty
         // padding piece moves nothing
         const unsigned long long d = solo_uniform(b.d[k]);
-        const brsrc r = make_rsrc(src_base + ((d & (kSoloOffMax - 1)) << F::kShift),
-                                  (int64_t)((d >> 48) & ((1u << F::kLenBits) - 1)) << F::kShift);
+        const unsigned rw = WV == 1 ? (unsigned)__builtin_amdgcn_readfirstlane((int)lclose[c * K + k]) : 0u;
+        const brsrc r = make_rsrc(src_base + (solo_src<WV, G>(d) << F::kShift), solo_len<WV, G>(d, rw) << F::kShift);
         if constexpr (G == 16) {
             const u32x4 x = bload16(r, (int)l16 * 16);
             b.v[k][0] = x.x; b.v[k][1] = x.y; b.v[k][2] = x.z; b.v[k][3] = x.w;
@@ -666,8 +696,8 @@ __device__ __forceinline__ void solo_close(unsigned long long *ts, const short *
 
 // store chunk c in row order; a row that begins new steps first closes the ones before
 // it: barrier (every wave issued their stores), stamp
-template <int K, int G>
-__device__ __forceinline__ void solo_store(const SoloChunk<K, G> &b, const unsigned short *lclose, const short *lcstep,
+template <int K, int WV, int G>
+__device__ __forceinline__ void solo_store(const SoloChunk<K, G> &b, const SoloRowT<WV> *lclose, const short *lcstep,
                                           unsigned long long *ts, int &s, int c, int rows, uint64_t l16,
                                           uint8_t *dst_base)
 {
@@ -675,14 +705,15 @@ __device__ __forceinline__ void solo_store(const SoloChunk<K, G> &b, const unsig
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         if (c * K + k >= rows) break;         // padding rows: no piece, no barrier
-        const int n = __builtin_amdgcn_readfirstlane((int)lclose[c * K + k]);     // barriers in this row
-        const int bf = __builtin_amdgcn_readfirstlane((int)(b.d[k] >> F::kBefore));  // ... before my piece
+        const unsigned rw = (unsigned)__builtin_amdgcn_readfirstlane((int)lclose[c * K + k]);
+        const int n = WV == 1 ? (int)(rw & 0xFF) : (int)rw;                      // barriers in this row
+        // ... before my piece (wide form: all of them)
+        const int bf = WV == 1 ? n : __builtin_amdgcn_readfirstlane((int)(b.d[k] >> F::kBefore));
         int j = 0;
         for (; j < bf; ++j) solo_close(ts, lcstep, s);
         asm volatile("" ::: "memory");        // the store stays between its steps' barriers
         const unsigned long long d = solo_uniform(b.d[k]);
-        const brsrc r = make_rsrc(dst_base + (((d >> 24) & (kSoloOffMax - 1)) << F::kShift),
-                                  (int64_t)((d >> 48) & ((1u << F::kLenBits) - 1)) << F::kShift);
+        const brsrc r = make_rsrc(dst_base + (solo_dst<WV, G>(d) << F::kShift), solo_len<WV, G>(d, rw) << F::kShift);
         if constexpr (G == 16) {
             u32x4 x;
             x.x = b.v[k][0]; x.y = b.v[k][1]; x.z = b.v[k][2]; x.w = b.v[k][3];
@@ -711,7 +742,7 @@ __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned lon
     const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
     const int rail = (int)blockIdx.x, R = (int)gridDim.x;
     __shared__ unsigned long long ldesc[kSoloMaxPieces];
-    __shared__ unsigned short lclose[kSoloMaxPieces / WV + 1];
+    __shared__ SoloRowT<WV> lclose[kSoloMaxPieces / WV + 1];
     __shared__ short lcstep[kSoloMaxSteps];
     __shared__ unsigned long long ts[kSoloMaxSteps];
     __shared__ int give_up;
@@ -723,7 +754,7 @@ __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned lon
     const int rows = meta[R * (nrows + 1) + R * nsteps + rail];     // rows holding real pieces
     const int nreal = (rows + K - 1) / K;                              // ... in that many chunks
     for (int i = (int)threadIdx.x; i < npieces; i += kT) ldesc[i] = desc[i];
-    for (int i = (int)threadIdx.x; i <= nrows; i += kT) lclose[i] = (unsigned short)row_close[i];
+    for (int i = (int)threadIdx.x; i <= nrows; i += kT) lclose[i] = (SoloRowT<WV>)row_close[i];
     for (int i = (int)threadIdx.x; i < nsteps; i += kT) {
         lcstep[i] = (short)cstep[i];
         ts[i] = 0;
@@ -771,13 +802,13 @@ __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned lon
     // the loop leaves after the last chunk that holds real pieces.
     SoloChunk<K, G> A, B;
     int k = 0;
-    solo_load<K, WV, G>(A, ldesc, 0, wave, l16, src_base);
+    solo_load<K, WV, G>(A, ldesc, lclose, 0, wave, l16, src_base);
     for (int c = 0; c < nreal; c += 2) {
-        solo_load<K, WV, G>(B, ldesc, c + 1, wave, l16, src_base);
-        solo_store<K, G>(A, lclose, lcstep, ts, k, c, rows, l16, dst_base);
+        solo_load<K, WV, G>(B, ldesc, lclose, c + 1, wave, l16, src_base);
+        solo_store<K, WV, G>(A, lclose, lcstep, ts, k, c, rows, l16, dst_base);
         if (c + 1 >= nreal) break;
-        solo_load<K, WV, G>(A, ldesc, c + 2, wave, l16, src_base);
-        solo_store<K, G>(B, lclose, lcstep, ts, k, c + 1, rows, l16, dst_base);
+        solo_load<K, WV, G>(A, ldesc, lclose, c + 2, wave, l16, src_base);
+        solo_store<K, WV, G>(B, lclose, lcstep, ts, k, c + 1, rows, l16, dst_base);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this rail's last steps: delivered
     __syncthreads();

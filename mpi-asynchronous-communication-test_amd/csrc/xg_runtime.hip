@@ -570,7 +570,7 @@ static bool engine_step(const xg_ctx *c, const StepR &st)
 static_assert(xgk::kSoloWaves == XG_SOLO_WAVES && xgk::kSoloMaxRails == XG_SOLO_MAX_RAILS &&
                   xgk::kSoloPiece == XG_SOLO_PIECE && xgk::kSoloK == XG_SOLO_K &&
                   xgk::kSoloMaxSteps == XG_SOLO_MAX_STEPS && xgk::kSoloMaxPieces == XG_SOLO_MAX_PIECES &&
-                  xgk::kSoloOffMax == XG_SOLO_OFF_MAX,
+                  xgk::kSoloOffMax == XG_SOLO_OFF_MAX && xgk::kSoloWideOffMax == XG_SOLO_WIDE_OFF_MAX,
               "solo engine constants: kernels.h and xg_sched.h disagree");
 
 // Solo or grid engine for a hazard-free segment of n steps (`busy` of them move
@@ -663,7 +663,7 @@ static std::vector<std::pair<int, int>> solo_split(const xg_plan *p, const SegCa
     std::vector<std::pair<int, int>> out;
     const int64_t rows_cap = xgk::kSoloMaxPieces - 3 * xgk::kSoloK * c->solo_waves;   // padding headroom
     const int64_t pieces_cap = (int64_t)c->solo_rails * rows_cap;
-    const uint64_t window = (uint64_t)xgk::kSoloOffMax * (uint64_t)k.gran;
+    const uint64_t window = (c->solo_waves == 1 ? xgk::kSoloWideOffMax : xgk::kSoloOffMax) * (uint64_t)k.gran;
     int a = k.s0;
     int64_t bytes = 0, np = 0;
     uintptr_t slo = UINTPTR_MAX, shi = 0, dlo = UINTPTR_MAX, dhi = 0;
@@ -697,6 +697,36 @@ static std::vector<std::pair<int, int>> solo_split(const xg_plan *p, const SegCa
     }
     out.push_back({a, k.s1});
     return out;
+}
+
+// Grid engine vs the same steps as chained copy launches, for a run larger than the
+// Infinity Cache (bytes > solo_max: every round of units pays HBM latency and address
+// translation of fresh pages).  Per step, the grid's workgroups take ceil(units / W)
+// dependent load -> store rounds of ~2 us each behind a ~0.9 us barrier; a chained
+// launch costs a ~2.3 us boundary and moves the step at the copy kernel's rate.  Measured
+// (profiles/r02/theta/): P16384 A256 d2048 m1 -c 8 (2048 steps of 2048 two-KiB
+// transfers) grid 30.0 ms vs chains 7.0 ms; -c 1 (16384 steps of 256) 60.6 vs 47.3 ms.
+static bool grid_pays(const xg_plan *p, const SegCand &k)
+{
+    const xg_ctx *c = p->ctx;
+    if (k.bytes <= c->solo_max) return true;
+    const int b = k.maxstep <= (1 << 20) ? 1 : (k.maxstep <= (4 << 20) ? 4 : 16);
+    const int64_t unit = (int64_t)b * xgk::kThreads * 16;
+    std::vector<int64_t> units(k.n, 0);
+    int64_t maxu = 0;
+    for (int t = 0; t < k.n; ++t) {
+        for (const xgk::DCopy &x : k.xfer[t]) units[t] += (x.len + unit - 1) / unit;
+        maxu = std::max(maxu, units[t]);
+    }
+    const int64_t W = std::max<int64_t>(1, std::min<int64_t>(maxu, c->engine_wmax));
+    double grid = 0, chain = 0;
+    for (int t = 0; t < k.n; ++t) {
+        const StepR &st = p->steps[k.s0 + t];
+        const double traffic = 2.0 * (double)(st.local_bytes + st.pack_bytes);
+        grid += 0.9e-6 + std::max((double)((units[t] + W - 1) / W) * 2e-6, traffic / 5e12);
+        chain += 2.3e-6 + traffic / 5.5e12;
+    }
+    return grid < chain;
 }
 
 // Commit a candidate as an engine segment (solo tables or grid units) to the plan.
@@ -802,6 +832,10 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         }
         if (!solo && busy < 2) {      // one busy step: an engine launch only if it runs solo
             s = run_end;
+            continue;
+        }
+        if (!solo && !grid_pays(p, k)) {   // streaming-size run of many small transfers per step
+            s = e;
             continue;
         }
         if ((rc = commit_seg(p, k, solo, ep, sb))) return rc;

@@ -14,7 +14,12 @@ PIECE, K, MAXP = 1024, 8, 4608
 LEN_BITS = {16: 7, 4: 9, 1: 11}      # kernels.h SoloFmt
 
 
-def decode(d, G=16):
+def decode(d, G=16, row_word=None):
+    """(src, dst, len in granules, before); row_word given: the WIDE form of one-wave rails
+    (32-bit offsets in the descriptor, the length in the row's barrier word, every barrier
+    of the row before its one piece)"""
+    if row_word is not None:
+        return d & 0xFFFFFFFF, d >> 32, (row_word >> 8) & 0xFFF, row_word & 0xFF
     L = LEN_BITS[G]
     return d & 0xFFFFFF, (d >> 24) & 0xFFFFFF, (d >> 48) & ((1 << L) - 1), d >> (48 + L)
 
@@ -38,7 +43,7 @@ def interpret(steps, rails_max, sbase, dbase, xg, WAVES=16, G=16):
     left = {key: list(v) for key, v in owner.items()}
     per_rail = []
     for r in range(R):
-        nb = sum(close[r])
+        nb = sum((x & 0xFF) if WAVES == 1 else x for x in close[r])
         cs = csteps[r]
         assert all(c >= 0 for c in cs[:nb]) and all(c == -1 for c in cs[nb:]), cs
         assert all(a < b for a, b in zip(cs[:nb], cs[1:nb])), cs       # closed steps increase
@@ -47,11 +52,11 @@ def interpret(steps, rails_max, sbase, dbase, xg, WAVES=16, G=16):
         real = 0
         rail_steps = []
         for row in range(nr):
-            nrow = close[r][row]
+            nrow = close[r][row] & 0xFF if WAVES == 1 else close[r][row]
             assert nrow <= WAVES
             prev_bf = 0
             for w in range(WAVES):
-                so, do, l16, bf = decode(descs[r][row * WAVES + w], G)
+                so, do, l16, bf = decode(descs[r][row * WAVES + w], G, close[r][row] if WAVES == 1 else None)
                 assert bf <= nrow and bf >= prev_bf
                 prev_bf = bf
                 if l16 == 0:
@@ -174,8 +179,12 @@ def test_rejects(xg):
     assert rc == 0
     rc, _s, *_ = xg.solo_tables([[(sb + 3, db + 1, 1001)]], 8, sb, db, waves=1, granule=1)
     assert rc == 0
-    rc, _s, *_ = xg.solo_tables([[(sb + (1 << 24), db, 64)]], 8, sb, db, waves=1, granule=1)   # 16 MiB window
+    rc, _s, *_ = xg.solo_tables([[(sb + (1 << 24), db, 64)]], 8, sb, db, waves=1, granule=1)   # wide: 4 GiB window
+    assert rc == 0
+    rc, _s, *_ = xg.solo_tables([[(sb + (1 << 32), db, 64)]], 8, sb, db, waves=1, granule=1)
     assert rc == 3
+    rc, _s, *_ = xg.solo_tables([[(sb + (1 << 28), db, 64)]], 8, sb, db, waves=1)             # wide: 64 GiB window
+    assert rc == 0
     rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 8, sb, db, waves=16, granule=4)   # fine granules: one-wave rails
     assert rc == 3
     rc, _s, *_ = xg.solo_tables([[(sb, db, 64)]], 8, sb, db, waves=1, granule=8)    # 16, 4 or 1
@@ -206,3 +215,26 @@ def test_reduce_stamps(xg, seed):
         exp = max(max([x for x in stamps[r][s0:t + 1] if x] or [0]) for r in range(R))
         assert got[t] == exp, (t, got[t], exp)
     assert all(a <= b for a, b in zip(got[s0:s1], got[s0 + 1:s1]))
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("G", [16, 4, 1])
+def test_wide_windows_one_wave_rails(xg, seed, G):
+    """one-wave rails address 32-bit granule offsets: transfers spread over GiBs (16384
+    logical ranks on one GPU) fit one table"""
+    rng = random.Random(seed * 7 + G)
+    sbase, dbase = 1 << 40, 1 << 44
+    span = min(1 << 32, (1 << 32) * G) - (1 << 20)          # stay inside the window
+    steps = []
+    for _ in range(rng.randint(2, 40)):
+        st = []
+        for _ in range(rng.randint(1, 4)):
+            ln = G * rng.randint(1, 200 * 16 // G)
+            so = rng.randrange(0, span - ln, G)
+            do = rng.randrange(0, span - ln, G)
+            st.append((sbase + so, dbase + do, ln))
+        steps.append(st)
+    srcs = [x[0] for st in steps for x in st]
+    dsts = [x[1] for st in steps for x in st]
+    assert max(srcs) - min(srcs) > (1 << 28) or G == 1     # past the packed form's window
+    interpret(steps, rng.choice([1, 16, 512]), min(srcs), min(dsts), xg, WAVES=1, G=G)
