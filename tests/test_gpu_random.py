@@ -74,8 +74,28 @@ def test_random_config_one_gpu(xg, ctx, cfg):
             assert all(0 <= x <= y for x, y in zip(done, done[1:])) and (not done or done[-1] <= wall + 1e-4)
         chk, bad, first = run.verify()
         _check(xg, s, rl, cfg, list(zip(run.slots, chk, bad, first)), 1)
+        if cfg[0] in (15, 16):
+            _check_tam_scratch(xg, s, rl, cfg, run)
     finally:
         run.close()
+
+
+def _check_tam_scratch(xg, s, rl, cfg, run):
+    """TAM: the aggregation buffers (aggregate_buf | send_buf2 | recv_buf per rank in SCRATCH)
+    hold what the oracle's MPI execution leaves in them"""
+    import numpy as np
+    import xg_oracle as O
+    m, P, A, d, c, k, t, pn, b, it = cfg
+    bufs = {}
+    O.execute(m, P, A, d, rl, O.programs(m, P, A, d, c, rl, k, pn, it=it), it, mode=1, buffers=bufs)
+    for r in range(P):
+        base, off = s.scratch_offset(1, r), 0
+        for name in ("AGG", "SBUF2", "RBUF"):
+            ref = bufs[r].get(name, np.zeros(0, np.uint8))
+            if ref.size:
+                got = np.frombuffer(run.read(xg.BUF_SCRATCH, base + off, ref.size), dtype=np.uint8)
+                assert (got == ref).all(), (cfg, r, name)
+            off += (ref.size + 255) // 256 * 256
 
 
 @pytest.fixture(scope="module")
