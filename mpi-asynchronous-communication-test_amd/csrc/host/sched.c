@@ -22,7 +22,7 @@
 #include <string.h>
 
 enum { OP_BARRIER, OP_SEND, OP_RECV, OP_WAIT, OP_A2AW, OP_COPY, OP_TMARK,
-       OP_REP, OP_MARK, OP_DELTA, OP_ACC, OP_COPYT, OP_ZERO };
+       OP_REP, OP_MARK, OP_DELTA, OP_ACC, OP_COPYT, OP_ZERO, OP_SYNC };
 /* timer fields in xg_timer order */
 enum { F_POST = 0, F_SEND = 1, F_RECV = 2, F_BARRIER = 3, F_TOTAL = 4, NF = 5 };
 /* logical buffers of a rank: send segments, receive slots, TAM's aggregate_buf /
@@ -591,10 +591,28 @@ static void m12_half_sync2(ctx_t *x)
 }
 
 /* many_to_all_pairwise :421-508 / all_to_many_pairwise :510-597 */
+/* "this rank has completed step k": its later posts move no earlier than k + 1, and its
+ * clock reaches step k's completion (the pairwise fast form's stand-in for the 0-byte
+ * MPI_Sendrecv rounds it leaves out) */
+static void sync_step(prog_t *p, int k) { op_t *o = push(p); o->kind = OP_SYNC; o->idx = k; }
+
+/* Large P: every rank makes P blocking MPI_Sendrecv calls per repetition, most of them
+ * 0 bytes -- P^2 calls to materialise (268 M at P = 16384).  They keep every rank in
+ * lockstep, so round i of repetition m is step m*P + i for every message; the fast form
+ * posts only the directions that carry bytes, each behind a sync to the round before, and
+ * ends with a sync to the last round (tests/test_host_sched.py checks it against the full
+ * form: same messages, steps and rank timers).  XG_PAIRWISE_FAST=0/1 forces either form. */
+static int pairwise_fast(int P)
+{
+    const char *e = getenv("XG_PAIRWISE_FAST");
+    return e ? atoi(e) != 0 : P > 1024;
+}
+
 static void m_pairwise(ctx_t *x, int dir)
 {
     prog_t *p = x->p;
     int P = x->P, m, i, pof2, src, dst;
+    const int fast = pairwise_fast(P);
     int64_t *sc = xmalloc(sizeof(int64_t) * 4 * P), *sd = sc + P, *rc = sc + 2 * P, *rd = sc + 3 * P;
     translate(x, dir, sc, sd, rc, rd);
     i = 1;
@@ -604,10 +622,24 @@ static void m_pairwise(ctx_t *x, int dir)
         for (i = 0; i < P; ++i) {
             if (pof2) src = dst = x->rank ^ i;
             else { src = (x->rank - i + P) % P; dst = (x->rank + i) % P; }
-            sendrecv(p, dst, sc[dst], sc[dst] ? (int)(sd[dst] / x->d) : -1,
-                     src, rc[src], rc[src] ? (int)(rd[src] / x->d) : -1);
+            if (!fast) {
+                sendrecv(p, dst, sc[dst], sc[dst] ? (int)(sd[dst] / x->d) : -1,
+                         src, rc[src], rc[src] ? (int)(rd[src] / x->d) : -1);
+                continue;
+            }
+            if (!sc[dst] && !rc[src]) continue;
+            const int k = m * P + i;
+            if (k > 0) sync_step(p, k - 1);
+            if (sc[dst] && rc[src]) {
+                sendrecv(p, dst, sc[dst], (int)(sd[dst] / x->d), src, rc[src], (int)(rd[src] / x->d));
+            } else if (sc[dst]) {
+                wait1(p, post_send(p, dst, sc[dst], (int)(sd[dst] / x->d), 1));
+            } else {
+                wait1(p, post_recv(p, src, rc[src], (int)(rd[src] / x->d)));
+            }
         }
     }
+    if (fast && x->ntimes > 0) sync_step(p, x->ntimes * P - 1);
     free(sc);
 }
 
@@ -1276,6 +1308,9 @@ static int compile_steps(xg_sched *s, char *err, size_t errlen)
                     if (arr_epoch[b] > epoch[r]) epoch[r] = arr_epoch[b];
                 } else if (o->kind == OP_SEND || o->kind == OP_RECV) {
                     pe[r][o->post] = epoch[r];
+                } else if (o->kind == OP_SYNC) {
+                    if (o->idx > epoch[r]) epoch[r] = o->idx;
+                    if (o->idx > maxstep) maxstep = o->idx;
                 } else if (o->kind == OP_COPY) {
                     /* after everything the rank completed, after the last copy that wrote its
                      * source, after the last copy that read its destination; what the rank
@@ -1587,6 +1622,9 @@ static int rank_timers(xg_sched *s, int ngpus, int rank, const double *step_done
             if (e >= 0 && step_done[e] > clock) clock = step_done[e];
             break;
         }
+        case OP_SYNC:
+            if (o->idx >= 0 && o->idx < s->nsteps && step_done[o->idx] > clock) clock = step_done[o->idx];
+            break;
         case OP_TMARK:
             if (o->sign > 0) {
                 if (depth[o->field]++ == 0) { open_c[o->field] = clock; open_p[o->field] = postacc; }

@@ -119,3 +119,42 @@ def test_cli_usage_matches_reference(pkg):
     assert out.returncode == 0
     ref = open(os.path.join(GOLDEN, "usage.txt")).read().replace("{argv0}", exe)
     assert out.stderr == ref
+
+
+def _pairwise(xg, method, P, A, d, k, fast, pn=1, t=1):
+    import os
+    old = os.environ.get("XG_PAIRWISE_FAST")
+    os.environ["XG_PAIRWISE_FAST"] = "1" if fast else "0"
+    try:
+        return xg.Schedule(method, P, A, d, 8, xg.aggregator_list(P, A, pn, t), ntimes=k)
+    finally:
+        if old is None:
+            del os.environ["XG_PAIRWISE_FAST"]
+        else:
+            os.environ["XG_PAIRWISE_FAST"] = old
+
+
+@pytest.mark.parametrize("method", [9, 10])
+@pytest.mark.parametrize("P,A,d,k", [(64, 8, 4096, 1), (64, 64, 100, 2), (100, 7, 70000, 2), (37, 5, 1000, 3),
+                                     (128, 3, 65424, 1), (48, 48, 8, 1)])
+def test_pairwise_fast_form_equals_full_form(xg, method, P, A, d, k):
+    """Large-P pairwise leaves out the 0-byte MPI_Sendrecv rounds (P^2 of them) and syncs each
+    rank to the round before its next exchange instead: the same messages in the same steps,
+    the same step count and the same rank timers as the full form, for power-of-two (XOR)
+    and shift rounds, both directions, eager and rendezvous sizes, -k repetitions."""
+    import random
+    full = _pairwise(xg, method, P, A, d, k, fast=False)
+    fast = _pairwise(xg, method, P, A, d, k, fast=True)
+    assert fast.nsteps == full.nsteps == k * P
+    key = lambda m: (m[0], m[2], m[1], m[3], m[5])
+    want = sorted((m for m in full.messages() if m[4] > 0), key=key)
+    got = sorted(fast.messages(), key=key)
+    assert [m[:6] for m in got] == [m[:6] for m in want]
+    rng = random.Random(P * 31 + k)
+    done, t = [], 0.0
+    for _ in range(full.nsteps):
+        t += rng.uniform(0.0, 2e-6)
+        done.append(t)
+    for r in range(P):
+        a, b = full.rank_timer(r, done).as_tuple(), fast.rank_timer(r, done).as_tuple()
+        assert a == b, (r, a, b)
