@@ -61,6 +61,7 @@ struct xg_ctx {
     int solo_rails;            // solo segments deal their pieces over up to this many rails
     int solo_waves;            // waves per rail: 16 (a workgroup) or 1
     int solo_min_steps;        // a whole plan of fewer steps stays a copy launch
+    int64_t launch_max;        // copy launches above this many bytes go as back-to-back launches of ~this size
     int solo_relay;            // armed solo: rail 0 alone polls the doorbell and relays the ring
     int step_chain;            // 1: time runs of one-launch local steps by in-kernel stamps (xg_plan_run)
     int piece_order;           // local pieces of a launch: 0 message order, 1 by destination, 2 by source
@@ -162,6 +163,7 @@ struct xg_plan {
     // first step), 0 elsewhere.
     std::vector<int> chain_end;
     unsigned long long *d_cstamp;  // nsteps wall-clock stamps of chained steps
+    std::vector<int64_t> plen;     // prefix sums of the piece lengths (npieces + 1), host side
 };
 
 // The copy kernel variant of a launch moving `bytes` (launch_copy).  Variant 0 picks
@@ -289,6 +291,8 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->solo_rails = c->solo_waves == 1 ? 512 : 16;     // 512 one-wave rails: 2 per CU by LDS
     env = getenv("XG_SOLO_RAILS");
     if (env && atoi(env) > 0) c->solo_rails = std::min(atoi(env), xgk::kSoloMaxRails);
+    env = getenv("XG_COPY_LAUNCH_MAX");      // bytes; 0 = one launch however large
+    c->launch_max = env ? atoll(env) : (int64_t)512 << 20;
     env = getenv("XG_SOLO_MIN_STEPS");       // plans of fewer steps never run as an armed solo launch
     c->solo_min_steps = env ? atoi(env) : 1;  // profiles/r02/one_step/: armed beats the event-timed launch
     env = getenv("XG_PIECE_ORDER");          // profiles/r02/piece_order/: by destination is fastest
@@ -1095,6 +1099,8 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         }
     }
     p->npieces = (int)pieces.size();
+    p->plen.assign(pieces.size() + 1, 0);
+    for (size_t i = 0; i < pieces.size(); ++i) p->plen[i + 1] = p->plen[i] + pieces[i].len;
     if (p->npieces) {
         HIPCHK(hipMalloc(&p->d_pieces, sizeof(xgk::DCopy) * pieces.size()));
         HIPCHK(hipMemcpy(p->d_pieces, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
@@ -1218,12 +1224,38 @@ extern "C" int xg_plan_displs(const xg_plan *p, int64_t *out, int n)
 // one keeps the default policy, which re-runs serve from the cache
 // (profiles/r02/copy_nt_sizes.txt).  1..6 force one form (A/B, tests).
 // start: stamp the launch's start there (variants 1 and 6 only; see copy_kernel_g)
+static int launch_one(xg_plan *p, int b, int n, int v, hipStream_t st, unsigned long long *start);
+
 static int launch_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t st, unsigned long long *start = nullptr,
                        bool reread = false)
 {
-    const xgk::DCopy *pc = p->d_pieces + b;
     const int v = copy_variant(p, bytes, reread);
     if (start && v != 1 && v != 6) return XG_EARG;
+    // a launch of more than launch_max bytes goes as back-to-back launches of about
+    // launch_max bytes each (its pieces are independent: the same step, a few more kernel
+    // boundaries).  P256 A32 -d 4 MiB m1 / m2 (one 32 GiB step, 1 M pieces): 12.6 -> 11.0 ms
+    // at 512 MiB per launch, 11.5 at 128 MiB; cutting by piece count instead hurt steps of
+    // small pieces (profiles/r02/launch_split/)
+    const int64_t cap = p->ctx->launch_max;
+    if (cap > 0 && bytes > cap + cap / 2 && !p->plen.empty()) {
+        const int64_t *pre = p->plen.data();        // prefix sums of the piece lengths
+        int rc, o = b;
+        while (o < b + n) {
+            // the first piece past cap bytes from o
+            const int64_t want = pre[o] + cap;
+            int e = (int)(std::lower_bound(pre + o + 1, pre + b + n + 1, want) - pre);
+            if (b + n - e < 16 || pre[b + n] - pre[e] < cap / 2) e = b + n;   // no runt launch at the end
+            if ((rc = launch_one(p, o, e - o, v, st, o == b ? start : nullptr))) return rc;
+            o = e;
+        }
+        return XG_OK;
+    }
+    return launch_one(p, b, n, v, st, start);
+}
+
+static int launch_one(xg_plan *p, int b, int n, int v, hipStream_t st, unsigned long long *start)
+{
+    const xgk::DCopy *pc = p->d_pieces + b;
     switch (v) {
     case 2: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxPlain>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
     case 3: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxSC1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
