@@ -177,6 +177,34 @@ def cpu_baseline_port(a, methods, note=""):
                       % (",".join(map(str, methods)), note)}
 
 
+# ---------------------------------------------------------------- xGMI latency / bandwidth floor (N > 1)
+SWEEP_SIZES = (4096, 65536, 1 << 20, 16 << 20)
+
+
+def p2p_sweep(ctx, world):
+    """The pt2pt_test analogue (mpi_sendrecv_test.c:15-74) as RCCL p2p over xGMI, a few
+    seconds at most: per message size, one direction 1 -> 0 (xg_p2p_bench mode 2: latency
+    of one send/recv pair, what a latency-bound step pays per cross-GPU message) and all
+    pairs at once (mode 0: every GPU sends `bytes` to each of its N-1 peers).  Every rank
+    runs every case (the calls are collective); the figures are MAX time / MIN rate over
+    the GPUs taking part."""
+    out = []
+    for nbytes in SWEEP_SIZES:
+        reps = 50 if nbytes <= 65536 else (20 if nbytes <= 1 << 20 else 5)
+        for mode, name in ((2, "one_way_1_to_0"), (0, "all_pairs")):
+            gbps, sec = ctx.p2p_bench(nbytes, mode=mode, reps=reps)
+            part = mode == 0 or ctx.rank < 2          # mode 2 moves bytes between GPUs 1 and 0 only
+            t_max, neg_rate = ctx.allreduce_max([sec if part else 0.0, -gbps if part else -1e30])
+            row = {"mode": name, "bytes": nbytes, "reps": reps, "us_per_rep": round(t_max * 1e6, 2)}
+            if mode == 2:
+                row["GBps"] = round(-neg_rate, 2)
+            else:
+                row["GBps_per_gpu_egress_min"] = round(-neg_rate, 2)
+                row["GBps_aggregate"] = round(-neg_rate * world, 2)
+            out.append(row)
+    return out
+
+
 # ---------------------------------------------------------------- N-GPU job without a launcher
 def spawn_ranks(a):
     """Parent of an N-GPU job (no WORLD_SIZE in the environment): never touches the GPU.
@@ -469,7 +497,8 @@ def main():
                 "frac": round(achieved / (ceil_min * world), 4) if ceil_min > 0 else None,
                 "cross_gpu_bytes_per_step": int(cross_step),
                 "peak_source": "measured: RCCL all-pairs send/recv, %d B per GPU pair, slowest GPU egress x %d "
-                               "(xg_p2p_bench mode 0)" % (per_pair, world)}
+                               "(xg_p2p_bench mode 0)" % (per_pair, world),
+                "sweep": p2p_sweep(ctx, world)}
     if rank != 0:
         ctx.close()
         return 0

@@ -161,9 +161,9 @@ int xg_p2p_bench(xg_ctx *ctx, int64_t bytes, int mode, int reps, double *gbps, d
 /* Tuning: bytes per copy workgroup (default 32768) and copy kernel variant: 0 (default)
  * = copy_kernel_g<4> with non-temporal loads/stores for launches moving >= XG_COPY_NT_MIN
  * bytes (default 128 MiB: source + destination past the 256 MiB Infinity Cache) and plain
- * ones below; 1 = always plain, 6 = always non-temporal; 2/3/4 = copy_kernel_b<4>, buffer
- * stores plain / sc1 write-through / nt; 5 = copy_kernel_b<8> nt.  variant < 0 keeps the
- * current one; XG_COPY_VARIANT / XG_COPY_CHUNK at xg_init.  Applies to plans loaded afterwards. */
+ * ones below; 1 = always plain, 6 = always non-temporal (XG_EARG for any other).  variant < 0
+ * keeps the current one; XG_COPY_VARIANT / XG_COPY_CHUNK at xg_init.  Applies to plans loaded
+ * afterwards. */
 int xg_set_copy_params(xg_ctx *ctx, int64_t chunk_bytes, int variant);
 
 /* ------------------------------------------------------------------ method operators

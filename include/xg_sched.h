@@ -103,7 +103,10 @@ int xg_sched_procs(const xg_sched *s);
 
 /* Canonical MPI call trace of one logical rank (same token format as the
  * PMPI capture in tests/golden/); returns the length written (truncated to
- * buflen-1) or the needed length if buf is NULL. */
+ * buflen-1) or the needed length if buf is NULL.  Pairwise m9/m10 above P = 1024
+ * (or with XG_PAIRWISE_FAST=1) are planned in a fast form that leaves out the
+ * 0-byte MPI_Sendrecv rounds: their trace is then NOT the reference's call trace
+ * (same byte-carrying posts, other completions; tests/test_host_sched.py). */
 size_t xg_sched_trace(const xg_sched *s, int rank, char *buf, size_t buflen);
 
 /* Per-rank timer from device step timestamps (ranks block-mapped on ngpus):
@@ -188,6 +191,39 @@ int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf);
  * is < pack_max_seg (0 = never pack); otherwise one RCCL op per segment. */
 xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg);
 void xg_devplan_free(xg_devplan *p);
+
+/* ---------------------------------------------------------------- RCCL calls (calls.c)
+ * The calls GPU dp->gpu posts in step `step`, in issue order: its send/recv calls
+ * (one ncclGroupStart/End around them), then XG_CALL_BARRIER (one ncclAllReduce)
+ * when the step ends in an in-loop MPI_Barrier.  The runtime posts exactly this
+ * list (replaces the Issend/Irecv/Sendrecv/Alltoallw posts, mpi_test.c:1776,1790,
+ * :551,558, :627,912).  Returns the count (out may be NULL), -1 for a bad step. */
+enum { XG_CALL_SEND = 1, XG_CALL_RECV = 2, XG_CALL_BARRIER = 3 };
+typedef struct {
+    int32_t kind, peer, buf, pad;     /* peer: GPU; buf: region (XG_BUF_*) */
+    int64_t off, len;
+} xg_call;
+int xg_devplan_step_calls(const xg_devplan *dp, int step, xg_call *out);
+
+/* RCCL's pairing of the calls of a G-GPU job: per ordered GPU pair (src, dst), the
+ * k-th send of src to dst with the k-th receive of dst from src, in issue order
+ * over the WHOLE run (RCCL's per-peer FIFO knows no steps).  calls[g] / step_begin[g]
+ * (nsteps + 1 entries): GPU g's calls and where each step's start.  Accepted only if
+ * every pair falls in one step with one length and every GPU ends the same steps
+ * with a barrier (each its step's last call) -- then no group can wait for one a
+ * peer posts later.  Returns the number of pairs, written step-major (inside a step
+ * by src, dst, k) to out when max_pairs suffices; -1 and a reason in err otherwise. */
+typedef struct {
+    int32_t step, src, dst;
+    int32_t send_call, recv_call;     /* indices into calls[src] / calls[dst] */
+    int32_t pad;
+    int64_t len;
+} xg_call_pair;
+int64_t xg_calls_match(int ngpus, int nsteps, const xg_call *const *calls, const int32_t *const *step_begin,
+                       xg_call_pair *out, int64_t max_pairs, char *err, size_t errlen);
+/* The same over the G device plans of one job (plans[g]: GPU g's, same schedule). */
+int64_t xg_devplans_match(const xg_devplan *const *plans, int ngpus, xg_call_pair *out, int64_t max_pairs,
+                          char *err, size_t errlen);
 
 /* Step engine ordering (xg.h xg_plan_engine; kernels.h step_engine_kernel).  The
  * transfers of step s are xfer[step_begin[s] .. step_begin[s+1]) (device addresses

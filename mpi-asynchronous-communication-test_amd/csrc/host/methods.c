@@ -25,6 +25,22 @@ void xg_run_opts_default(xg_run_opts *o)
 
 #define TRY(x) do { rc = (x); if (rc) goto out; } while (0)
 
+/* A G-GPU job's RCCL calls pair step by step as RCCL pairs them (xg_devplans_match over
+ * every GPU's plan, calls.c); otherwise err says which call would not. */
+static int pairing_ok(const xg_sched *s, int G, int64_t pack_max_seg, char *err, size_t errlen)
+{
+    xg_devplan **plans = (xg_devplan **)calloc(G, sizeof *plans);
+    int g, ok = 0;
+    char why[400];
+    if (!plans) return 0;
+    for (g = 0; g < G; ++g) plans[g] = xg_devplan_build(s, G, g, pack_max_seg);
+    if (xg_devplans_match((const xg_devplan *const *)plans, G, NULL, 0, why, sizeof why) >= 0) ok = 1;
+    else snprintf(err, errlen, "the GPUs' RCCL calls do not pair: %s", why);
+    for (g = 0; g < G; ++g) xg_devplan_free(plans[g]);
+    free(plans);
+    return ok;
+}
+
 int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list,
                   int comm_size, xg_timer *timers, int iter, int ntimes, const xg_run_opts *opts,
                   int64_t *bad_slots, char *err, size_t errlen)
@@ -47,6 +63,12 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
     s = xg_sched_build_iter(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, opts->proc_node,
                             opts->barrier_type, opts->eager_limit, iter, err, errlen);
     if (!s) return XG_ESCHED;
+    if (G > 1 && !pairing_ok(s, G, opts->pack_max_seg, err, errlen)) {
+        /* every GPU derives every GPU's calls from the same schedule, so every GPU refuses
+         * alike -- before any of them posts a call that could wait forever */
+        xg_sched_free(s);
+        return XG_EARG;
+    }
     dp = xg_devplan_build(s, G, g, opts->pack_max_seg);
     TRY(xg_regions_alloc(ctx, dp->region_bytes, &reg));
     nruns = xg_fill_runs(s, G, g, NULL);

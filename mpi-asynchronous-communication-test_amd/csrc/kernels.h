@@ -199,30 +199,6 @@ __device__ __forceinline__ void bstore16(brsrc r, int off, u32x4 v)
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
 }
 
-// Pipelined piece copy through buffer resources (n: bytes, a multiple of 16,
-// < 2^31): every lane keeps U 16-B loads of the next block in flight while it
-// stores the current block.  The trip count is wave-uniform; out-of-range
-// lanes of the last block load 0 and their stores are dropped by the range check.
-template <int U, int AUX>
-__device__ __forceinline__ void pipelined_copy16_b(const uint8_t *src, uint8_t *dst, int n)
-{
-    const brsrc rs = make_rsrc(src, n), rd = make_rsrc(dst, n);
-    constexpr int blk = U * kThreads * 16;
-    const int lane = (int)threadIdx.x * 16;
-    u32x4 cur[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) cur[u] = bload16(rs, lane + u * kThreads * 16);
-    for (int base = 0; base < n; base += blk) {
-        u32x4 nxt[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) nxt[u] = bload16(rs, base + blk + lane + u * kThreads * 16);
-#pragma unroll
-        for (int u = 0; u < U; ++u) bstore16<AUX>(rd, base + lane + u * kThreads * 16, cur[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-    }
-}
-
 // LDS-staged realignment for a piece whose source and destination disagree mod
 // 16 (any -d that is not a multiple of 16: segment offsets k*d land on every
 // phase).  The destination gets whole aligned 16-B stores: the head (< 16 B) and
@@ -281,9 +257,8 @@ __device__ void realign_copy(const uint8_t *s, uint8_t *t, int64_t n, uint32_t (
     }
 }
 
-// One workgroup per DCopy piece (<= the context's chunk bytes).  Variants:
-//   copy_kernel_g<U, NT>   global loads/stores, U-deep software pipeline; NT: non-temporal
-//   copy_kernel_b<U, AUX>  the same through buffer resources, store policy AUX
+// One workgroup per DCopy piece (<= the context's chunk bytes): copy_kernel_g<U, NT>,
+// global loads/stores, U-deep software pipeline; NT: non-temporal loads and stores.
 // Pieces whose pointers or length are not 16-B aligned take realign_copy.
 // start != nullptr: workgroup 0 stamps the launch's start (wall clock) there -- in a
 // chain of back-to-back step launches that is the time the previous step completed
@@ -297,17 +272,6 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restric
     const DCopy c = pieces[blockIdx.x];
     if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
         pipelined_copy16<U, NT>((g_cu4 *)c.src, (g_u4 *)c.dst, c.len >> 4);
-    else
-        realign_copy(c.src, c.dst, c.len, lds);
-}
-
-template <int U, int AUX>
-__global__ __launch_bounds__(kThreads) void copy_kernel_b(const DCopy *__restrict__ pieces)
-{
-    __shared__ uint32_t lds[2][kTileWords];
-    const DCopy c = pieces[blockIdx.x];
-    if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
-        pipelined_copy16_b<U, AUX>(c.src, c.dst, (int)c.len);
     else
         realign_copy(c.src, c.dst, c.len, lds);
 }

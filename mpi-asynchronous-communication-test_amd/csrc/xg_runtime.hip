@@ -45,6 +45,55 @@
         }                                                                                          \
     } while (0)
 
+// Device scratch freed on every return path (error returns of HIPCHK included).
+struct DevMem {
+    void *p = nullptr;
+    DevMem() = default;
+    DevMem(const DevMem &) = delete;
+    DevMem &operator=(const DevMem &) = delete;
+    ~DevMem()
+    {
+        if (p) (void)hipFree(p);
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+struct EventPair {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~EventPair()
+    {
+        for (hipEvent_t x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+};
+
+// One RCCL group whose calls come from `post`, a callable returning ncclResult_t for
+// call i (i = 0..n-1): the group is closed (ncclGroupEnd) on every path, so an error
+// never leaves this rank inside an open group.  Returns XG_OK or XG_ERCCL.
+template <class F>
+static int rccl_group(int n, F post, const char *what)
+{
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) {
+        fprintf(stderr, "xg: RCCL error %s: ncclGroupStart (%s)\n", ncclGetErrorString(r), what);
+        return XG_ERCCL;
+    }
+    int rc = XG_OK;
+    for (int i = 0; i < n && rc == XG_OK; ++i) {
+        r = post(i);
+        if (r != ncclSuccess) {
+            fprintf(stderr, "xg: RCCL error %s: call %d of %d in a group (%s)\n", ncclGetErrorString(r), i, n, what);
+            rc = XG_ERCCL;
+        }
+    }
+    r = ncclGroupEnd();
+    if (r != ncclSuccess) {
+        fprintf(stderr, "xg: RCCL error %s: ncclGroupEnd (%s)\n", ncclGetErrorString(r), what);
+        rc = XG_ERCCL;
+    }
+    return rc;
+}
+
 struct xg_ctx {
     int rank, nranks, device;
     bool virt;              // xg_init_virtual: one of nranks GPUs emulated on one device, no RCCL
@@ -58,6 +107,7 @@ struct xg_ctx {
     int engine_drain;          // 1: always drain before each barrier arrival (XG_ENGINE_DRAIN=1)
     int solo;                  // 0: never use the solo engine
     int64_t solo_max;          // solo segments move <= this many bytes per run
+    int64_t grid_cache_max;    // grid_pays: runs of <= this many bytes stay cache-resident (the 256 MiB MALL)
     int solo_rails;            // solo segments deal their pieces over up to this many rails
     int solo_waves;            // waves per rail: 16 (a workgroup) or 1
     int solo_min_steps;        // a whole plan of fewer steps stays a copy launch
@@ -96,7 +146,9 @@ struct StepR {
     //   fused: this step's packs go in ONE launch with the previous step's unpacks
     //   (deferred there); a pack only fills staging and delivers nothing, so every
     //   message of this step is still delivered after every one of the previous step.
-    int stage_b, stage_n, local_b, local_n, pack_b, pack_n, post_b, post_n, p2p_b, p2p_n, sync_after;
+    // call_b / call_n: the step's RCCL calls in the plan's call list (xg_devplan_step_calls);
+    // p2p_n of them are send/recv (one group), sync_after: the last is the in-loop barrier
+    int stage_b, stage_n, local_b, local_n, pack_b, pack_n, post_b, post_n, call_b, call_n, p2p_n, sync_after;
     int pre_n;                       // local_n + pack_n
     int64_t stage_bytes, local_bytes, pack_bytes, post_bytes;   // bytes copied by each part (read + written once)
     bool split, fused, deferred;
@@ -130,7 +182,8 @@ struct xg_plan {
     xgk::DCopy *d_pieces;
     int npieces;
     std::vector<StepR> steps;
-    std::vector<xg_p2p> p2p;
+    std::vector<xg_call> calls;       // every step's RCCL calls, as xg_devplan_step_calls lists them
+    std::vector<int32_t> call_begin;  // nsteps + 1: where each step's calls start
     std::vector<hipEvent_t> ev;
     std::vector<hipEvent_t> fork, join;   // per split step: main -> side, side -> main
     hipEvent_t ev0;
@@ -250,8 +303,9 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->chunk = 32768; c->variant = 0; c->kt_mode = 0; c->nk = 0; c->kt_bytes = 0;   // profiles/r01_copy_ab.txt
     const char *env = getenv("XG_COPY_CHUNK");
     if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
-    env = getenv("XG_COPY_VARIANT");
-    if (env) c->variant = atoi(env);
+    env = getenv("XG_COPY_VARIANT");          // 0 by size (default), 1 plain, 6 non-temporal
+    if (env && (atoi(env) == 1 || atoi(env) == 6)) c->variant = atoi(env);
+    else if (env && atoi(env) != 0) fprintf(stderr, "xg: XG_COPY_VARIANT=%s ignored (0, 1 or 6)\n", env);
     c->nt_min = 128 << 20;
     env = getenv("XG_COPY_NT_MIN");
     if (env) c->nt_min = atol(env);
@@ -285,6 +339,9 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->solo_max = (int64_t)1 << 30;
     env = getenv("XG_ENGINE_SOLO_MAX");
     if (env) c->solo_max = atol(env);
+    c->grid_cache_max = (int64_t)256 << 20;   // the Infinity Cache, not solo_max (1 GiB since a9cb48e)
+    env = getenv("XG_GRID_CACHE_MAX");
+    if (env) c->grid_cache_max = atol(env);
     env = getenv("XG_SOLO_WAVES");           // waves per rail: 1 (default) or 16
     c->solo_waves = env && atoi(env) == xgk::kSoloWaves ? xgk::kSoloWaves : 1;
     // see DESIGN.md (solo engine): profiles/r02/rails/solo_probe.txt
@@ -301,8 +358,11 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->step_chain = !(env && !strcmp(env, "0"));
     env = getenv("XG_SOLO_RELAY");           // "0": every rail polls the doorbell itself
     c->solo_relay = !(env && !strcmp(env, "0"));
-    env = getenv("XG_ENGINE_ARM");           // "0": launch latency inside the timed region
-    c->engine_arm = !(env && !strcmp(env, "0"));
+    // "1": arm single-segment plans (launched before the timed region, started by the host's
+    // doorbell ring).  Off by default: the reference's total_time brackets its request posts
+    // (mpi_test.c:1444, :1763), so the like-for-like time includes the kernel launch
+    env = getenv("XG_ENGINE_ARM");
+    c->engine_arm = env && !strcmp(env, "1");
     env = getenv("XG_SPLIT_LOCAL");          // "0": local gather + packs in one launch
     c->split_local = !(env && !strcmp(env, "0"));
     env = getenv("XG_FUSE_UNPACK");          // "0": unpacks and the next step's packs apart
@@ -389,12 +449,15 @@ extern "C" int xg_allreduce_max(xg_ctx *c, double *vals, int n)
     if (n < 0) return XG_EARG;
     if (c->nranks == 1 || n == 0 || c->virt) return XG_OK;   // virtual: one process holds every GPU
     double *buf = c->d_red;
-    if (n > 64) HIPCHK(hipMalloc(&buf, sizeof(double) * n));
+    DevMem big;
+    if (n > 64) {
+        HIPCHK(hipMalloc(&big.p, sizeof(double) * n));
+        buf = big.as<double>();
+    }
     HIPCHK(hipMemcpyAsync(buf, vals, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
     NCCLCHK(ncclAllReduce(buf, buf, n, ncclFloat64, ncclMax, c->comm, c->stream));
     HIPCHK(hipMemcpyAsync(vals, buf, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (buf != c->d_red) HIPCHK(hipFree(buf));
     return XG_OK;
 }
 
@@ -420,6 +483,7 @@ extern "C" int xg_device_info(xg_ctx *c, char *name, size_t namelen, int *cus, s
 
 extern "C" int xg_set_copy_params(xg_ctx *c, int64_t chunk, int variant)
 {
+    if (variant > 0 && variant != 1 && variant != 6) return XG_EARG;   // 0 by size, 1 plain, 6 non-temporal
     if (chunk >= 4096) c->chunk = chunk & ~(int64_t)15;
     if (variant >= 0) c->variant = variant;
     return XG_OK;
@@ -508,14 +572,14 @@ extern "C" int xg_fill(xg_regions *r, const xg_segrun *runs, int nruns, int64_t 
     const int64_t chunk = 65536;
     const int64_t cps = (d + chunk - 1) / chunk;
     if ((int64_t)segs.size() * cps > 0x7fffffff) return XG_EARG;
-    xgk::DSeg *dsegs;
-    HIPCHK(hipMalloc(&dsegs, sizeof(xgk::DSeg) * segs.size()));
+    DevMem m_segs;
+    HIPCHK(hipMalloc(&m_segs.p, sizeof(xgk::DSeg) * segs.size()));
+    xgk::DSeg *dsegs = m_segs.as<xgk::DSeg>();
     HIPCHK(hipMemcpyAsync(dsegs, segs.data(), sizeof(xgk::DSeg) * segs.size(), hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(xgk::fill_kernel, dim3((unsigned)(segs.size() * cps)), dim3(xgk::kThreads), 0, c->stream,
                        r->ptr[XG_BUF_SEND], dsegs, (int)cps, d, chunk, iter, mode);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipFree(dsegs));
     return XG_OK;
 }
 
@@ -531,10 +595,11 @@ extern "C" int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_
     }
     const int64_t chunk = 65536;
     const int64_t cps = d > 0 ? (d + chunk - 1) / chunk : 1;
-    xgk::DSlot *dsl;
-    unsigned long long *dout;
-    HIPCHK(hipMalloc(&dsl, sizeof(xgk::DSlot) * nslots));
-    HIPCHK(hipMalloc(&dout, sizeof(unsigned long long) * 3 * nslots));
+    DevMem m_sl, m_out;
+    HIPCHK(hipMalloc(&m_sl.p, sizeof(xgk::DSlot) * nslots));
+    HIPCHK(hipMalloc(&m_out.p, sizeof(unsigned long long) * 3 * nslots));
+    xgk::DSlot *dsl = m_sl.as<xgk::DSlot>();
+    unsigned long long *dout = m_out.as<unsigned long long>();
     HIPCHK(hipMemcpyAsync(dsl, sl.data(), sizeof(xgk::DSlot) * nslots, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemsetAsync(dout, 0, sizeof(unsigned long long) * 2 * nslots, c->stream));
     HIPCHK(hipMemsetAsync(dout + 2 * nslots, 0xff, sizeof(unsigned long long) * nslots, c->stream));
@@ -547,8 +612,6 @@ extern "C" int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_
     std::vector<unsigned long long> h(3 * (size_t)nslots);
     HIPCHK(hipMemcpyAsync(h.data(), dout, sizeof(unsigned long long) * 3 * nslots, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipFree(dsl));
-    HIPCHK(hipFree(dout));
     const uint64_t lenk = 0xD6E8FEB86659FD93ull * (uint64_t)d;
     for (int i = 0; i < nslots; ++i) {
         if (chk) chk[i] = h[i] + lenk;
@@ -707,8 +770,8 @@ static std::vector<std::pair<int, int>> solo_split(const xg_plan *p, const SegCa
 }
 
 // Grid engine vs the same steps as chained copy launches, for a run larger than the
-// Infinity Cache (bytes > solo_max: every round of units pays HBM latency and address
-// translation of fresh pages).  Per step, the grid's workgroups take ceil(units / W)
+// Infinity Cache (bytes > grid_cache_max = 256 MiB, the MALL, XG_GRID_CACHE_MAX: every
+// round of units pays HBM latency and address translation of fresh pages).  Per step, the grid's workgroups take ceil(units / W)
 // dependent load -> store rounds of ~2 us each behind a ~0.9 us barrier; a chained
 // launch costs a ~2.3 us boundary and moves the step at the copy kernel's rate.  Measured
 // (profiles/r02/theta/): P16384 A256 d2048 m1 -c 8 (2048 steps of 2048 two-KiB
@@ -716,7 +779,7 @@ static std::vector<std::pair<int, int>> solo_split(const xg_plan *p, const SegCa
 static bool grid_pays(const xg_plan *p, const SegCand &k)
 {
     const xg_ctx *c = p->ctx;
-    if (k.bytes <= c->solo_max) return true;
+    if (k.bytes <= c->grid_cache_max) return true;
     const int b = k.maxstep <= (1 << 20) ? 1 : (k.maxstep <= (4 << 20) ? 4 : 16);
     const int64_t unit = (int64_t)b * xgk::kThreads * 16;
     std::vector<int64_t> units(k.n, 0);
@@ -804,11 +867,10 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         while (s < e && !p->steps[s].pre_n) ++s;
         while (e > s && !p->steps[e - 1].pre_n) --e;
         for (int t = s; t < e; ++t) busy += p->steps[t].pre_n > 0;
-        // one busy step is worth an (armed) engine launch only as the whole plan: a small
-        // one-step plan armed on rails takes 5 us against 6 us (10-24 us cold) as an
-        // event-timed copy launch (profiles/r02/one_step/; XG_SOLO_MIN_STEPS=2 restores it)
-        const bool whole = s_run == 0 && run_end == p->nsteps && p->nsteps >= c->solo_min_steps && c->engine_arm &&
-                           !c->virt;
+        // one busy step is worth an engine launch only as the whole plan: a small one-step
+        // plan on rails takes 5 us armed against 6 us (10-24 us cold) as an event-timed copy
+        // launch (profiles/r02/one_step/; XG_SOLO_MIN_STEPS=2 restores the copy launch)
+        const bool whole = s_run == 0 && run_end == p->nsteps && p->nsteps >= c->solo_min_steps && !c->virt;
         if (busy < (whole ? 1 : 2)) {
             s = run_end > s ? run_end : s + 1;
             continue;
@@ -895,15 +957,16 @@ static int run_displ_scan(xg_plan *p, DisplScan &ds)
     p->ndisp = (int)ds.len.size();
     if (!p->ndisp) return XG_OK;
     const int ng = (int)ds.groups.size() - 1;
-    int64_t *d_len, *d_base;
-    int *d_groups;
-    xgk::DFix *d_fix;
+    DevMem m_len, m_base, m_groups, m_fix;     // freed on every return (the cross-check's included)
     const std::vector<int64_t> base(ng, 0);    // every step's staging starts at 0 (xg_devplan_build)
-    HIPCHK(hipMalloc(&p->d_disp, sizeof(int64_t) * p->ndisp));
-    HIPCHK(hipMalloc(&d_len, sizeof(int64_t) * p->ndisp));
-    HIPCHK(hipMalloc(&d_base, sizeof(int64_t) * ng));
-    HIPCHK(hipMalloc(&d_groups, sizeof(int) * (ng + 1)));
-    HIPCHK(hipMalloc(&d_fix, sizeof(xgk::DFix) * ds.fix.size()));
+    HIPCHK(hipMalloc(&p->d_disp, sizeof(int64_t) * p->ndisp));   // the plan's (xg_plan_free)
+    HIPCHK(hipMalloc(&m_len.p, sizeof(int64_t) * p->ndisp));
+    HIPCHK(hipMalloc(&m_base.p, sizeof(int64_t) * ng));
+    HIPCHK(hipMalloc(&m_groups.p, sizeof(int) * (ng + 1)));
+    HIPCHK(hipMalloc(&m_fix.p, sizeof(xgk::DFix) * ds.fix.size()));
+    int64_t *d_len = m_len.as<int64_t>(), *d_base = m_base.as<int64_t>();
+    int *d_groups = m_groups.as<int>();
+    xgk::DFix *d_fix = m_fix.as<xgk::DFix>();
     HIPCHK(hipMemcpyAsync(d_len, ds.len.data(), sizeof(int64_t) * p->ndisp, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(d_base, base.data(), sizeof(int64_t) * ng, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(d_groups, ds.groups.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice, c->stream));
@@ -926,14 +989,35 @@ static int run_displ_scan(xg_plan *p, DisplScan &ds)
                        p->reg->ptr[XG_BUF_STAGE_RECV]);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipFree(d_len));
-    HIPCHK(hipFree(d_base));
-    HIPCHK(hipFree(d_groups));
-    HIPCHK(hipFree(d_fix));
     return XG_OK;
 }
 
 extern "C" int xg_plan_free(xg_plan *p);
+static int launch_dispatches(const xg_plan *p, int b, int n, int64_t bytes);
+
+// Device half of a plan load: the piece table, the step events, the displacement scan
+// and the engine segments.  On an error the caller frees the plan (xg_plan_free takes a
+// half-loaded one: every handle starts null).
+static int plan_upload(xg_plan *p, const std::vector<xgk::DCopy> &pieces, DisplScan &ds)
+{
+    int rc;
+    if (p->npieces) {
+        HIPCHK(hipMalloc(&p->d_pieces, sizeof(xgk::DCopy) * pieces.size()));
+        HIPCHK(hipMemcpy(p->d_pieces, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
+    }
+    p->ev.assign(p->nsteps, nullptr);
+    for (auto &e : p->ev) HIPCHK(hipEventCreate(&e));
+    p->fork.assign(p->nsteps, nullptr);
+    p->join.assign(p->nsteps, nullptr);
+    for (int s = 0; s < p->nsteps; ++s)
+        if (p->steps[s].split) {
+            HIPCHK(hipEventCreateWithFlags(&p->fork[s], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&p->join[s], hipEventDisableTiming));
+        }
+    HIPCHK(hipEventCreate(&p->ev0));
+    if ((rc = run_displ_scan(p, ds)) || (rc = build_segments(p, pieces))) return rc;
+    return XG_OK;
+}
 
 extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_plan **out)
 {
@@ -1000,22 +1084,37 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         }
         for (int i = 0; i < sp.post_count; ++i)
             if (dp->copies[sp.post_begin + i].src_buf != XG_BUF_STAGE_RECV) goto bad;   // post copies unpack
-        st.p2p_b = (int)p->p2p.size();
-        for (int i = 0; i < sp.p2p_count; ++i) {
-            const xg_p2p &o = dp->p2p[sp.p2p_begin + i];
-            if (o.peer < 0 || o.peer >= c->nranks || o.peer == c->rank || o.buf < 0 || o.buf >= XG_NBUF || o.off < 0 ||
-                o.off + o.len > r->bytes[o.buf])
-                goto bad;
-            p->p2p.push_back(o);
+        {
+            // the step's RCCL calls: exactly what libxghost says this GPU posts (calls.c)
+            const int nc = xg_devplan_step_calls(dp, s, nullptr);
+            if (nc < 0) goto bad;
+            st.call_b = (int)p->calls.size();
+            st.call_n = nc;
+            p->call_begin.push_back(st.call_b);
+            p->calls.resize(st.call_b + nc);
+            xg_devplan_step_calls(dp, s, p->calls.data() + st.call_b);
+            st.p2p_n = 0;
+            st.sync_after = 0;
+            for (int i = 0; i < nc; ++i) {
+                const xg_call &o = p->calls[st.call_b + i];
+                if (o.kind == XG_CALL_BARRIER) {
+                    st.sync_after = c->nranks > 1;
+                    continue;
+                }
+                if ((o.kind != XG_CALL_SEND && o.kind != XG_CALL_RECV) || o.peer < 0 || o.peer >= c->nranks ||
+                    o.peer == c->rank || o.buf < 0 || o.buf >= XG_NBUF || o.off < 0 || o.len < 0 ||
+                    o.off + o.len > r->bytes[o.buf])
+                    goto bad;
+                st.p2p_n++;
+            }
         }
-        st.p2p_n = (int)p->p2p.size() - st.p2p_b;
-        st.sync_after = sp.sync_after && c->nranks > 1;
         st.split = c->split_local && st.p2p_n > 0 && nloc > 0;
         st.deferred = false;
         st.fused = c->fuse_unpack && s > 0 && npack > 0 && sp.stage_count == 0 && (st.split || nloc == 0) &&
                    !p->steps[s - 1].sync_after && dp->steps[s - 1].post_count > 0;
         if (st.fused) p->steps[s - 1].deferred = true;
     }
+    p->call_begin.push_back((int32_t)p->calls.size());
     // pass 2: the piece table, each launch's pieces contiguous (a fused launch: the
     // previous step's unpacks, then this step's packs)
     for (int s = 0; s < dp->nsteps; ++s) {
@@ -1101,22 +1200,8 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->npieces = (int)pieces.size();
     p->plen.assign(pieces.size() + 1, 0);
     for (size_t i = 0; i < pieces.size(); ++i) p->plen[i + 1] = p->plen[i] + pieces[i].len;
-    if (p->npieces) {
-        HIPCHK(hipMalloc(&p->d_pieces, sizeof(xgk::DCopy) * pieces.size()));
-        HIPCHK(hipMemcpy(p->d_pieces, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
-    }
-    p->ev.resize(dp->nsteps);
-    for (auto &e : p->ev) HIPCHK(hipEventCreate(&e));
-    p->fork.assign(dp->nsteps, nullptr);
-    p->join.assign(dp->nsteps, nullptr);
-    for (int s = 0; s < dp->nsteps; ++s)
-        if (p->steps[s].split) {
-            HIPCHK(hipEventCreateWithFlags(&p->fork[s], hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&p->join[s], hipEventDisableTiming));
-        }
-    HIPCHK(hipEventCreate(&p->ev0));
-    if ((rc = run_displ_scan(p, ds)) || (rc = build_segments(p, pieces))) {
-        xg_plan_free(p);
+    if ((rc = plan_upload(p, pieces, ds))) {
+        xg_plan_free(p);        // frees whatever the upload got to
         return rc;
     }
     for (int s = 0; s < p->nsteps; ++s) {
@@ -1125,8 +1210,18 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             p->nlaunch += p->segs[p->seg_of[s]].s0 == s;
             continue;
         }
-        p->nlaunch += (st.stage_n > 0) + (st.split ? (st.local_n > 0) + (st.pack_n > 0 || st.fused) : st.pre_n > 0 || st.fused) +
-                      (st.post_n > 0 && !st.deferred);
+        // kernel dispatches, as enqueue_pre / enqueue_post issue them (launch_cuts)
+        auto D = [&](int b, int n, int64_t bytes) { return n > 0 ? launch_dispatches(p, b, n, bytes) : 0; };
+        p->nlaunch += D(st.stage_b, st.stage_n, st.stage_bytes);
+        if (st.fused) {
+            const StepR &pv = p->steps[s - 1];
+            p->nlaunch += D(pv.post_b, pv.post_n + st.pack_n, pv.post_bytes + st.pack_bytes);
+        }
+        if (st.split)
+            p->nlaunch += D(st.local_b, st.local_n, st.local_bytes) + (st.fused ? 0 : D(st.pack_b, st.pack_n, st.pack_bytes));
+        else if (!st.fused)
+            p->nlaunch += D(st.local_b, st.pre_n, st.local_bytes + st.pack_bytes);
+        if (!st.deferred) p->nlaunch += D(st.post_b, st.post_n, st.post_bytes);
     }
     {
         int64_t run = 0;
@@ -1157,7 +1252,15 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             }
             s = e > s ? e : s + 1;
         }
-        if (any) HIPCHK(hipMalloc(&p->d_cstamp, 8 * (size_t)p->nsteps));
+        if (any) {
+            const hipError_t e = hipMalloc(&p->d_cstamp, 8 * (size_t)p->nsteps);
+            if (e != hipSuccess) {
+                p->d_cstamp = nullptr;
+                fprintf(stderr, "xg: HIP error %s: chain stamps\n", hipGetErrorString(e));
+                xg_plan_free(p);
+                return XG_EHIP;
+            }
+        }
     }
     *out = p;
     return XG_OK;
@@ -1170,21 +1273,26 @@ bad:
 extern "C" int xg_plan_free(xg_plan *p)
 {
     if (!p) return XG_OK;
-    HIPCHK(hipStreamSynchronize(p->ctx->stream));
-    HIPCHK(hipStreamSynchronize(p->ctx->side));
-    if (p->d_pieces) HIPCHK(hipFree(p->d_pieces));
-    if (p->d_sb) HIPCHK(hipFree(p->d_sb));
-    if (p->d_epieces) HIPCHK(hipFree(p->d_epieces));
-    if (p->d_engine) HIPCHK(hipFree(p->d_engine));
-    if (p->d_disp) HIPCHK(hipFree(p->d_disp));
-    if (p->db) HIPCHK(hipHostFree((void *)p->db));
-    if (p->d_solo) HIPCHK(hipFree(p->d_solo));
-    if (p->d_cstamp) HIPCHK(hipFree(p->d_cstamp));
-    for (auto &e : p->ev) HIPCHK(hipEventDestroy(e));
-    for (auto &e : p->fork) if (e) HIPCHK(hipEventDestroy(e));
-    for (auto &e : p->join) if (e) HIPCHK(hipEventDestroy(e));
-    if (p->ev0) HIPCHK(hipEventDestroy(p->ev0));
+    // release everything even after an error (a half-loaded plan included); report the first
+    hipError_t first = hipSuccess;
+    auto keep = [&](hipError_t e) {
+        if (e != hipSuccess && first == hipSuccess) first = e;
+    };
+    keep(hipStreamSynchronize(p->ctx->stream));
+    keep(hipStreamSynchronize(p->ctx->side));
+    for (void *q : {(void *)p->d_pieces, (void *)p->d_sb, (void *)p->d_epieces, (void *)p->d_engine,
+                    (void *)p->d_disp, (void *)p->d_solo, (void *)p->d_cstamp})
+        if (q) keep(hipFree(q));
+    if (p->db) keep(hipHostFree((void *)p->db));
+    for (auto &e : p->ev) if (e) keep(hipEventDestroy(e));
+    for (auto &e : p->fork) if (e) keep(hipEventDestroy(e));
+    for (auto &e : p->join) if (e) keep(hipEventDestroy(e));
+    if (p->ev0) keep(hipEventDestroy(p->ev0));
     delete p;
+    if (first != hipSuccess) {
+        fprintf(stderr, "xg: HIP error %s while freeing a plan\n", hipGetErrorString(first));
+        return XG_EHIP;
+    }
     return XG_OK;
 }
 
@@ -1222,53 +1330,52 @@ extern "C" int xg_plan_displs(const xg_plan *p, int64_t *out, int n)
 // whose source + destination exceed the 256 MiB Infinity Cache streams through it with
 // non-temporal loads and stores (6.3 TB/s vs 5.5-5.6 plain from 256 MiB up), a smaller
 // one keeps the default policy, which re-runs serve from the cache
-// (profiles/r02/copy_nt_sizes.txt).  1..6 force one form (A/B, tests).
-// start: stamp the launch's start there (variants 1 and 6 only; see copy_kernel_g)
-static int launch_one(xg_plan *p, int b, int n, int v, hipStream_t st, unsigned long long *start);
-
-static int launch_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t st, unsigned long long *start = nullptr,
-                       bool reread = false)
+// (profiles/r02/copy_nt_sizes.txt).  1 / 6 force one form (A/B, tests).
+//
+// A launch of more than 1.5 x launch_max bytes goes as back-to-back kernel dispatches of
+// about launch_max bytes each (its pieces are independent: the same step, a few more
+// kernel boundaries).  P256 A32 -d 4 MiB m1 / m2 (one 32 GiB step, 1 M pieces): 12.6 ->
+// 11.0 ms at 512 MiB per dispatch, 11.5 at 128 MiB; cutting by piece count instead hurt
+// steps of small pieces (profiles/r02/launch_split/).  launch_cuts gives the dispatches
+// [first piece, end) of pieces [b, b + n): every count of launches (xg_plan_launches, the
+// kernel-timing sessions) counts these dispatches, as rocprofv3 does.
+static void launch_cuts(const xg_plan *p, int b, int n, int64_t bytes, std::vector<std::pair<int, int>> &out)
 {
-    const int v = copy_variant(p, bytes, reread);
-    if (start && v != 1 && v != 6) return XG_EARG;
-    // a launch of more than launch_max bytes goes as back-to-back launches of about
-    // launch_max bytes each (its pieces are independent: the same step, a few more kernel
-    // boundaries).  P256 A32 -d 4 MiB m1 / m2 (one 32 GiB step, 1 M pieces): 12.6 -> 11.0 ms
-    // at 512 MiB per launch, 11.5 at 128 MiB; cutting by piece count instead hurt steps of
-    // small pieces (profiles/r02/launch_split/)
+    out.clear();
     const int64_t cap = p->ctx->launch_max;
-    if (cap > 0 && bytes > cap + cap / 2 && !p->plen.empty()) {
-        const int64_t *pre = p->plen.data();        // prefix sums of the piece lengths
-        int rc, o = b;
-        while (o < b + n) {
-            // the first piece past cap bytes from o
-            const int64_t want = pre[o] + cap;
-            int e = (int)(std::lower_bound(pre + o + 1, pre + b + n + 1, want) - pre);
-            if (b + n - e < 16 || pre[b + n] - pre[e] < cap / 2) e = b + n;   // no runt launch at the end
-            if ((rc = launch_one(p, o, e - o, v, st, o == b ? start : nullptr))) return rc;
-            o = e;
-        }
-        return XG_OK;
+    if (!(cap > 0 && bytes > cap + cap / 2 && (int)p->plen.size() > b + n)) {
+        out.push_back({b, b + n});
+        return;
     }
-    return launch_one(p, b, n, v, st, start);
+    const int64_t *pre = p->plen.data();        // prefix sums of the piece lengths
+    for (int o = b; o < b + n;) {
+        // the first piece boundary at least cap bytes past o (lower_bound may return b + n + 1
+        // when fewer than cap bytes remain: clamp), then no runt dispatch at the end
+        int e = (int)(std::lower_bound(pre + o + 1, pre + b + n + 1, pre[o] + cap) - pre);
+        if (e > b + n) e = b + n;
+        if (b + n - e < 16 || pre[b + n] - pre[e] < cap / 2) e = b + n;
+        out.push_back({o, e});
+        o = e;
+    }
+}
+
+static int launch_dispatches(const xg_plan *p, int b, int n, int64_t bytes)
+{
+    std::vector<std::pair<int, int>> cuts;
+    launch_cuts(p, b, n, bytes, cuts);
+    return (int)cuts.size();
 }
 
 static int launch_one(xg_plan *p, int b, int n, int v, hipStream_t st, unsigned long long *start)
 {
     const xgk::DCopy *pc = p->d_pieces + b;
-    switch (v) {
-    case 2: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxPlain>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 3: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxSC1>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 4: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 5: hipLaunchKernelGGL((xgk::copy_kernel_b<8, xgk::kAuxNT>), dim3(n), dim3(xgk::kThreads), 0, st, pc); break;
-    case 6: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start); break;
-    default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start); break;
-    }
+    if (v == 6) hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start);
+    else hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start);
     HIPCHK(hipGetLastError());
     return XG_OK;
 }
 
-// kernel-timing session bookkeeping around one launch of `bytes` copied bytes
+// kernel-timing session bookkeeping around one kernel dispatch of `bytes` copied bytes
 static int kt_before(xg_ctx *c, hipStream_t stream, bool *kt)
 {
     *kt = c->kt_mode == 1 && 2 * (size_t)c->nk + 1 < c->kev.size();
@@ -1289,14 +1396,31 @@ static int kt_after(xg_ctx *c, hipStream_t stream, bool kt, int64_t bytes)
     return XG_OK;
 }
 
+// One copy launch of pieces [b, b + n) moving `bytes`, as its dispatches (launch_cuts),
+// each bracketed by kernel-timing events when a per-launch session is on.  start: the
+// first dispatch stamps its start there (see copy_kernel_g).
+static int launch_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t st, unsigned long long *start = nullptr,
+                       bool reread = false)
+{
+    const int v = copy_variant(p, bytes, reread);
+    if (start && v != 1 && v != 6) return XG_EARG;
+    std::vector<std::pair<int, int>> cuts;
+    launch_cuts(p, b, n, bytes, cuts);
+    int rc;
+    for (const auto &q : cuts) {
+        const int64_t nb = cuts.size() == 1 ? bytes : p->plen[q.second] - p->plen[q.first];
+        bool kt;
+        if ((rc = kt_before(p->ctx, st, &kt))) return rc;
+        if ((rc = launch_one(p, q.first, q.second - q.first, v, st, q.first == b ? start : nullptr))) return rc;
+        if ((rc = kt_after(p->ctx, st, kt, nb))) return rc;
+    }
+    return XG_OK;
+}
+
 // one copy launch, bracketed by kernel-timing events when a per-launch session is on
 static int timed_copy(xg_plan *p, int b, int n, int64_t bytes, hipStream_t stream, bool reread = false)
 {
-    int rc;
-    bool kt;
-    if ((rc = kt_before(p->ctx, stream, &kt))) return rc;
-    if ((rc = launch_copy(p, b, n, bytes, stream, nullptr, reread))) return rc;
-    return kt_after(p->ctx, stream, kt, bytes);
+    return launch_copy(p, b, n, bytes, stream, nullptr, reread);
 }
 
 // step part 1: stage copies, then local gather/scatter + packs.  A split step
@@ -1350,18 +1474,20 @@ static int enqueue_step(xg_plan *p, int s)
         return XG_EARG;
     }
     if ((rc = enqueue_pre(p, s, c->stream, c->side))) return rc;
-    if (st.p2p_n) {
-        NCCLCHK(ncclGroupStart());
-        for (int i = 0; i < st.p2p_n; ++i) {
-            const xg_p2p &o = p->p2p[st.p2p_b + i];
-            uint8_t *ptr = p->reg->ptr[o.buf] + o.off;
-            if (o.is_send)
-                NCCLCHK(ncclSend(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream));
-            else
-                NCCLCHK(ncclRecv(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream));
-        }
-        NCCLCHK(ncclGroupEnd());
-    }
+    // the step's send/recv calls, in the order libxghost lists them (xg_devplan_step_calls),
+    // as one group; the barrier call, if any, is the step's last and follows the unpacks
+    const xg_call *cl = p->calls.data() + st.call_b;
+    if (st.p2p_n && (rc = rccl_group(
+                         st.p2p_n,
+                         [&](int i) {
+                             const xg_call &o = cl[i];
+                             uint8_t *ptr = p->reg->ptr[o.buf] + o.off;
+                             return o.kind == XG_CALL_SEND
+                                        ? ncclSend(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream)
+                                        : ncclRecv(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream);
+                         },
+                         "step exchange")))
+        return rc;
     if ((rc = enqueue_post(p, s, c->stream))) return rc;
     if (st.sync_after)   /* in-loop MPI_Barrier: every GPU finishes this step before any goes on */
         NCCLCHK(ncclAllReduce(c->d_red, c->d_red, 1, ncclFloat64, ncclMax, c->comm, c->stream));
@@ -1645,8 +1771,29 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
         NCCLCHK(ncclGetUniqueId(&id));
         NCCLCHK(ncclCommInitRank(&c0->comm, 1, id, 0));
     }
+    // RCCL's pairing of every GPU's calls (libxghost, calls.c): the same lists a real rank
+    // posts in enqueue_step, paired as RCCL pairs them; refused unless every pair falls in
+    // one step with one length and the GPUs agree on the barriers
+    std::vector<xg_call_pair> pairs;
+    {
+        std::vector<const xg_call *> cl(n);
+        std::vector<const int32_t *> cb(n);
+        for (int g = 0; g < n; ++g) {
+            cl[g] = plans[g]->calls.data();
+            cb[g] = plans[g]->call_begin.data();
+        }
+        char err[256];
+        const int64_t np = xg_calls_match(n, nst, cl.data(), cb.data(), nullptr, 0, err, sizeof err);
+        if (np < 0) {
+            fprintf(stderr, "xg_vplans_run: the GPUs' RCCL calls do not pair: %s\n", err);
+            return XG_EARG;
+        }
+        pairs.resize((size_t)np + 1);
+        xg_calls_match(n, nst, cl.data(), cb.data(), pairs.data(), np, err, sizeof err);
+        pairs.resize((size_t)np);
+    }
     HIPCHK(hipEventRecord(plans[0]->ev0, st));
-    std::vector<std::vector<const xg_p2p *>> sends((size_t)n * n), recvs((size_t)n * n);
+    size_t q0 = 0;
     for (int s = 0; s < nst; ++s) {
         for (int g = 0; g < n; ++g) {
             xg_plan *pg = plans[g];
@@ -1655,47 +1802,34 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
             else rc = pg->segs[gi].s0 == s ? launch_seg(pg, pg->segs[gi], st) : XG_OK;
             if (rc) return rc;
         }
-        for (auto &v : sends) v.clear();
-        for (auto &v : recvs) v.clear();
-        for (int g = 0; g < n; ++g) {
-            const StepR &sr = plans[g]->steps[s];
-            for (int i = 0; i < sr.p2p_n; ++i) {
-                const xg_p2p &o = plans[g]->p2p[sr.p2p_b + i];
-                if (o.is_send) sends[(size_t)g * n + o.peer].push_back(&o);
-                else recvs[(size_t)o.peer * n + g].push_back(&o);
+        size_t q1 = q0;
+        while (q1 < pairs.size() && pairs[q1].step == s) ++q1;
+        auto ends = [&](const xg_call_pair &q, uint8_t **src, uint8_t **dst) {
+            const xg_call &sc = plans[q.src]->calls[q.send_call], &rcv = plans[q.dst]->calls[q.recv_call];
+            *src = plans[q.src]->reg->ptr[sc.buf] + sc.off;
+            *dst = plans[q.dst]->reg->ptr[rcv.buf] + rcv.off;
+        };
+        if (!rccl) {
+            for (size_t q = q0; q < q1; ++q) {
+                uint8_t *src, *dst;
+                ends(pairs[q], &src, &dst);
+                if (pairs[q].len) HIPCHK(hipMemcpyAsync(dst, src, (size_t)pairs[q].len, hipMemcpyDeviceToDevice, st));
             }
+        } else if (q1 > q0) {
+            // every pair of the step as a self send + receive in ONE group (issue order = pair order)
+            if ((rc = rccl_group(
+                     (int)(2 * (q1 - q0)),
+                     [&](int i) {
+                         uint8_t *src, *dst;
+                         const xg_call_pair &q = pairs[q0 + i / 2];
+                         ends(q, &src, &dst);
+                         return i % 2 == 0 ? ncclSend(src, (size_t)q.len, ncclUint8, 0, c0->comm, st)
+                                           : ncclRecv(dst, (size_t)q.len, ncclUint8, 0, c0->comm, st);
+                     },
+                     "virtual job step")))
+                return rc;
         }
-        bool grouped = false;
-        for (int g = 0; g < n; ++g)
-            for (int h = 0; h < n; ++h) {
-                const auto &sv = sends[(size_t)g * n + h], &rv = recvs[(size_t)g * n + h];
-                if (sv.size() != rv.size()) {
-                    fprintf(stderr, "xg_vplans_run: step %d: GPU %d posts %zu sends to %d, which posts %zu receives\n",
-                            s, g, sv.size(), h, rv.size());
-                    return XG_EARG;
-                }
-                for (size_t k = 0; k < sv.size(); ++k) {
-                    if (sv[k]->len != rv[k]->len) {
-                        fprintf(stderr, "xg_vplans_run: step %d: %d->%d op %zu: send %lld B, receive %lld B\n", s,
-                                g, h, k, (long long)sv[k]->len, (long long)rv[k]->len);
-                        return XG_EARG;
-                    }
-                    if (!sv[k]->len) continue;
-                    uint8_t *dst = plans[h]->reg->ptr[rv[k]->buf] + rv[k]->off;
-                    uint8_t *src = plans[g]->reg->ptr[sv[k]->buf] + sv[k]->off;
-                    if (!rccl) {
-                        HIPCHK(hipMemcpyAsync(dst, src, (size_t)sv[k]->len, hipMemcpyDeviceToDevice, st));
-                        continue;
-                    }
-                    if (!grouped) {
-                        NCCLCHK(ncclGroupStart());
-                        grouped = true;
-                    }
-                    NCCLCHK(ncclSend(src, (size_t)sv[k]->len, ncclUint8, 0, c0->comm, st));
-                    NCCLCHK(ncclRecv(dst, (size_t)rv[k]->len, ncclUint8, 0, c0->comm, st));
-                }
-            }
-        if (grouped) NCCLCHK(ncclGroupEnd());
+        q0 = q1;
         for (int g = 0; g < n; ++g)
             if (plans[g]->seg_of[s] < 0 && (rc = enqueue_post(plans[g], s, st))) return rc;
         if (rccl && plans[0]->steps[s].sync_after)
@@ -1792,52 +1926,54 @@ extern "C" int xg_p2p_bench(xg_ctx *c, int64_t bytes, int mode, int reps, double
     if ((n < 2 && !self) || bytes <= 0 || reps < 1 || mode < 0 || mode > 2) return XG_EARG;
     HIPCHK(hipSetDevice(c->device));
     const int npeer = self ? 1 : (mode == 0 ? n - 1 : 1);
-    uint8_t *sb, *rb;
-    HIPCHK(hipMalloc(&sb, bytes * npeer));
-    HIPCHK(hipMalloc(&rb, bytes * npeer));
+    DevMem m_sb, m_rb;                  // freed, and the events destroyed, on every return path
+    EventPair ev;
+    HIPCHK(hipMalloc(&m_sb.p, bytes * npeer));
+    HIPCHK(hipMalloc(&m_rb.p, bytes * npeer));
+    uint8_t *sb = m_sb.as<uint8_t>(), *rb = m_rb.as<uint8_t>();
     HIPCHK(hipMemsetAsync(sb, r & 0xff, bytes * npeer, c->stream));
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    int rc = XG_OK;
-    auto one = [&]() -> int {
-        NCCLCHK(ncclGroupStart());
-        if (self) {
-            NCCLCHK(ncclSend(sb, (size_t)bytes, ncclUint8, 0, c->comm, c->stream));
-            NCCLCHK(ncclRecv(rb, (size_t)bytes, ncclUint8, 0, c->comm, c->stream));
-        } else if (mode == 0) {
-            for (int k = 1; k < n; ++k) {
-                const int to = (r + k) % n, from = (r - k + n) % n;
-                NCCLCHK(ncclSend(sb + (int64_t)(k - 1) * bytes, (size_t)bytes, ncclUint8, to, c->comm, c->stream));
-                NCCLCHK(ncclRecv(rb + (int64_t)(k - 1) * bytes, (size_t)bytes, ncclUint8, from, c->comm, c->stream));
-            }
-        } else if (mode == 1) {
-            NCCLCHK(ncclSend(sb, (size_t)bytes, ncclUint8, (r + 1) % n, c->comm, c->stream));
-            NCCLCHK(ncclRecv(rb, (size_t)bytes, ncclUint8, (r - 1 + n) % n, c->comm, c->stream));
-        } else if (r == 1) {
-            NCCLCHK(ncclSend(sb, (size_t)bytes, ncclUint8, 0, c->comm, c->stream));
-        } else if (r == 0) {
-            NCCLCHK(ncclRecv(rb, (size_t)bytes, ncclUint8, 1, c->comm, c->stream));
+    HIPCHK(hipEventCreate(&ev.e[0]));
+    HIPCHK(hipEventCreate(&ev.e[1]));
+    // this rank's calls of one repetition: (send?, peer, offset into sb / rb)
+    struct Op { bool send; int peer; int64_t off; };
+    std::vector<Op> ops;
+    if (self) {
+        ops = {{true, 0, 0}, {false, 0, 0}};
+    } else if (mode == 0) {
+        for (int k = 1; k < n; ++k) {
+            ops.push_back({true, (r + k) % n, (int64_t)(k - 1) * bytes});
+            ops.push_back({false, (r - k + n) % n, (int64_t)(k - 1) * bytes});
         }
-        NCCLCHK(ncclGroupEnd());
-        return XG_OK;
+    } else if (mode == 1) {
+        ops = {{true, (r + 1) % n, 0}, {false, (r - 1 + n) % n, 0}};
+    } else if (r == 1) {
+        ops = {{true, 0, 0}};
+    } else if (r == 0) {
+        ops = {{false, 1, 0}};
+    }
+    auto one = [&]() -> int {
+        return rccl_group(
+            (int)ops.size(),
+            [&](int i) {
+                const Op &o = ops[i];
+                return o.send ? ncclSend(sb + o.off, (size_t)bytes, ncclUint8, o.peer, c->comm, c->stream)
+                              : ncclRecv(rb + o.off, (size_t)bytes, ncclUint8, o.peer, c->comm, c->stream);
+            },
+            "xg_p2p_bench");
     };
+    int rc = XG_OK;
     for (int w = 0; w < 2 && !rc; ++w) rc = one();          // connection set-up + warm-up
     if (!rc) rc = xg_barrier(c);
-    if (!rc) {
-        HIPCHK(hipEventRecord(e0, c->stream));
-        for (int k = 0; k < reps && !rc; ++k) rc = one();
-        HIPCHK(hipEventRecord(e1, c->stream));
-        HIPCHK(hipEventSynchronize(e1));
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-        const double s_rep = ms * 1e-3 / reps;
-        if (sec) *sec = s_rep;
-        if (gbps) *gbps = (mode == 2 && !self ? (r < 2 ? (double)bytes : 0.0) : (double)bytes * npeer) / s_rep / 1e9;
-    }
-    HIPCHK(hipEventDestroy(e0));
-    HIPCHK(hipEventDestroy(e1));
-    HIPCHK(hipFree(sb));
-    HIPCHK(hipFree(rb));
-    return rc;
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(ev.e[0], c->stream));
+    for (int k = 0; k < reps && !rc; ++k) rc = one();
+    HIPCHK(hipEventRecord(ev.e[1], c->stream));
+    HIPCHK(hipEventSynchronize(ev.e[1]));
+    if (rc) return rc;
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ev.e[0], ev.e[1]));
+    const double s_rep = ms * 1e-3 / reps;
+    if (sec) *sec = s_rep;
+    if (gbps) *gbps = (mode == 2 && !self ? (r < 2 ? (double)bytes : 0.0) : (double)bytes * npeer) / s_rep / 1e9;
+    return XG_OK;
 }

@@ -29,6 +29,44 @@
 
 namespace {
 
+// copy_kernel_b<U, AUX>: the exchange's piece copy through buffer resources with store policy
+// AUX (an A/B variant measured in round 1/2, kept here for the ceiling tables only)
+// Pipelined piece copy through buffer resources (n: bytes, a multiple of 16,
+// < 2^31): every lane keeps U 16-B loads of the next block in flight while it
+// stores the current block.  The trip count is wave-uniform; out-of-range
+// lanes of the last block load 0 and their stores are dropped by the range check.
+template <int U, int AUX>
+__device__ __forceinline__ void pipelined_copy16_b(const uint8_t *src, uint8_t *dst, int n)
+{
+    const xgk::brsrc rs = xgk::make_rsrc(src, n), rd = xgk::make_rsrc(dst, n);
+    constexpr int blk = U * xgk::kThreads * 16;
+    const int lane = (int)threadIdx.x * 16;
+    xgk::u32x4 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = xgk::bload16(rs, lane + u * xgk::kThreads * 16);
+    for (int base = 0; base < n; base += blk) {
+        xgk::u32x4 nxt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) nxt[u] = xgk::bload16(rs, base + blk + lane + u * xgk::kThreads * 16);
+#pragma unroll
+        for (int u = 0; u < U; ++u) xgk::bstore16<AUX>(rd, base + lane + u * xgk::kThreads * 16, cur[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+    }
+}
+
+template <int U, int AUX>
+__global__ __launch_bounds__(xgk::kThreads) void copy_kernel_b(const xgk::DCopy *__restrict__ pieces)
+{
+    __shared__ uint32_t lds[2][xgk::kTileWords];
+    const xgk::DCopy c = pieces[blockIdx.x];
+    if ((((uintptr_t)c.src | (uintptr_t)c.dst | (uint64_t)c.len) & 15) == 0)
+        pipelined_copy16_b<U, AUX>(c.src, c.dst, (int)c.len);
+    else
+        xgk::realign_copy(c.src, c.dst, c.len, lds);
+}
+
+
 __global__ __launch_bounds__(xgk::kThreads) void gridstride_copy(const xgk::u32x4 *__restrict__ s,
                                                                  xgk::u32x4 *__restrict__ t, int64_t n4)
 {
@@ -138,7 +176,7 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
         case 0: hipLaunchKernelGGL(gridstride_copy, dim3(2048), dim3(xgk::kThreads), 0, st, (const xgk::u32x4 *)a,
                                    (xgk::u32x4 *)b, n4); break;
         case 1: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
-        case 2: hipLaunchKernelGGL((xgk::copy_kernel_b<4, xgk::kAuxSC1>), dim3(np), dim3(xgk::kThreads), 0, st, dp);
+        case 2: hipLaunchKernelGGL((copy_kernel_b<4, xgk::kAuxSC1>), dim3(np), dim3(xgk::kThreads), 0, st, dp);
                 break;
         case 3: hipLaunchKernelGGL(read_only, dim3(4096), dim3(xgk::kThreads), 0, st, (const xgk::u32x4 *)a, n4, sink);
                 break;

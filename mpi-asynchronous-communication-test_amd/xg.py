@@ -60,6 +60,20 @@ class DevPlan(C.Structure):
                 ("remote_recv_bytes", C.c_int64)]
 
 
+class Call(C.Structure):
+    """xg_call: one RCCL call of a step (XG_CALL_SEND / RECV / BARRIER)."""
+    _fields_ = [("kind", C.c_int32), ("peer", C.c_int32), ("buf", C.c_int32), ("pad", C.c_int32),
+                ("off", C.c_int64), ("len", C.c_int64)]
+
+
+class CallPair(C.Structure):
+    _fields_ = [("step", C.c_int32), ("src", C.c_int32), ("dst", C.c_int32), ("send_call", C.c_int32),
+                ("recv_call", C.c_int32), ("pad", C.c_int32), ("len", C.c_int64)]
+
+
+CALL_SEND, CALL_RECV, CALL_BARRIER = 1, 2, 3
+
+
 class SoloShape(C.Structure):
     _fields_ = [("rails", C.c_int32), ("npieces", C.c_int32), ("nrows", C.c_int32), ("nmeta", C.c_int32)]
 
@@ -134,6 +148,13 @@ def host():
         h.xg_devplan_build.restype = C.POINTER(DevPlan)
         h.xg_devplan_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64]
         h.xg_devplan_free.argtypes = [C.POINTER(DevPlan)]
+        h.xg_devplan_step_calls.argtypes = [C.POINTER(DevPlan), C.c_int, C.POINTER(Call)]
+        h.xg_calls_match.restype = C.c_int64
+        h.xg_calls_match.argtypes = [C.c_int, C.c_int, C.POINTER(C.POINTER(Call)), C.POINTER(C.POINTER(C.c_int32)),
+                                     C.POINTER(CallPair), C.c_int64, C.c_char_p, C.c_size_t]
+        h.xg_devplans_match.restype = C.c_int64
+        h.xg_devplans_match.argtypes = [C.POINTER(C.POINTER(DevPlan)), C.c_int, C.POINTER(CallPair), C.c_int64,
+                                        C.c_char_p, C.c_size_t]
         h.xg_fill_runs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(SegRun)]
         h.xg_verify_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(Slot)]
         h.xg_engine_hazards.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int)]
@@ -206,6 +227,50 @@ def solo_reduce_stamps(stamps, s0, s1):
     out = (C.c_uint64 * n)()
     host().xg_solo_reduce_stamps(arr, R, n, s0, s1, out)
     return list(out)
+
+
+def _pairs(n, arr):
+    return [(q.step, q.src, q.dst, q.send_call, q.recv_call, q.len) for q in arr[:n]]
+
+
+def calls_match(calls, nsteps):
+    """xg_calls_match over calls[g] = [[(kind, peer, buf, off, len), ...] per step]: RCCL's
+    pairing of a G-GPU job's calls; returns [(step, src, dst, send_call, recv_call, len)]
+    (step-major) or raises XGError with the reason."""
+    G = len(calls)
+    arrs, begs = [], []
+    for g in range(G):
+        flat = [c for st in calls[g] for c in st]
+        a = (Call * max(1, len(flat)))(*[Call(k, p, b, 0, o, n) for k, p, b, o, n in flat])
+        beg = [0]
+        for st in calls[g]:
+            beg.append(beg[-1] + len(st))
+        arrs.append(a)
+        begs.append((C.c_int32 * len(beg))(*beg))
+    ca = (C.POINTER(Call) * G)(*[C.cast(a, C.POINTER(Call)) for a in arrs])
+    cb = (C.POINTER(C.c_int32) * G)(*[C.cast(b, C.POINTER(C.c_int32)) for b in begs])
+    err = C.create_string_buffer(512)
+    n = host().xg_calls_match(G, nsteps, ca, cb, None, 0, err, 512)
+    if n < 0:
+        raise XGError(err.value.decode())
+    out = (CallPair * max(1, n))()
+    host().xg_calls_match(G, nsteps, ca, cb, out, n, err, 512)
+    return _pairs(n, out)
+
+
+def devplans_match(plans):
+    """xg_devplans_match over the G device plans (DevicePlanView or raw POINTER(DevPlan)) of one
+    job: the pairs, or XGError naming the first call that RCCL would pair differently."""
+    ptrs = [p.ptr if isinstance(p, DevicePlanView) else p for p in plans]
+    G = len(ptrs)
+    arr = (C.POINTER(DevPlan) * G)(*ptrs)
+    err = C.create_string_buffer(512)
+    n = host().xg_devplans_match(arr, G, None, 0, err, 512)
+    if n < 0:
+        raise XGError(err.value.decode())
+    out = (CallPair * max(1, n))()
+    host().xg_devplans_match(arr, G, out, n, err, 512)
+    return _pairs(n, out)
 
 
 def method_label(method):
@@ -303,6 +368,23 @@ class Schedule:
     def devplan(self, ngpus, g, pack_max_seg=4 << 20):
         return DevicePlanView(self, ngpus, g, pack_max_seg)
 
+    def check_pairing(self, ngpus, pack_max_seg=4 << 20):
+        """Refuse (XGError) a job whose GPUs' RCCL calls RCCL would not pair step by step
+        (xg_devplans_match over every GPU's plan, built in C); returns the number of pairs."""
+        h = host()
+        plans = [h.xg_devplan_build(self._h, ngpus, g, pack_max_seg) for g in range(ngpus)]
+        try:
+            arr = (C.POINTER(DevPlan) * ngpus)(*plans)
+            err = C.create_string_buffer(512)
+            n = h.xg_devplans_match(arr, ngpus, None, 0, err, 512)
+            if n < 0:
+                raise XGError("method %d on %d GPUs: RCCL calls do not pair: %s"
+                              % (self.method, ngpus, err.value.decode()))
+            return n
+        finally:
+            for q in plans:
+                h.xg_devplan_free(q)
+
     def fill_runs(self, ngpus, g):
         n = host().xg_fill_runs(self._h, ngpus, g, None)
         runs = (SegRun * max(1, n))()
@@ -338,6 +420,13 @@ class DevicePlanView:
     @property
     def ptr(self):
         return self._p
+
+    def calls(self, step):
+        """xg_devplan_step_calls: [(kind, peer, buf, off, len)] this GPU posts in `step`"""
+        n = host().xg_devplan_step_calls(self._p, step, None)
+        arr = (Call * max(1, n))()
+        host().xg_devplan_step_calls(self._p, step, arr)
+        return [(c.kind, c.peer, c.buf, c.off, c.len) for c in arr[:n]]
 
     def __del__(self):
         if getattr(self, "_p", None) and _host is not None:
@@ -416,6 +505,7 @@ class Context:
         ub = C.create_string_buffer(uid, 128) if uid else None
         _check(d.xg_init(C.byref(self._c), rank, nranks, dev, ub), "xg_init")
         self.rank, self.nranks = rank, nranks
+        self.is_virtual = False
 
     @classmethod
     def virtual(cls, rank, nranks, device=0):
@@ -425,6 +515,7 @@ class Context:
         self._c = C.c_void_p()
         _check(globals()["device"]().xg_init_virtual(C.byref(self._c), rank, nranks, device), "xg_init_virtual")
         self.rank, self.nranks = rank, nranks
+        self.is_virtual = True
         return self
 
     @property
@@ -530,6 +621,10 @@ class MethodRun:
         d = device()
         self.ctx, self.sched, self.it, self.mode, self.pack_max_seg = ctx, sched, it, mode, pack_max_seg
         G, g = ctx.nranks, ctx.rank
+        if G > 1 and not getattr(ctx, "is_virtual", False):
+            # a real multi-GPU job: refuse, on every rank alike, calls RCCL would not pair
+            # step by step, before any rank posts one (xg_devplans_match)
+            sched.check_pairing(G, pack_max_seg)
         self.view = sched.devplan(G, g, pack_max_seg)
         self._shared = regions is not None
         if regions is not None:

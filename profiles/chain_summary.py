@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Tabulate profiles/chain_modes.sh output: per method label and experiment, the median over
 repetitions of the CLI's 'max total time' in each mode, the reference's beside it, and the
-ratio of the default mode to the reference.  usage: chain_summary.py <outdir>"""
+ratio of the default mode (the first present: launch, then the round-2 solo_armed) to the
+reference.  usage: chain_summary.py <outdir>"""
 import glob
 import os
 import re
@@ -19,11 +20,11 @@ def parse(path):
 
 
 def main(d):
-    modes = [m for m in ["solo_armed", "solo1_armed", "grid_armed", "solo_launch", "grid_launch"]
-             if glob.glob(os.path.join(d, m + "_*.txt"))]
+    modes = [m for m in ["launch", "armed", "grid_launch", "copy1", "solo_armed", "solo1_armed", "grid_armed",
+                         "solo_launch"] if glob.glob(os.path.join(d, m + "_*.txt"))]
     runs = {m: [parse(f) for f in sorted(glob.glob(os.path.join(d, m + "_*.txt")))] for m in modes}
     refs = [parse(f) for f in sorted(glob.glob(os.path.join(d, "ref*.txt")))]   # ref.txt or ref_<r>.txt
-    base = runs["solo_armed"][0]
+    base = runs[modes[0]][0]
     print(("%-36s %4s" + " %11s" * len(modes) + " %10s %7s") % ("method", "exp", *modes, "reference", "ratio"))
     seen = {}
     for i, (lab, _t) in enumerate(base):
@@ -37,8 +38,8 @@ def main(d):
                 rv.append(rf[e] * 1e6)
         rv = S.median(rv) if rv else float("nan")
         print(("%-36s %4d" + " %11.1f" * len(modes) + " %10.1f %7.2f") % (lab, e, *med, rv, med[0] / rv))
-    print("(us, median over %d repetitions, reference median over %d runs; ratio = solo_armed / reference)"
-          % (len(runs["solo_armed"]), len(refs)))
+    print("(us, median over %d repetitions, reference median over %d runs; ratio = %s / reference)"
+          % (len(runs[modes[0]]), len(refs), modes[0]))
 
 
 if __name__ == "__main__":

@@ -2,6 +2,7 @@
 CPU (tests/test_bench_logic.py).  Schedules, device plans, fill/verify descriptors and
 timers are the REAL host library (libxghost.so); only what needs a GPU -- contexts,
 RCCL, kernels -- is replaced by plausible no-ops.  Never imported by the product."""
+import json
 import os
 import sys
 import time
@@ -15,6 +16,17 @@ def make(real_xg):
         setattr(fake, name, getattr(real_xg, name))
     calls = {"p2p_bench": 0, "ktime": [], "runs": 0}
     fake.calls = calls
+    # every collective-level call this rank makes, in order (what its RCCL communicator
+    # would see): compared across ranks by tests/test_rccl_calls.py
+    trace = []
+    fake.trace = trace
+
+    def _wait_all(d, name, nranks):
+        t0 = time.time()
+        while not all(os.path.exists(os.path.join(d, name % r)) for r in range(nranks)):
+            if time.time() - t0 > 120:
+                raise RuntimeError("fake collective %s: peers missing" % name)
+            time.sleep(0.005)
 
     def unique_id():
         return b"\x01" * 128
@@ -32,23 +44,35 @@ def make(real_xg):
         def barrier(self):
             """XG_FAKE_BARRIER_DIR set: a real barrier across the job's processes (one
             marker file per rank and barrier); otherwise a no-op"""
+            trace.append(["barrier"])
             d = os.environ.get("XG_FAKE_BARRIER_DIR")
             if not d or self.nranks == 1:
                 return
             i = self._nbar
             self._nbar += 1
             open(os.path.join(d, "b%d_r%d" % (i, self.rank)), "w").close()
-            t0 = time.time()
-            while not all(os.path.exists(os.path.join(d, "b%d_r%d" % (i, r))) for r in range(self.nranks)):
-                if time.time() - t0 > 120:
-                    raise RuntimeError("fake barrier %d: peers missing" % i)
-                time.sleep(0.01)
+            _wait_all(d, "b%d_r%%d" % i, self.nranks)
 
         def device_sync(self):
             pass
 
         def allreduce_max(self, vals):
-            return list(vals)
+            """XG_FAKE_BARRIER_DIR set: a real MAX over the job's processes (one file per rank
+            and call), so every rank takes the same decisions as under RCCL"""
+            trace.append(["allreduce_max", len(vals)])
+            d = os.environ.get("XG_FAKE_BARRIER_DIR")
+            if not d or self.nranks == 1:
+                return list(vals)
+            i = self._nred = getattr(self, "_nred", -1) + 1
+            tmp = os.path.join(d, "a%d_r%d.tmp" % (i, self.rank))
+            with open(tmp, "w") as f:
+                json.dump(list(vals), f)
+            os.replace(tmp, os.path.join(d, "a%d_r%d" % (i, self.rank)))
+            _wait_all(d, "a%d_r%%d" % i, self.nranks)
+            got = [json.load(open(os.path.join(d, "a%d_r%d" % (i, r)))) for r in range(self.nranks)]
+            if any(len(x) != len(vals) for x in got):
+                raise RuntimeError("fake allreduce %d: ranks reduce different lengths" % i)
+            return [max(col) for col in zip(*got)]
 
         def info(self):
             return "gfx950:sramecc+:xnack-", 256, 309220868096
@@ -59,6 +83,7 @@ def make(real_xg):
         def ktime_begin(self, max_launches=4096, per_launch=True):
             self._kt = (max_launches, per_launch)
             calls["ktime"].append(self._kt)
+            trace.append(["ktime_begin", bool(per_launch)])
 
         def ktime_end(self):
             per_launch = self._kt[1]
@@ -69,6 +94,7 @@ def make(real_xg):
 
         def p2p_bench(self, nbytes, mode=0, reps=20):
             calls["p2p_bench"] += 1
+            trace.append(["p2p_bench", int(nbytes), int(mode), int(reps)])
             return 50.0, nbytes / 50e9
 
         def close(self):
@@ -78,7 +104,15 @@ def make(real_xg):
         def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None):
             self.ctx, self.sched, self.pack_max_seg = ctx, sched, pack_max_seg
             G, g = ctx.nranks, ctx.rank
+            if G > 1:     # as the real MethodRun: refuse calls RCCL would not pair
+                sched.check_pairing(G, pack_max_seg)
             self.view = sched.devplan(G, g, pack_max_seg)
+            # the RCCL calls this GPU's plan posts per run: per step its send/recv group and
+            # its barrier (xg_devplan_step_calls), as a signature the ranks must agree on in
+            # everything collective (the barriers) -- the p2p pairing is xg_devplans_match's
+            self.barrier_steps = [st for st in range(self.view.nsteps) if self.view.sync_after[st]]
+            self.key = [sched.method, sched.P, sched.A, sched.d, sched.c, sched.ntimes, pack_max_seg]
+            trace.append(["plan"] + self.key + [self.barrier_steps])
             self.nsteps = self.view.nsteps
             self.slots = sched.verify_slots(G, g)
             self.engine_workgroups = 0
@@ -90,6 +124,7 @@ def make(real_xg):
 
         def run_timed(self):
             calls["runs"] += 1
+            trace.append(["run"] + self.key)
             done = [1e-5 * (s + 1) for s in range(self.nsteps)]
             return done, [1e-6] * self.nsteps, done[-1] if done else 0.0
 
@@ -98,7 +133,7 @@ def make(real_xg):
             return [0] * n, [0] * n, [-1] * n
 
         def enqueue(self):
-            pass
+            trace.append(["enqueue"] + self.key)
 
         def check(self):
             pass

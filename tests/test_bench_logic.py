@@ -48,7 +48,13 @@ def test_bench_multi_gpu_rank0_line(world, tmp_path):
     assert out["roofline"] and out["roofline"]["bound"] == "hbm"
     assert set(out["pack_autotune_ms_per_run"]) == {"1", "2", "3", "4"}
     calls = json.loads([l for l in p.stdout.splitlines() if l.startswith("CALLS ")][0][6:])
-    assert calls["p2p"] == 1
+    sweep = out["xgmi"]["sweep"]          # the pt2pt_test analogue: 1 -> 0 latency + all pairs, 4 sizes
+    assert calls["p2p"] == 1 + len(sweep) == 9
+    assert [(r["mode"], r["bytes"]) for r in sweep] == [(m, b) for b in (4096, 65536, 1 << 20, 16 << 20)
+                                                        for m in ("one_way_1_to_0", "all_pairs")]
+    for r in sweep:
+        assert r["us_per_rep"] > 0 and r["reps"] >= 5
+        assert r["GBps"] > 0 if r["mode"] == "one_way_1_to_0" else r["GBps_aggregate"] == pytest.approx(r["GBps_per_gpu_egress_min"] * world, rel=1e-3)
     assert calls["ktime"] and calls["ktime"][0][1] is True      # N > 1: per-launch roofline pass
 
 

@@ -160,14 +160,14 @@ def test_step_engine_matches_per_step_launches(xg, ctx, method, d):
 
 
 ENGINE_MODES = {
-    "solo_armed": {},                                           # default at README sizes: 512 one-wave rails
-    "solo64_armed": {"XG_SOLO_RAILS": "64"},
+    "solo_armed": {"XG_ENGINE_ARM": "1"},                       # 512 one-wave rails, doorbell-armed
+    "solo64_armed": {"XG_SOLO_RAILS": "64", "XG_ENGINE_ARM": "1"},
     "solo37_launch": {"XG_SOLO_RAILS": "37", "XG_ENGINE_ARM": "0"},
-    "solo_norelay": {"XG_SOLO_RELAY": "0", "XG_SOLO_RAILS": "16"},   # every rail polls the doorbell
-    "wg_armed": {"XG_SOLO_WAVES": "16"},                        # 16 workgroup rails of 16 waves
+    "solo_norelay": {"XG_SOLO_RELAY": "0", "XG_SOLO_RAILS": "16", "XG_ENGINE_ARM": "1"},   # every rail polls
+    "wg_armed": {"XG_SOLO_WAVES": "16", "XG_ENGINE_ARM": "1"},  # 16 workgroup rails of 16 waves
     "wg1_launch": {"XG_SOLO_WAVES": "16", "XG_SOLO_RAILS": "1", "XG_ENGINE_ARM": "0"},
-    "grid_armed": {"XG_ENGINE_SOLO": "0"},
-    "solo_launch": {"XG_ENGINE_ARM": "0"},
+    "grid_armed": {"XG_ENGINE_SOLO": "0", "XG_ENGINE_ARM": "1"},
+    "solo_launch": {},                                          # the default: launched inside the timed region
     "grid_drain": {"XG_ENGINE_SOLO": "0", "XG_ENGINE_DRAIN": "1", "XG_ENGINE_ARM": "0"},
 }
 

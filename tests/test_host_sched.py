@@ -158,3 +158,24 @@ def test_pairwise_fast_form_equals_full_form(xg, method, P, A, d, k):
     for r in range(P):
         a, b = full.rank_timer(r, done).as_tuple(), fast.rank_timer(r, done).as_tuple()
         assert a == b, (r, a, b)
+
+
+@pytest.mark.parametrize("method", [9, 10])
+def test_pairwise_fast_form_trace_is_not_the_reference_trace(xg, method):
+    """XG_PAIRWISE_FAST=1 (the default above P = 1024) drops the 0-byte MPI_Sendrecv rounds, so
+    xg_sched_trace is then NOT the reference's call trace (include/xg_sched.h says so): pinned
+    here at the README size, where the full form reproduces the golden trace.  The fast trace
+    is exactly the reference trace's byte-carrying posts (a one-sided round becomes a single
+    blocking send or receive), with its own completion tokens."""
+    meta, traces, _ = load_golden("readme_p32_a14")
+    P, A = meta["P"], meta["A"]
+    full = _pairwise(xg, method, P, A, meta["d"], meta["ntimes"], fast=False)
+    fast = _pairwise(xg, method, P, A, meta["d"], meta["ntimes"], fast=True)
+    posts = lambda tr: [t for t in tr.split() if t[0] in "sir" and not t.endswith(":0")]
+    differs = 0
+    for r in range(P):
+        ref = traces[(method, r)]
+        assert full.trace(r) == ref
+        assert posts(fast.trace(r)) == posts(ref), r
+        differs += fast.trace(r) != ref
+    assert differs > 0

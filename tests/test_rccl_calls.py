@@ -1,0 +1,184 @@
+"""The RCCL calls of a multi-GPU job (libxghost calls.c) -- the code the driver's 8-GPU run
+executes and no one-GPU box can: what each GPU posts per step (xg_devplan_step_calls, the
+list enqueue_step posts) and whether RCCL pairs those calls step by step (xg_calls_match:
+per ordered GPU pair, the k-th send with the k-th receive over the whole run, as RCCL's
+per-peer FIFO does).  Every golden configuration x method, every BASELINE configuration,
+G = 2..8, direct and packed; bench.py's own call sequence (tuning passes included) on G
+processes; and the matcher's refusals."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO, golden_configs, load_golden
+
+CONFIGS = golden_configs()
+PACKS = (0, 4 << 20)          # direct (one call per segment) and the default packed plan
+
+
+def _ref_pairs(views):
+    """Independent restatement of the pairing, per step (tests/plan_exec.py's rule): in
+    each step, the k-th send of g to h with the k-th receive of h from g."""
+    G = len(views)
+    out = []
+    for st in range(views[0].nsteps):
+        calls = [v.calls(st) for v in views]
+        for g in range(G):
+            for h in range(G):
+                sends = [i for i, c in enumerate(calls[g]) if c[0] == 1 and c[1] == h]
+                recvs = [i for i, c in enumerate(calls[h]) if c[0] == 2 and c[1] == g]
+                assert len(sends) == len(recvs), (st, g, h)
+                b0, b1 = views[g].steps[st][2], views[h].steps[st][2]
+                for si, ri in zip(sends, recvs):
+                    assert calls[g][si][4] == calls[h][ri][4]
+                    out.append((st, g, h, b0 + si + sum(views[g].sync_after[:st]),
+                                b1 + ri + sum(views[h].sync_after[:st]), calls[g][si][4]))
+    return out
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_golden_jobs_pair_step_by_step(xg, cfg):
+    """every golden config x method x G = 2..8 x {direct, packed}: RCCL's whole-run FIFO
+    pairing puts every send and its receive in the same step, with the same length, and
+    every GPU ends the same steps with a barrier"""
+    meta, _, _ = load_golden(cfg)
+    rl = meta["aggregators"]
+    for m in meta["method_list"]:
+        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, ntimes=meta["ntimes"],
+                        proc_node=meta["proc_node"], barrier_type=meta["barrier"])
+        for G in range(2, min(8, meta["P"]) + 1):
+            for pack in PACKS:
+                n = s.check_pairing(G, pack)
+                views = [s.devplan(G, g, pack) for g in range(G)]
+                assert n == sum(1 for v in views for st in range(v.nsteps) for c in v.calls(st) if c[0] == 1)
+                assert all(v.sync_after == views[0].sync_after for v in views)
+
+
+@pytest.mark.parametrize("cfg", ["readme_p32_a14", "p16_a5_c3_b1", "p24_a7_t3_c1", "p8_a3_d1m_c2"])
+def test_pairs_equal_the_per_step_rule(xg, cfg):
+    """the C matcher's pairs = an independent per-step pairing, call for call; the step's
+    calls are its p2p list then the barrier; the pairs carry every cross-GPU byte"""
+    meta, _, _ = load_golden(cfg)
+    for m in meta["method_list"]:
+        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], meta["aggregators"], ntimes=meta["ntimes"],
+                        proc_node=meta["proc_node"], barrier_type=meta["barrier"])
+        for G in (2, 3, 8):
+            if G > meta["P"]:
+                continue
+            for pack in PACKS:
+                views = [s.devplan(G, g, pack) for g in range(G)]
+                for v in views:
+                    for st in range(v.nsteps):
+                        c = v.calls(st)
+                        qb, qc = v.steps[st][2], v.steps[st][3]
+                        assert [(x[1], x[0] == 1, x[2], x[3], x[4]) for x in c if x[0] != 3] == \
+                            [(o[0], bool(o[1]), o[2], o[3], o[4]) for o in v.p2p[qb:qb + qc]]
+                        assert [x[0] for x in c].count(3) == v.sync_after[st]
+                        assert all(x[0] != 3 for x in c[:-1])          # the barrier is the step's last call
+                pairs = xg.devplans_match(views)
+                assert pairs == _ref_pairs(views), (cfg, m, G, pack)
+                assert sum(p[5] for p in pairs) == sum(v.remote_send_bytes for v in views)
+
+
+# BASELINE.json configs[1..4] at full size (host plans only: nothing is allocated)
+BASELINE = [
+    ("configs1", 32, 14, 1 << 20, [200000000], (1, 2, 3, 4)),
+    ("configs2", 64, 16, 256 << 10, [200000000], (5, 8)),
+    ("configs3", 256, 32, 4 << 20, [200000000], (1, 2, 9, 10)),
+    ("configs4", 256, 64, 64 << 20, list(range(1, 9)), (7, 11, 12)),
+]
+
+
+@pytest.mark.parametrize("case", BASELINE, ids=[b[0] for b in BASELINE])
+def test_baseline_configs_pair_on_2_to_8_gpus(xg, case):
+    _, P, A, d, cs, methods = case
+    rl = xg.aggregator_list(P, A)
+    for m in methods:
+        for c in cs:
+            s = xg.Schedule(m, P, A, d, c, rl)
+            for G in (2, 3, 4, 8):
+                for pack in PACKS:
+                    assert s.check_pairing(G, pack) > 0
+
+
+# ---------------------------------------------------------------- the matcher's refusals
+S, R, B = 1, 2, 3
+
+
+def _refused(xg, calls, nsteps, what):
+    with pytest.raises(xg.XGError) as e:
+        xg.calls_match(calls, nsteps)
+    assert what in str(e.value), str(e.value)
+
+
+def test_matcher_accepts_and_orders_a_valid_job(xg):
+    calls = [[[(S, 1, 0, 0, 8), (R, 1, 1, 0, 4)], [(S, 1, 0, 8, 8), (B, -1, -1, 0, 0)]],
+             [[(S, 0, 0, 0, 4), (R, 0, 1, 0, 8)], [(R, 0, 1, 8, 8), (B, -1, -1, 0, 0)]]]
+    assert xg.calls_match(calls, 2) == [(0, 0, 1, 0, 1, 8), (0, 1, 0, 0, 1, 4), (1, 0, 1, 2, 2, 8)]
+
+
+def test_matcher_refuses_mismatches(xg):
+    # a send nobody receives
+    _refused(xg, [[[(S, 1, 0, 0, 8)]], [[]]], 1, "sends and 0 receives")
+    # equal counts per channel but the receive one step late: RCCL would pair them across steps
+    _refused(xg, [[[(S, 1, 0, 0, 8)], [(S, 1, 0, 8, 8)]], [[], [(R, 0, 1, 0, 8), (R, 0, 1, 8, 8)]]], 2,
+             "is posted in step 0, its receive in step 1")
+    # lengths differ
+    _refused(xg, [[[(S, 1, 0, 0, 8)]], [[(R, 0, 1, 0, 16)]]], 1, "carries 8 bytes, its receive 16")
+    # one GPU's in-loop barrier missing
+    _refused(xg, [[[(B, -1, -1, 0, 0)]], [[]]], 1, "GPU 0 ends with a barrier")
+    # a send posted after the step's barrier
+    _refused(xg, [[[(B, -1, -1, 0, 0), (S, 1, 0, 0, 8)]], [[(R, 0, 1, 0, 8), (B, -1, -1, 0, 0)]]], 1,
+             "after the step's barrier")
+    # per channel: the job's totals agree (3 sends, 3 receives) but GPU 1 takes one receive
+    # from GPU 0 for GPU 0's two sends
+    _refused(xg, [[[(S, 1, 0, 0, 8), (S, 1, 0, 8, 8)]], [[(R, 0, 1, 0, 8), (R, 2, 1, 8, 8), (R, 2, 1, 16, 8)]],
+                  [[(S, 1, 0, 0, 8)]]], 1, "posts 2 sends to GPU 1, which posts 1 receives")
+    # a peer out of range
+    _refused(xg, [[[(S, 5, 0, 0, 8)]], [[]]], 1, "to peer 5")
+
+
+# ---------------------------------------------------------------- bench.py's call sequence on G processes
+DRIVER = r'''
+import os, sys, json
+sys.path.insert(0, {repo!r}); sys.path.insert(0, os.path.join({repo!r}, "tests"))
+import __graft_entry__ as G
+import fake_xg
+real = G.load_package()
+fx = fake_xg.install(real)
+sys.argv = ["bench.py"] + {argv!r}
+import bench
+rc = bench.main()
+print("TRACE " + json.dumps(fx.trace))
+sys.exit(rc)
+'''
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_ranks_issue_the_same_collectives(tmp_path, world):
+    """bench.py as a G-process job (fake device layer whose barrier and MAX really span the
+    processes; REAL host plans): every rank issues the same sequence of barriers, MAX
+    reductions, RCCL ceiling runs and plan runs, tuning passes included -- the plans it runs
+    are refused up front unless their calls pair (check_pairing in MethodRun)."""
+    key = "calls_%s_%d" % (tmp_path.name, world)
+    argv = ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--watchdog", "200"]
+    code = DRIVER.format(repo=REPO, argv=argv)
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), XG_RDZV_KEY=key,
+                   XG_FAKE_BARRIER_DIR=str(tmp_path))
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    traces = [json.loads([l for l in o.splitlines() if l.startswith("TRACE ")][0][6:]) for o, _ in outs]
+    for r in range(1, world):
+        assert traces[r] == traces[0], "rank %d's collective sequence differs from rank 0's" % r
+    kinds = [t[0] for t in traces[0]]
+    assert kinds.count("plan") == 8               # 4 methods x {direct, packed} tuning candidates
+    assert "p2p_bench" in kinds and "allreduce_max" in kinds
+    line = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+    assert line["n_gpus"] == world and line["pack_autotune_ms_per_run"]
