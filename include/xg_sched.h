@@ -195,15 +195,21 @@ void xg_devplan_free(xg_devplan *p);
 /* ---------------------------------------------------------------- RCCL calls (calls.c)
  * The calls GPU dp->gpu posts in step `step`, in issue order: its send/recv calls
  * (one ncclGroupStart/End around them), then XG_CALL_BARRIER (one ncclAllReduce)
- * when the step ends in an in-loop MPI_Barrier.  The runtime posts exactly this
- * list (replaces the Issend/Irecv/Sendrecv/Alltoallw posts, mpi_test.c:1776,1790,
- * :551,558, :627,912).  Returns the count (out may be NULL), -1 for a bad step. */
+ * when the step ends in an in-loop MPI_Barrier.  self_max > 0: a step that posts
+ * cross-GPU calls and whose local gather/scatter copies move <= self_max bytes
+ * posts those copies inside the same group as self send/recv pairs (peer = dp->gpu,
+ * send then receive per copy; xg_devplan_step_self_calls counts them, 0 = the copies
+ * stay copy-kernel launches) -- one RCCL launch then carries the whole step.  The
+ * runtime posts exactly this list (replaces the Issend/Irecv/Sendrecv/Alltoallw
+ * posts, mpi_test.c:1776,1790, :551,558, :627,912).  Returns the count (out may be
+ * NULL), -1 for a bad step. */
 enum { XG_CALL_SEND = 1, XG_CALL_RECV = 2, XG_CALL_BARRIER = 3 };
 typedef struct {
     int32_t kind, peer, buf, pad;     /* peer: GPU; buf: region (XG_BUF_*) */
     int64_t off, len;
 } xg_call;
-int xg_devplan_step_calls(const xg_devplan *dp, int step, xg_call *out);
+int xg_devplan_step_calls(const xg_devplan *dp, int step, int64_t self_max, xg_call *out);
+int xg_devplan_step_self_calls(const xg_devplan *dp, int step, int64_t self_max);
 
 /* RCCL's pairing of the calls of a G-GPU job: per ordered GPU pair (src, dst), the
  * k-th send of src to dst with the k-th receive of dst from src, in issue order
@@ -221,9 +227,10 @@ typedef struct {
 } xg_call_pair;
 int64_t xg_calls_match(int ngpus, int nsteps, const xg_call *const *calls, const int32_t *const *step_begin,
                        xg_call_pair *out, int64_t max_pairs, char *err, size_t errlen);
-/* The same over the G device plans of one job (plans[g]: GPU g's, same schedule). */
-int64_t xg_devplans_match(const xg_devplan *const *plans, int ngpus, xg_call_pair *out, int64_t max_pairs,
-                          char *err, size_t errlen);
+/* The same over the G device plans of one job (plans[g]: GPU g's, same schedule), their
+ * calls listed with self_max as xg_devplan_step_calls lists them. */
+int64_t xg_devplans_match(const xg_devplan *const *plans, int ngpus, int64_t self_max, xg_call_pair *out,
+                          int64_t max_pairs, char *err, size_t errlen);
 
 /* Step engine ordering (xg.h xg_plan_engine; kernels.h step_engine_kernel).  The
  * transfers of step s are xfer[step_begin[s] .. step_begin[s+1]) (device addresses

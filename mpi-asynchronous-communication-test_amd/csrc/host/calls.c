@@ -2,8 +2,9 @@
  * calls.c -- the RCCL calls of a device plan, and how RCCL pairs them across GPUs.
  *
  * xg_devplan_step_calls is THE definition of what GPU g posts in step s: one
- * ncclGroupStart/End around its send/recv calls (in this order), then one
- * ncclAllReduce when the step ends in an in-loop MPI_Barrier.  The real
+ * ncclGroupStart/End around its send/recv calls (in this order; with self_max > 0
+ * a cross-GPU step's small local part joins them as self send/recv pairs), then
+ * one ncclAllReduce when the step ends in an in-loop MPI_Barrier.  The real
  * multi-GPU path of the runtime (xg_runtime.hip, enqueue_step) posts exactly
  * that list; the one-device virtual runner (xg_vplans_run / _rccl) moves exactly
  * the pairs xg_calls_match makes of every GPU's lists.
@@ -27,7 +28,36 @@
 #include <stdlib.h>
 #include <string.h>
 
-int xg_devplan_step_calls(const xg_devplan *dp, int step, xg_call *out)
+/* the step's local gather/scatter copies: pre copies after the stage copies, before the packs */
+static void local_range(const xg_devplan *dp, const xg_stepplan *sp, int *b, int *e, int64_t *bytes)
+{
+    int i;
+    *b = sp->pre_begin + sp->stage_count;
+    *e = *b;
+    *bytes = 0;
+    for (i = sp->stage_count; i < sp->pre_count; ++i) {
+        const xg_copy *c = &dp->copies[sp->pre_begin + i];
+        if (c->dst_buf == XG_BUF_STAGE_SEND) break;
+        *e = sp->pre_begin + i + 1;
+        *bytes += c->len > 0 ? c->len : 0;
+    }
+}
+
+int xg_devplan_step_self_calls(const xg_devplan *dp, int step, int64_t self_max)
+{
+    int b, e, i, n = 0;
+    int64_t bytes;
+    const xg_stepplan *sp;
+    if (!dp || step < 0 || step >= dp->nsteps || self_max <= 0) return 0;
+    sp = &dp->steps[step];
+    if (!sp->p2p_count) return 0;
+    local_range(dp, sp, &b, &e, &bytes);
+    if (bytes > self_max) return 0;
+    for (i = b; i < e; ++i) n += dp->copies[i].len > 0;
+    return n;
+}
+
+int xg_devplan_step_calls(const xg_devplan *dp, int step, int64_t self_max, xg_call *out)
 {
     const xg_stepplan *sp;
     int i, n = 0;
@@ -42,6 +72,25 @@ int xg_devplan_step_calls(const xg_devplan *dp, int step, xg_call *out)
         out[n].pad = 0;
         out[n].off = o->off;
         out[n].len = o->len;
+    }
+    if (xg_devplan_step_self_calls(dp, step, self_max)) {
+        /* the step's local copies as self send + receive pairs inside its group: one RCCL
+         * launch carries the whole step (RCCL pairs the k-th self send with the k-th self
+         * receive, so each pair is one copy) */
+        int b, e;
+        int64_t bytes;
+        local_range(dp, sp, &b, &e, &bytes);
+        for (i = b; i < e; ++i) {
+            const xg_copy *c = &dp->copies[i];
+            if (c->len <= 0) continue;
+            if (out) {
+                out[n].kind = XG_CALL_SEND; out[n].peer = dp->gpu; out[n].buf = c->src_buf; out[n].pad = 0;
+                out[n].off = c->src_off; out[n].len = c->len;
+                out[n + 1].kind = XG_CALL_RECV; out[n + 1].peer = dp->gpu; out[n + 1].buf = c->dst_buf;
+                out[n + 1].pad = 0; out[n + 1].off = c->dst_off; out[n + 1].len = c->len;
+            }
+            n += 2;
+        }
     }
     if (sp->sync_after) {
         if (out) {
@@ -220,8 +269,8 @@ done:
     return rc;
 }
 
-int64_t xg_devplans_match(const xg_devplan *const *plans, int ngpus, xg_call_pair *out, int64_t max_pairs, char *err,
-                          size_t errlen)
+int64_t xg_devplans_match(const xg_devplan *const *plans, int ngpus, int64_t self_max, xg_call_pair *out,
+                          int64_t max_pairs, char *err, size_t errlen)
 {
     const int G = ngpus;
     int g, s, nsteps;
@@ -248,12 +297,12 @@ int64_t xg_devplans_match(const xg_devplan *const *plans, int ngpus, xg_call_pai
         if (!sb[g]) goto done;
         for (s = 0; s < nsteps; ++s) {
             sb[g][s] = n;
-            n += xg_devplan_step_calls(plans[g], s, NULL);
+            n += xg_devplan_step_calls(plans[g], s, self_max, NULL);
         }
         sb[g][nsteps] = n;
         calls[g] = (xg_call *)malloc(sizeof(xg_call) * ((size_t)n + 1));
         if (!calls[g]) goto done;
-        for (s = 0; s < nsteps; ++s) xg_devplan_step_calls(plans[g], s, calls[g] + sb[g][s]);
+        for (s = 0; s < nsteps; ++s) xg_devplan_step_calls(plans[g], s, self_max, calls[g] + sb[g][s]);
     }
     rc = xg_calls_match(G, nsteps, (const xg_call *const *)calls, (const int32_t *const *)sb, out, max_pairs, err,
                         errlen);

@@ -34,7 +34,7 @@ static int pairing_ok(const xg_sched *s, int G, int64_t pack_max_seg, char *err,
     char why[400];
     if (!plans) return 0;
     for (g = 0; g < G; ++g) plans[g] = xg_devplan_build(s, G, g, pack_max_seg);
-    if (xg_devplans_match((const xg_devplan *const *)plans, G, NULL, 0, why, sizeof why) >= 0) ok = 1;
+    if (xg_devplans_match((const xg_devplan *const *)plans, G, 0, NULL, 0, why, sizeof why) >= 0) ok = 1;
     else snprintf(err, errlen, "the GPUs' RCCL calls do not pair: %s", why);
     for (g = 0; g < G; ++g) xg_devplan_free(plans[g]);
     free(plans);

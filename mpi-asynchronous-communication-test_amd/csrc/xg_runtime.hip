@@ -112,11 +112,14 @@ struct xg_ctx {
     int solo_waves;            // waves per rail: 16 (a workgroup) or 1
     int solo_min_steps;        // a whole plan of fewer steps stays a copy launch
     int64_t launch_max;        // copy launches above this many bytes go as back-to-back launches of ~this size
+    int min_wg;                // a copy launch of fewer bytes than min_wg x chunk gets smaller pieces (>= 4 KiB)
     int solo_relay;            // armed solo: rail 0 alone polls the doorbell and relays the ring
     int step_chain;            // 1: time runs of one-launch local steps by in-kernel stamps (xg_plan_run)
     int piece_order;           // local pieces of a launch: 0 message order, 1 by destination, 2 by source
     int engine_arm;            // 1: xg_plan_run arms single-segment plans (doorbell)
     int split_local;           // 1: a cross-GPU step's local gather runs on the side stream
+    int64_t split_min;         // ... when it moves >= this many bytes (smaller: in the pack / fused launch)
+    int64_t self_max;          // a cross-GPU step's local part of <= this many bytes goes in its RCCL group
     int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
@@ -152,6 +155,8 @@ struct StepR {
     int pre_n;                       // local_n + pack_n
     int64_t stage_bytes, local_bytes, pack_bytes, post_bytes;   // bytes copied by each part (read + written once)
     bool split, fused, deferred;
+    bool self_local;                 // the local copies travel in the RCCL group as self send/recv (XG_SELF_MAX)
+    bool fused_local;                // fused, and the local copies join that launch (small, hazard-free)
 };
 
 // A run of >= 2 consecutive GPU-local steps (no RCCL op, no in-loop barrier, no
@@ -350,6 +355,12 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     if (env && atoi(env) > 0) c->solo_rails = std::min(atoi(env), xgk::kSoloMaxRails);
     env = getenv("XG_COPY_LAUNCH_MAX");      // bytes; 0 = one launch however large
     c->launch_max = env ? atoll(env) : (int64_t)512 << 20;
+    {
+        int cus = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        env = getenv("XG_COPY_MIN_WG");       // 0: always chunk-sized pieces
+        c->min_wg = env ? atoi(env) : 2 * cus;
+    }
     env = getenv("XG_SOLO_MIN_STEPS");       // plans of fewer steps never run as an armed solo launch
     c->solo_min_steps = env ? atoi(env) : 1;  // profiles/r02/one_step/: armed beats the event-timed launch
     env = getenv("XG_PIECE_ORDER");          // profiles/r02/piece_order/: by destination is fastest
@@ -365,6 +376,10 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->engine_arm = env && !strcmp(env, "1");
     env = getenv("XG_SPLIT_LOCAL");          // "0": local gather + packs in one launch
     c->split_local = !(env && !strcmp(env, "0"));
+    env = getenv("XG_SPLIT_MIN");            // bytes: a smaller local part is not split off
+    c->split_min = env ? atoll(env) : 0;
+    env = getenv("XG_SELF_MAX");             // bytes: local part posted as self send/recv (0: never)
+    c->self_max = env ? atoll(env) : 0;
     env = getenv("XG_FUSE_UNPACK");          // "0": unpacks and the next step's packs apart
     c->fuse_unpack = !(env && !strcmp(env, "0"));
     {
@@ -995,6 +1010,33 @@ static int run_displ_scan(xg_plan *p, DisplScan &ds)
 extern "C" int xg_plan_free(xg_plan *p);
 static int launch_dispatches(const xg_plan *p, int b, int n, int64_t bytes);
 
+// Does any local copy of step s read or write bytes that step s-1's unpacks write?  (Then
+// they cannot share one launch: its workgroups run in any order.)  Intervals per region.
+static bool touches_unpacked(const xg_devplan *dp, int s)
+{
+    const xg_stepplan &pv = dp->steps[s - 1], &sp = dp->steps[s];
+    std::vector<std::pair<int64_t, int64_t>> w[XG_NBUF];      // unpack destinations [off, end)
+    for (int i = 0; i < pv.post_count; ++i) {
+        const xg_copy &c = dp->copies[pv.post_begin + i];
+        if (c.len > 0) w[c.dst_buf].push_back({c.dst_off, c.dst_off + c.len});
+    }
+    for (auto &v : w) std::sort(v.begin(), v.end());
+    auto hit = [&](int buf, int64_t a, int64_t b) {
+        const auto &v = w[buf];
+        auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(b, (int64_t)0));
+        // intervals starting before b: the one just before may reach past a (they do not
+        // overlap each other: every unpack writes its own slot)
+        return it != v.begin() && std::prev(it)->second > a;
+    };
+    for (int i = sp.stage_count; i < sp.pre_count; ++i) {
+        const xg_copy &c = dp->copies[sp.pre_begin + i];
+        if (c.dst_buf == XG_BUF_STAGE_SEND) break;
+        if (c.len > 0 && (hit(c.src_buf, c.src_off, c.src_off + c.len) || hit(c.dst_buf, c.dst_off, c.dst_off + c.len)))
+            return true;
+    }
+    return false;
+}
+
 // Device half of a plan load: the piece table, the step events, the displacement scan
 // and the engine segments.  On an error the caller frees the plan (xg_plan_free takes a
 // half-loaded one: every handle starts null).
@@ -1042,7 +1084,20 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
     // pieces for small launches were measured no faster, and slower where they stop
     // dividing the segment size (profiles/r01_min_pieces_ab.txt)
-    const int64_t chunk = c->chunk;
+    // bytes per piece = per workgroup: c->chunk (32 KiB), or less for a launch too small to
+    // spread over min_wg workgroups -- a 4 MiB gather as 128 pieces of 32 KiB kept half the
+    // CUs idle (1.4 TB/s, profiles/r02/pack_virtual.txt); pieces stay >= 4 KiB, 16-B multiples
+    int64_t chunk = c->chunk;
+    auto launch_chunk = [&](int64_t bytes) {
+        chunk = c->chunk;
+        if (c->min_wg > 0 && bytes > 0 && bytes < (int64_t)c->min_wg * chunk)
+            chunk = std::min(c->chunk, std::max<int64_t>(4096, (bytes / c->min_wg + 15) & ~(int64_t)15));
+    };
+    auto copy_bytes = [&](int b, int n) {
+        int64_t t = 0;
+        for (int i = 0; i < n; ++i) t += std::max<int64_t>(0, dp->copies[b + i].len);
+        return t;
+    };
     std::vector<xgk::DCopy> pieces;
     DisplScan ds;
     int rc;
@@ -1086,13 +1141,14 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             if (dp->copies[sp.post_begin + i].src_buf != XG_BUF_STAGE_RECV) goto bad;   // post copies unpack
         {
             // the step's RCCL calls: exactly what libxghost says this GPU posts (calls.c)
-            const int nc = xg_devplan_step_calls(dp, s, nullptr);
+            const int nc = xg_devplan_step_calls(dp, s, c->self_max, nullptr);
             if (nc < 0) goto bad;
+            st.self_local = xg_devplan_step_self_calls(dp, s, c->self_max) > 0;
             st.call_b = (int)p->calls.size();
             st.call_n = nc;
             p->call_begin.push_back(st.call_b);
             p->calls.resize(st.call_b + nc);
-            xg_devplan_step_calls(dp, s, p->calls.data() + st.call_b);
+            xg_devplan_step_calls(dp, s, c->self_max, p->calls.data() + st.call_b);
             st.p2p_n = 0;
             st.sync_after = 0;
             for (int i = 0; i < nc; ++i) {
@@ -1102,16 +1158,27 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
                     continue;
                 }
                 if ((o.kind != XG_CALL_SEND && o.kind != XG_CALL_RECV) || o.peer < 0 || o.peer >= c->nranks ||
-                    o.peer == c->rank || o.buf < 0 || o.buf >= XG_NBUF || o.off < 0 || o.len < 0 ||
-                    o.off + o.len > r->bytes[o.buf])
+                    (o.peer == c->rank && !st.self_local) || o.buf < 0 || o.buf >= XG_NBUF || o.off < 0 ||
+                    o.len < 0 || o.off + o.len > r->bytes[o.buf])
                     goto bad;
                 st.p2p_n++;
             }
         }
-        st.split = c->split_local && st.p2p_n > 0 && nloc > 0;
+        if (st.self_local) nloc = 0;        // the local copies travel in the step's RCCL group
+        int64_t b_loc = 0;
+        for (int i = sp.stage_count; i < sp.pre_count; ++i)
+            if (dp->copies[sp.pre_begin + i].dst_buf != XG_BUF_STAGE_SEND && !st.self_local)
+                b_loc += std::max<int64_t>(0, dp->copies[sp.pre_begin + i].len);
+        // a cross-GPU step's local part runs on the side stream beside the packs and the RCCL
+        // group (split) when it is large enough to pay for the fork / join; a smaller one joins
+        // the step's first launch -- the fused one too, if it touches none of the bytes the
+        // previous step's unpacks write (then the step is ONE copy launch + its RCCL group)
+        st.split = c->split_local && st.p2p_n > 0 && nloc > 0 && b_loc >= c->split_min;
         st.deferred = false;
-        st.fused = c->fuse_unpack && s > 0 && npack > 0 && sp.stage_count == 0 && (st.split || nloc == 0) &&
-                   !p->steps[s - 1].sync_after && dp->steps[s - 1].post_count > 0;
+        const bool prev_ok = c->fuse_unpack && s > 0 && npack > 0 && sp.stage_count == 0 &&
+                             !p->steps[s - 1].sync_after && dp->steps[s - 1].post_count > 0;
+        st.fused = prev_ok && (st.split || nloc == 0 || !touches_unpacked(dp, s));
+        st.fused_local = st.fused && !st.split && nloc > 0;
         if (st.fused) p->steps[s - 1].deferred = true;
     }
     p->call_begin.push_back((int32_t)p->calls.size());
@@ -1125,7 +1192,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             for (int i = b; i < (int)pieces.size(); ++i) n += pieces[i].len;
             return n;
         };
-        auto add_post = [&](int t) -> bool {
+        auto add_post = [&](int t) -> bool {      // (chunk set by the caller for its launch)
             const xg_stepplan &tp = dp->steps[t];
             StepR &tt = p->steps[t];
             tt.post_b = (int)pieces.size();
@@ -1136,23 +1203,41 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             tt.post_bytes = span(tt.post_b);
             return true;
         };
+        // each launch's pieces cut for that launch's bytes (launch_chunk): stage | local (+ packs,
+        // unless split) | [previous unpacks +] packs | unpacks
+        int first_pack = sp.pre_count;
+        for (int i = sp.stage_count; i < sp.pre_count; ++i)
+            if (dp->copies[sp.pre_begin + i].dst_buf == XG_BUF_STAGE_SEND) {
+                first_pack = i;
+                break;
+            }
+        const int64_t b_local = copy_bytes(sp.pre_begin + sp.stage_count, first_pack - sp.stage_count);
+        const int64_t b_pack = copy_bytes(sp.pre_begin + first_pack, sp.pre_count - first_pack);
+        const int64_t b_prev = st.fused ? copy_bytes(dp->steps[s - 1].post_begin, dp->steps[s - 1].post_count) : 0;
+        launch_chunk(copy_bytes(sp.pre_begin, sp.stage_count));
         st.stage_b = (int)pieces.size();
         for (int i = 0; i < sp.stage_count; ++i)
             if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
         st.stage_n = (int)pieces.size() - st.stage_b;
         st.stage_bytes = span(st.stage_b);
-        st.local_b = (int)pieces.size();
-        int first_pack = sp.pre_count;
-        for (int i = sp.stage_count; i < sp.pre_count; ++i) {
-            if (dp->copies[sp.pre_begin + i].dst_buf == XG_BUF_STAGE_SEND) {
-                first_pack = i;
-                break;
-            }
-            if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
+        // piece order: stage | local | [previous unpacks] | packs (split or not fused), or
+        // stage | previous unpacks | local | packs (fused_local: one launch over all three)
+        const int64_t b_own = st.self_local ? 0 : b_local;
+        if (st.fused_local) {
+            launch_chunk(b_prev + b_own + b_pack);
+            if (!add_post(s - 1)) goto bad;
+        } else {
+            launch_chunk(st.split ? b_own : b_own + b_pack);
         }
+        st.local_b = (int)pieces.size();
+        for (int i = sp.stage_count; i < first_pack && !st.self_local; ++i)
+            if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
         st.local_n = (int)pieces.size() - st.local_b;
         st.local_bytes = span(st.local_b);
-        if (st.fused && !add_post(s - 1)) goto bad;
+        if (!st.fused_local) {
+            if (st.split || st.fused) launch_chunk(b_prev + b_pack);
+            if (st.fused && !add_post(s - 1)) goto bad;
+        }
         st.pack_b = (int)pieces.size();
         for (int i = first_pack; i < sp.pre_count; ++i)
             if (!add(dp->copies[sp.pre_begin + i], 0)) goto bad;
@@ -1163,6 +1248,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.post_b = (int)pieces.size();
         st.post_n = 0;
         st.post_bytes = 0;
+        launch_chunk(copy_bytes(sp.post_begin, sp.post_count));
         if (!st.deferred && !add_post(s)) goto bad;
     }
     // order of a launch's local pieces (workgroup i copies piece i): by destination address
@@ -1215,7 +1301,8 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         p->nlaunch += D(st.stage_b, st.stage_n, st.stage_bytes);
         if (st.fused) {
             const StepR &pv = p->steps[s - 1];
-            p->nlaunch += D(pv.post_b, pv.post_n + st.pack_n, pv.post_bytes + st.pack_bytes);
+            p->nlaunch += D(pv.post_b, pv.post_n + (st.fused_local ? st.local_n : 0) + st.pack_n,
+                            pv.post_bytes + (st.fused_local ? st.local_bytes : 0) + st.pack_bytes);
         }
         if (st.split)
             p->nlaunch += D(st.local_b, st.local_n, st.local_bytes) + (st.fused ? 0 : D(st.pack_b, st.pack_n, st.pack_bytes));
@@ -1435,9 +1522,11 @@ static int enqueue_pre(xg_plan *p, int s, hipStream_t stream, hipStream_t side)
     int rc;
     if (st.stage_n && (rc = timed_copy(p, st.stage_b, st.stage_n, st.stage_bytes, stream, true))) return rc;
     if (st.fused) {
+        // the previous step's unpacks, [this step's local copies,] this step's packs: one launch
         const StepR &pv = p->steps[s - 1];
-        if ((rc = timed_copy(p, pv.post_b, pv.post_n + st.pack_n, pv.post_bytes + st.pack_bytes, stream, true)))
-            return rc;
+        const int n = pv.post_n + (st.fused_local ? st.local_n : 0) + st.pack_n;
+        const int64_t b = pv.post_bytes + (st.fused_local ? st.local_bytes : 0) + st.pack_bytes;
+        if ((rc = timed_copy(p, pv.post_b, n, b, stream, true))) return rc;
         if (p->rec_ev) HIPCHK(hipEventRecord(p->ev[s - 1], stream));
     }
     if (st.split) {

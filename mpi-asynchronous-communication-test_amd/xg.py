@@ -148,13 +148,14 @@ def host():
         h.xg_devplan_build.restype = C.POINTER(DevPlan)
         h.xg_devplan_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64]
         h.xg_devplan_free.argtypes = [C.POINTER(DevPlan)]
-        h.xg_devplan_step_calls.argtypes = [C.POINTER(DevPlan), C.c_int, C.POINTER(Call)]
+        h.xg_devplan_step_calls.argtypes = [C.POINTER(DevPlan), C.c_int, C.c_int64, C.POINTER(Call)]
+        h.xg_devplan_step_self_calls.argtypes = [C.POINTER(DevPlan), C.c_int, C.c_int64]
         h.xg_calls_match.restype = C.c_int64
         h.xg_calls_match.argtypes = [C.c_int, C.c_int, C.POINTER(C.POINTER(Call)), C.POINTER(C.POINTER(C.c_int32)),
                                      C.POINTER(CallPair), C.c_int64, C.c_char_p, C.c_size_t]
         h.xg_devplans_match.restype = C.c_int64
-        h.xg_devplans_match.argtypes = [C.POINTER(C.POINTER(DevPlan)), C.c_int, C.POINTER(CallPair), C.c_int64,
-                                        C.c_char_p, C.c_size_t]
+        h.xg_devplans_match.argtypes = [C.POINTER(C.POINTER(DevPlan)), C.c_int, C.c_int64, C.POINTER(CallPair),
+                                        C.c_int64, C.c_char_p, C.c_size_t]
         h.xg_fill_runs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(SegRun)]
         h.xg_verify_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(Slot)]
         h.xg_engine_hazards.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int)]
@@ -258,18 +259,19 @@ def calls_match(calls, nsteps):
     return _pairs(n, out)
 
 
-def devplans_match(plans):
+def devplans_match(plans, self_max=0):
     """xg_devplans_match over the G device plans (DevicePlanView or raw POINTER(DevPlan)) of one
-    job: the pairs, or XGError naming the first call that RCCL would pair differently."""
+    job (calls listed with self_max): the pairs, or XGError naming the first call that RCCL
+    would pair differently."""
     ptrs = [p.ptr if isinstance(p, DevicePlanView) else p for p in plans]
     G = len(ptrs)
     arr = (C.POINTER(DevPlan) * G)(*ptrs)
     err = C.create_string_buffer(512)
-    n = host().xg_devplans_match(arr, G, None, 0, err, 512)
+    n = host().xg_devplans_match(arr, G, self_max, None, 0, err, 512)
     if n < 0:
         raise XGError(err.value.decode())
     out = (CallPair * max(1, n))()
-    host().xg_devplans_match(arr, G, out, n, err, 512)
+    host().xg_devplans_match(arr, G, self_max, out, n, err, 512)
     return _pairs(n, out)
 
 
@@ -376,7 +378,7 @@ class Schedule:
         try:
             arr = (C.POINTER(DevPlan) * ngpus)(*plans)
             err = C.create_string_buffer(512)
-            n = h.xg_devplans_match(arr, ngpus, None, 0, err, 512)
+            n = h.xg_devplans_match(arr, ngpus, 0, None, 0, err, 512)
             if n < 0:
                 raise XGError("method %d on %d GPUs: RCCL calls do not pair: %s"
                               % (self.method, ngpus, err.value.decode()))
@@ -421,11 +423,11 @@ class DevicePlanView:
     def ptr(self):
         return self._p
 
-    def calls(self, step):
+    def calls(self, step, self_max=0):
         """xg_devplan_step_calls: [(kind, peer, buf, off, len)] this GPU posts in `step`"""
-        n = host().xg_devplan_step_calls(self._p, step, None)
+        n = host().xg_devplan_step_calls(self._p, step, self_max, None)
         arr = (Call * max(1, n))()
-        host().xg_devplan_step_calls(self._p, step, arr)
+        host().xg_devplan_step_calls(self._p, step, self_max, arr)
         return [(c.kind, c.peer, c.buf, c.off, c.len) for c in arr[:n]]
 
     def __del__(self):

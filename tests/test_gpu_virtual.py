@@ -114,3 +114,46 @@ def test_config2_full_size_through_rccl(xg, worlds, G, method):
         assert all(nb == 0 for _slot, _ck, nb, _fb in res), (method, G, pack)
         for (src, seed, _dst, _off), ck, _nb, _fb in res[:: max(1, len(res) // 6)]:
             assert ck == O.chk64(O.fingerprint(1, src, seed, it, d)), (method, G, pack, src, seed)
+
+
+STEP_FORMS = {
+    "self_in_group": {"XG_SELF_MAX": str(1 << 30)},          # local part as self send/recv in the RCCL group
+    "local_in_fused": {"XG_SPLIT_MIN": str(1 << 40)},        # local part in the (fused) pack launch
+}
+
+
+@pytest.mark.parametrize("form", list(STEP_FORMS))
+@pytest.mark.parametrize("rccl", [False, True])
+@pytest.mark.parametrize("G", (2, 8))
+def test_cross_gpu_step_forms(xg, form, rccl, G):
+    """The two cheaper forms of a cross-GPU step (one launch fewer than the split local
+    gather + its fork/join): every method, packed and direct, collision-free fingerprint,
+    unaligned d, every slot against the oracle."""
+    import os
+    import xg_oracle as O
+    env = STEP_FORMS[form]
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        ctxs = [xg.Context.virtual(g, G, device=0) for g in range(G)]
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        P, A, d, c, k, it = 20, 6, 1000, 7, 2, 3
+        rl = xg.aggregator_list(P, A)
+        for method in range(1, 21):
+            s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2, iteration=it)
+            exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
+            for pack in (0, 1 << 20):
+                res = _run_job(xg, ctxs, s, it, 1, pack, rccl=rccl)
+                for (src, seed, dst, off), ck, nb, _fb in res:
+                    assert nb == 0, (form, method, G, pack, src, dst)
+                    local = off - s.recv_offset(G, dst)
+                    assert ck == O.chk64(exp[dst][local: local + d]), (form, method, G, pack, src, dst)
+    finally:
+        for cx in ctxs:
+            cx.close()

@@ -182,3 +182,35 @@ def test_bench_ranks_issue_the_same_collectives(tmp_path, world):
     assert "p2p_bench" in kinds and "allreduce_max" in kinds
     line = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
     assert line["n_gpus"] == world and line["pack_autotune_ms_per_run"]
+
+
+@pytest.mark.parametrize("cfg", ["readme_p32_a14", "p20_a6_c7", "p16_a4_t2_c5"])
+def test_self_calls_carry_the_local_part(xg, cfg):
+    """XG_SELF_MAX: a cross-GPU step whose local copies move <= self_max bytes lists them as
+    self send + receive pairs (peer = its own GPU) after its cross-GPU calls, before the
+    barrier; the job still pairs step by step, and the self pairs are exactly those copies"""
+    meta, _, _ = load_golden(cfg)
+    for m in meta["method_list"]:
+        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], meta["aggregators"], ntimes=meta["ntimes"],
+                        proc_node=meta["proc_node"], barrier_type=meta["barrier"])
+        for G in (2, 8):
+            for pack in PACKS:
+                views = [s.devplan(G, g, pack) for g in range(G)]
+                pairs = xg.devplans_match(views, self_max=1 << 30)
+                cross = xg.devplans_match(views)
+                assert [(p[0], p[1], p[2], p[5]) for p in pairs if p[1] != p[2]] == \
+                    [(p[0], p[1], p[2], p[5]) for p in cross]
+                for g, v in enumerate(views):
+                    for st in range(v.nsteps):
+                        c = v.calls(st, self_max=1 << 30)
+                        own = [x for x in c if x[0] != 3 and x[1] == g]
+                        pb, pc = v.steps[st][0], v.steps[st][1]
+                        sc = v.stage_count[st]
+                        local = [cp for cp in v.copies[pb + sc: pb + pc] if cp[2] != 2 and cp[4] > 0]
+                        if not v.steps[st][3]:              # no cross-GPU call: nothing moves into a group
+                            assert not own
+                            continue
+                        assert [(x[0], x[2], x[3], x[4]) for x in own] == \
+                            [t for cp in local for t in ((1, cp[0], cp[1], cp[4]), (2, cp[2], cp[3], cp[4]))]
+                        assert [x for x in c if x[0] == 3 or x[1] != g] == v.calls(st)   # cross calls + barrier as before
+                        assert not own or c.index(own[0]) == len(v.calls(st)) - v.sync_after[st]   # after the cross calls
