@@ -121,6 +121,7 @@ struct xg_ctx {
     int64_t split_min;         // ... when it moves >= this many bytes (smaller: in the pack / fused launch)
     int64_t self_max;          // a cross-GPU step's local part of <= this many bytes goes in its RCCL group
     int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
+    int graph;                 // 1: multi-step runs are captured once into a hipGraph and replayed (XG_GRAPH)
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
     int64_t nt_min;         // variant 0: launches moving >= this many bytes use non-temporal loads/stores
@@ -222,7 +223,48 @@ struct xg_plan {
     std::vector<int> chain_end;
     unsigned long long *d_cstamp;  // nsteps wall-clock stamps of chained steps
     std::vector<int64_t> plen;     // prefix sums of the piece lengths (npieces + 1), host side
+    // hipGraph replay (XG_GRAPH=1): the launches of one xg_plan_enqueue / one timed xg_plan_run,
+    // captured at first use and replayed after (a launch-bound multi-step run then costs one
+    // graph launch of host time instead of a launch, an event and an RCCL group per step)
+    hipGraphExec_t g_enq, g_run;
+    uint64_t id;                   // unique per loaded plan (keys the virtual runner's graphs)
+    struct VGraph {
+        std::vector<uint64_t> ids;
+        bool rccl;
+        hipGraphExec_t exec;
+    } vg;                          // plans[0] of a virtual job: the job's captured run
 };
+
+static uint64_t next_plan_id()
+{
+    static uint64_t n = 0;
+    return __atomic_add_fetch(&n, 1, __ATOMIC_RELAXED);
+}
+
+// Capture what `body` enqueues on `stream` into a graph and instantiate it.  The stream
+// leaves capture mode on every path; on failure nothing is kept.
+template <class F>
+static int capture(hipStream_t stream, hipGraphExec_t *out, F body)
+{
+    *out = nullptr;
+    HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    const int rc = body();
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(stream, &g);
+    if (rc || e != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        if (!rc) fprintf(stderr, "xg: hipStreamEndCapture: %s\n", hipGetErrorString(e));
+        return rc ? rc : XG_EHIP;
+    }
+    const hipError_t ie = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ie != hipSuccess) {
+        *out = nullptr;
+        fprintf(stderr, "xg: hipGraphInstantiate: %s\n", hipGetErrorString(ie));
+        return XG_EHIP;
+    }
+    return XG_OK;
+}
 
 // The copy kernel variant of a launch moving `bytes` (launch_copy).  Variant 0 picks
 // non-temporal loads/stores (6) when the bytes cannot come back from the 256 MiB
@@ -382,6 +424,8 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->self_max = env ? atoll(env) : 0;
     env = getenv("XG_FUSE_UNPACK");          // "0": unpacks and the next step's packs apart
     c->fuse_unpack = !(env && !strcmp(env, "0"));
+    env = getenv("XG_GRAPH");                // "1": replay captured runs (hipGraph)
+    c->graph = env && !strcmp(env, "1");
     {
         int khz = 0;
         HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
@@ -1081,6 +1125,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->d_pieces = nullptr; p->d_sb = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->d_disp = nullptr;
     p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
     p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1; p->d_cstamp = nullptr;
+    p->g_enq = p->g_run = nullptr; p->id = next_plan_id(); p->vg.rccl = false; p->vg.exec = nullptr;
     // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
     // pieces for small launches were measured no faster, and slower where they stop
     // dividing the segment size (profiles/r01_min_pieces_ab.txt)
@@ -1375,6 +1420,8 @@ extern "C" int xg_plan_free(xg_plan *p)
     for (auto &e : p->fork) if (e) keep(hipEventDestroy(e));
     for (auto &e : p->join) if (e) keep(hipEventDestroy(e));
     if (p->ev0) keep(hipEventDestroy(p->ev0));
+    for (hipGraphExec_t g : {p->g_enq, p->g_run, p->vg.exec})
+        if (g) keep(hipGraphExecDestroy(g));
     delete p;
     if (first != hipSuccess) {
         fprintf(stderr, "xg: HIP error %s while freeing a plan\n", hipGetErrorString(first));
@@ -1723,13 +1770,13 @@ static int run_armed(xg_plan *p, double *step_done, double *step_post, double *w
     return XG_OK;
 }
 
-extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
+// The timed run's launches: ev0, then every step (a chain's launches stamp the steps'
+// completions, an engine segment is one launch), each followed by its step event.
+// step_post (may be null): host seconds spent enqueueing each step.
+static int enqueue_run(xg_plan *p, double *step_post)
 {
     xg_ctx *c = p->ctx;
     int rc;
-    HIPCHK(hipSetDevice(c->device));
-    if (p->db && !c->kt_mode) return run_armed(p, step_done, step_post, wall);
-    const double t0 = xg_now();
     HIPCHK(hipEventRecord(p->ev0, c->stream));
     p->rec_ev = true;
     const bool chains = p->d_cstamp && !c->kt_mode;
@@ -1777,6 +1824,38 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
         s = e;
     }
     p->rec_ev = false;
+    return XG_OK;
+}
+
+// graph replay applies: asked for, not inside a kernel-timing session (its per-launch
+// events are host bookkeeping), and a plan of more than one launch
+static bool use_graph(const xg_plan *p)
+{
+    return p->ctx->graph && !p->ctx->kt_mode && p->nlaunch > 1;
+}
+
+extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
+{
+    xg_ctx *c = p->ctx;
+    int rc;
+    HIPCHK(hipSetDevice(c->device));
+    if (p->db && !c->kt_mode) return run_armed(p, step_done, step_post, wall);
+    const bool chains = p->d_cstamp && !c->kt_mode;
+    if (use_graph(p) && !p->g_run) {
+        // captured once: the grid engine's ticket counter restarts from zero in every replay
+        p->engine_reset = true;
+        if ((rc = capture(c->stream, &p->g_run, [&] { return enqueue_run(p, nullptr); }))) return rc;
+    }
+    const double t0 = xg_now();
+    if (p->g_run && use_graph(p)) {
+        HIPCHK(hipGraphLaunch(p->g_run, c->stream));
+        if (step_post) {
+            step_post[0] = xg_now() - t0;          // the whole run is posted by one graph launch
+            for (int s = 1; s < p->nsteps; ++s) step_post[s] = 0;
+        }
+    } else if ((rc = enqueue_run(p, step_post))) {
+        return rc;
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     if (wall) *wall = xg_now() - t0;
     if ((rc = xg_plan_check(p))) return rc;
@@ -1820,8 +1899,18 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
 extern "C" int xg_plan_enqueue(xg_plan *p)
 {
     int rc;
-    for (int s = 0; s < p->nsteps; ++s)
-        if ((rc = enqueue_unit(p, s))) return rc;
+    auto body = [&] {
+        int r;
+        for (int s = 0; s < p->nsteps; ++s)
+            if ((r = enqueue_unit(p, s))) return r;
+        return XG_OK;
+    };
+    if (!use_graph(p)) return body();
+    if (!p->g_enq) {
+        p->engine_reset = true;
+        if ((rc = capture(p->ctx->stream, &p->g_enq, body))) return rc;
+    }
+    HIPCHK(hipGraphLaunch(p->g_enq, p->ctx->stream));
     return XG_OK;
 }
 
@@ -1864,7 +1953,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
     // posts in enqueue_step, paired as RCCL pairs them; refused unless every pair falls in
     // one step with one length and the GPUs agree on the barriers
     std::vector<xg_call_pair> pairs;
-    {
+    auto pair_calls = [&]() -> int {
         std::vector<const xg_call *> cl(n);
         std::vector<const int32_t *> cb(n);
         for (int g = 0; g < n; ++g) {
@@ -1880,50 +1969,73 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
         pairs.resize((size_t)np + 1);
         xg_calls_match(n, nst, cl.data(), cb.data(), pairs.data(), np, err, sizeof err);
         pairs.resize((size_t)np);
-    }
-    HIPCHK(hipEventRecord(plans[0]->ev0, st));
-    size_t q0 = 0;
-    for (int s = 0; s < nst; ++s) {
-        for (int g = 0; g < n; ++g) {
-            xg_plan *pg = plans[g];
-            const int gi = pg->seg_of[s];
-            if (gi < 0) rc = enqueue_pre(pg, s, st, pg->ctx->side);
-            else rc = pg->segs[gi].s0 == s ? launch_seg(pg, pg->segs[gi], st) : XG_OK;
-            if (rc) return rc;
-        }
-        size_t q1 = q0;
-        while (q1 < pairs.size() && pairs[q1].step == s) ++q1;
-        auto ends = [&](const xg_call_pair &q, uint8_t **src, uint8_t **dst) {
-            const xg_call &sc = plans[q.src]->calls[q.send_call], &rcv = plans[q.dst]->calls[q.recv_call];
-            *src = plans[q.src]->reg->ptr[sc.buf] + sc.off;
-            *dst = plans[q.dst]->reg->ptr[rcv.buf] + rcv.off;
-        };
-        if (!rccl) {
-            for (size_t q = q0; q < q1; ++q) {
-                uint8_t *src, *dst;
-                ends(pairs[q], &src, &dst);
-                if (pairs[q].len) HIPCHK(hipMemcpyAsync(dst, src, (size_t)pairs[q].len, hipMemcpyDeviceToDevice, st));
+        return XG_OK;
+    };
+    // the job's launches, RCCL groups and step events on plans[0]'s stream
+    auto body = [&]() -> int {
+        HIPCHK(hipEventRecord(plans[0]->ev0, st));
+        size_t q0 = 0;
+        for (int s = 0; s < nst; ++s) {
+            for (int g = 0; g < n; ++g) {
+                xg_plan *pg = plans[g];
+                const int gi = pg->seg_of[s];
+                if (gi < 0) rc = enqueue_pre(pg, s, st, pg->ctx->side);
+                else rc = pg->segs[gi].s0 == s ? launch_seg(pg, pg->segs[gi], st) : XG_OK;
+                if (rc) return rc;
             }
-        } else if (q1 > q0) {
-            // every pair of the step as a self send + receive in ONE group (issue order = pair order)
-            if ((rc = rccl_group(
-                     (int)(2 * (q1 - q0)),
-                     [&](int i) {
-                         uint8_t *src, *dst;
-                         const xg_call_pair &q = pairs[q0 + i / 2];
-                         ends(q, &src, &dst);
-                         return i % 2 == 0 ? ncclSend(src, (size_t)q.len, ncclUint8, 0, c0->comm, st)
-                                           : ncclRecv(dst, (size_t)q.len, ncclUint8, 0, c0->comm, st);
-                     },
-                     "virtual job step")))
-                return rc;
+            size_t q1 = q0;
+            while (q1 < pairs.size() && pairs[q1].step == s) ++q1;
+            auto ends = [&](const xg_call_pair &q, uint8_t **src, uint8_t **dst) {
+                const xg_call &sc = plans[q.src]->calls[q.send_call], &rcv = plans[q.dst]->calls[q.recv_call];
+                *src = plans[q.src]->reg->ptr[sc.buf] + sc.off;
+                *dst = plans[q.dst]->reg->ptr[rcv.buf] + rcv.off;
+            };
+            if (!rccl) {
+                for (size_t q = q0; q < q1; ++q) {
+                    uint8_t *src, *dst;
+                    ends(pairs[q], &src, &dst);
+                    if (pairs[q].len) HIPCHK(hipMemcpyAsync(dst, src, (size_t)pairs[q].len, hipMemcpyDeviceToDevice, st));
+                }
+            } else if (q1 > q0) {
+                // every pair of the step as a self send + receive in ONE group (issue order = pair order)
+                if ((rc = rccl_group(
+                         (int)(2 * (q1 - q0)),
+                         [&](int i) {
+                             uint8_t *src, *dst;
+                             const xg_call_pair &q = pairs[q0 + i / 2];
+                             ends(q, &src, &dst);
+                             return i % 2 == 0 ? ncclSend(src, (size_t)q.len, ncclUint8, 0, c0->comm, st)
+                                               : ncclRecv(dst, (size_t)q.len, ncclUint8, 0, c0->comm, st);
+                         },
+                         "virtual job step")))
+                    return rc;
+            }
+            q0 = q1;
+            for (int g = 0; g < n; ++g)
+                if (plans[g]->seg_of[s] < 0 && (rc = enqueue_post(plans[g], s, st))) return rc;
+            if (rccl && plans[0]->steps[s].sync_after)
+                NCCLCHK(ncclAllReduce(c0->d_red, c0->d_red, 1, ncclFloat64, ncclMax, c0->comm, st));
+            HIPCHK(hipEventRecord(plans[0]->ev[s], st));
         }
-        q0 = q1;
-        for (int g = 0; g < n; ++g)
-            if (plans[g]->seg_of[s] < 0 && (rc = enqueue_post(plans[g], s, st))) return rc;
-        if (rccl && plans[0]->steps[s].sync_after)
-            NCCLCHK(ncclAllReduce(c0->d_red, c0->d_red, 1, ncclFloat64, ncclMax, c0->comm, st));
-        HIPCHK(hipEventRecord(plans[0]->ev[s], st));
+        return XG_OK;
+    };
+    if (c0->graph && !c0->kt_mode) {
+        // XG_GRAPH=1: the job captured once (per set of plans and transport) and replayed
+        std::vector<uint64_t> ids(n);
+        for (int g = 0; g < n; ++g) ids[g] = plans[g]->id;
+        xg_plan::VGraph &vg = plans[0]->vg;
+        if (!vg.exec || vg.ids != ids || vg.rccl != rccl) {
+            if (vg.exec) HIPCHK(hipGraphExecDestroy(vg.exec));
+            vg.exec = nullptr;
+            if ((rc = pair_calls())) return rc;
+            for (int g = 0; g < n; ++g) plans[g]->engine_reset = true;
+            if ((rc = capture(st, &vg.exec, body))) return rc;
+            vg.ids = ids;
+            vg.rccl = rccl;
+        }
+        HIPCHK(hipGraphLaunch(vg.exec, st));
+    } else if ((rc = pair_calls()) || (rc = body())) {
+        return rc;
     }
     HIPCHK(hipStreamSynchronize(st));
     for (int g = 0; g < n; ++g)

@@ -2,6 +2,7 @@
 # One GPU call: the -m gpu suite, smoke, the N = 1 bench line, and the README configuration
 # through the CLI in each engine mode beside the reference.  usage: profiles/r03_gpu_round.sh <outdir>
 out=${1:-gpurun_out/r03}; mkdir -p $out
+timeout -k 10 120 mpi-asynchronous-communication-test_amd/tools/bin/graph_probe 38 > $out/graph_probe.txt 2>&1; cat $out/graph_probe.txt
 timeout -k 10 1000 python3 -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -p no:cacheprovider \
   > $out/gpu_tests.log 2>&1; rc=$?
 tail -5 $out/gpu_tests.log

@@ -309,3 +309,60 @@ def test_long_runs_split_into_solo_launches(xg, method, k, env):
     assert res["split"][0] == res["eager"][0] == res["grid"][0]
     print("method %d -k %d: split solo %.1f us, grid engine %.1f us, per-step launches %.1f us"
           % (method, k, res["split"][1] * 1e6, res["grid"][1] * 1e6, res["eager"][1] * 1e6))
+
+
+GRAPH_FORMS = {
+    "chains": {"XG_GRAPH": "1", "XG_ENGINE_MAX_STEP": "0"},                  # chained step launches, stamps
+    "grid_and_launches": {"XG_GRAPH": "1", "XG_ENGINE_SOLO": "0", "XG_ENGINE_MAX_STEP": str(64 << 10)},
+    "solo_and_launches": {"XG_GRAPH": "1", "XG_ENGINE_MAX_STEP": str(64 << 10)},
+}
+
+
+@pytest.mark.parametrize("form", list(GRAPH_FORMS))
+@pytest.mark.parametrize("method", [1, 4, 6, 9, 12, 13, 15])
+def test_graph_replay_one_gpu(xg, form, method):
+    """XG_GRAPH=1: a multi-launch plan is captured once (copy launches, chain stamps, engine
+    segments -- the grid engine's ticket counter reset inside the graph) and every later run
+    replays it.  Three runs, the receive slots re-poisoned between them: every replay delivers
+    every byte (strong fingerprint, against the oracle), step times ordered inside the wall
+    time."""
+    import os
+    import xg_oracle as O
+    P, A, d, c, k, it = 24, 7, 48 << 10, 3, 2, 1
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=4, barrier_type=1, iteration=it)
+    exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
+    env = GRAPH_FORMS[form]
+    old = {key: os.environ.get(key) for key in env}
+    os.environ.update(env)
+    try:
+        cx = xg.Context(rank=0, nranks=1, device=0)
+    finally:
+        for key, v in old.items():
+            if v is None:
+                del os.environ[key]
+            else:
+                os.environ[key] = v
+    try:
+        run = xg.MethodRun(cx, s, it=it, mode=1)
+        try:
+            for rep in range(3):
+                if rep:
+                    run.poison()
+                done, post, wall = run.run_timed()
+                assert all(0 <= a <= b for a, b in zip(done, done[1:])), (form, done)
+                assert done[-1] <= wall + 1e-4
+                chk, bad, _f = run.verify()
+                assert all(b == 0 for b in bad), (form, method, rep)
+                for (src, seed, dst, off), ck in zip(run.slots, chk):
+                    local = off - s.recv_offset(1, dst)
+                    assert ck == O.chk64(exp[dst][local: local + d]), (form, method, rep, src, dst)
+            run.poison()
+            run.enqueue()                     # the enqueue graph (bench loops) delivers too
+            cx.sync()
+            run.check()
+            assert all(b == 0 for b in run.verify()[1]), (form, method)
+        finally:
+            run.close()
+    finally:
+        cx.close()

@@ -31,11 +31,15 @@ def worlds(xg):
             c.close()
 
 
-def _run_job(xg, ctxs, s, it, mode, pack, rccl=False):
+def _run_job(xg, ctxs, s, it, mode, pack, rccl=False, reps=1):
     runs = [xg.MethodRun(c, s, it=it, mode=mode, pack_max_seg=pack) for c in ctxs]
     try:
-        done = xg.run_virtual(runs, rccl=rccl)
-        assert all(b >= a for a, b in zip(done, done[1:]))
+        for rep in range(reps):           # reps > 1: a replay (graph mode) must deliver again
+            if rep:
+                for r in runs:
+                    r.poison()
+            done = xg.run_virtual(runs, rccl=rccl)
+            assert all(b >= a for a, b in zip(done, done[1:]))
         out = []
         for r in runs:
             chk, bad, first = r.verify()
@@ -119,6 +123,8 @@ def test_config2_full_size_through_rccl(xg, worlds, G, method):
 STEP_FORMS = {
     "self_in_group": {"XG_SELF_MAX": str(1 << 30)},          # local part as self send/recv in the RCCL group
     "local_in_fused": {"XG_SPLIT_MIN": str(1 << 40)},        # local part in the (fused) pack launch
+    "graph": {"XG_GRAPH": "1"},                               # the whole job captured once, replayed
+    "graph_self": {"XG_GRAPH": "1", "XG_SELF_MAX": str(1 << 30)},
 }
 
 
@@ -149,7 +155,7 @@ def test_cross_gpu_step_forms(xg, form, rccl, G):
             s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2, iteration=it)
             exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
             for pack in (0, 1 << 20):
-                res = _run_job(xg, ctxs, s, it, 1, pack, rccl=rccl)
+                res = _run_job(xg, ctxs, s, it, 1, pack, rccl=rccl, reps=2 if "graph" in form else 1)
                 for (src, seed, dst, off), ck, nb, _fb in res:
                     assert nb == 0, (form, method, G, pack, src, dst)
                     local = off - s.recv_offset(G, dst)
