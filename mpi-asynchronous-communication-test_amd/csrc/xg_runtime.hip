@@ -25,12 +25,16 @@
 #include "kernels.h"
 #include "xg.h"
 
+// On an error, hipGetLastError() is read once more: HIP keeps the last failing call's error
+// for it, and a later launch check (hipGetLastError right after a launch) would otherwise
+// report this old error as its own.
 #define HIPCHK(x)                                                                                  \
     do {                                                                                           \
         hipError_t e_ = (x);                                                                       \
         if (e_ != hipSuccess) {                                                                    \
             fprintf(stderr, "xg: HIP error %s at %s:%d: %s\n", hipGetErrorString(e_), __FILE__,   \
                     __LINE__, #x);                                                                 \
+            (void)hipGetLastError();                                                               \
             return XG_EHIP;                                                                        \
         }                                                                                          \
     } while (0)
@@ -227,6 +231,12 @@ struct xg_plan {
     // captured at first use and replayed after (a launch-bound multi-step run then costs one
     // graph launch of host time instead of a launch, an event and an RCCL group per step)
     hipGraphExec_t g_enq, g_run;
+    // Captured HIP events are not re-recorded by a replay on this stack (tools/graph_probe.hip:
+    // elapsed times of a replay read the capture-time values, then 'invalid resource handle'),
+    // so a captured run marks its step boundaries with clock_kernel stamps instead: mark(i)
+    // writes the wall clock to d_gstamp[i + 1] (i = -1: the start) where it would record ev[i]
+    unsigned long long *d_gstamp;
+    bool stamp_marks;              // mark() stamps (graph capture) instead of recording events
     uint64_t id;                   // unique per loaded plan (keys the virtual runner's graphs)
     struct VGraph {
         std::vector<uint64_t> ids;
@@ -234,6 +244,31 @@ struct xg_plan {
         hipGraphExec_t exec;
     } vg;                          // plans[0] of a virtual job: the job's captured run
 };
+
+// step boundary i of a run (-1: its start) on `stream`: an event, or in a captured run a stamp
+static int mark(xg_plan *p, int i, hipStream_t stream)
+{
+    if (!p->stamp_marks) {
+        HIPCHK(hipEventRecord(i < 0 ? p->ev0 : p->ev[i], stream));
+        return XG_OK;
+    }
+    hipLaunchKernelGGL(xgk::clock_kernel, dim3(1), dim3(64), 0, stream, p->d_gstamp + i + 1);
+    HIPCHK(hipGetLastError());
+    return XG_OK;
+}
+
+// seconds from the run's start to boundary i, after the run (events or stamps, as marked)
+static int mark_elapsed(const xg_plan *p, int i, bool stamps, const std::vector<unsigned long long> &gs, double *sec)
+{
+    if (stamps) {
+        *sec = (double)(gs[i + 1] - gs[0]) / p->ctx->wall_hz;
+        return XG_OK;
+    }
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[i]));
+    *sec = ms * 1e-3;
+    return XG_OK;
+}
 
 static uint64_t next_plan_id()
 {
@@ -418,10 +453,15 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     c->engine_arm = env && !strcmp(env, "1");
     env = getenv("XG_SPLIT_LOCAL");          // "0": local gather + packs in one launch
     c->split_local = !(env && !strcmp(env, "0"));
+    // a cross-GPU step's local part: <= self_max bytes travels in the step's RCCL group as self
+    // send/recv (one RCCL launch carries a latency-bound step), < split_min bytes joins the
+    // step's pack / fused launch, larger runs on the side stream beside the exchange (split).
+    // README configuration as a virtual 8-GPU job (profiles/r03/hybrid/): m6 direct 49 -> 2
+    // launches per run, m12 46 -> 6; configs[1..4]'s bulk local parts (MiBs) stay split
     env = getenv("XG_SPLIT_MIN");            // bytes: a smaller local part is not split off
-    c->split_min = env ? atoll(env) : 0;
+    c->split_min = env ? atoll(env) : (int64_t)1 << 20;
     env = getenv("XG_SELF_MAX");             // bytes: local part posted as self send/recv (0: never)
-    c->self_max = env ? atoll(env) : 0;
+    c->self_max = env ? atoll(env) : (int64_t)256 << 10;
     env = getenv("XG_FUSE_UNPACK");          // "0": unpacks and the next step's packs apart
     c->fuse_unpack = !(env && !strcmp(env, "0"));
     env = getenv("XG_GRAPH");                // "1": replay captured runs (hipGraph)
@@ -1101,6 +1141,7 @@ static int plan_upload(xg_plan *p, const std::vector<xgk::DCopy> &pieces, DisplS
             HIPCHK(hipEventCreateWithFlags(&p->join[s], hipEventDisableTiming));
         }
     HIPCHK(hipEventCreate(&p->ev0));
+    if (p->ctx->graph) HIPCHK(hipMalloc(&p->d_gstamp, 8 * ((size_t)p->nsteps + 1)));
     if ((rc = run_displ_scan(p, ds)) || (rc = build_segments(p, pieces))) return rc;
     return XG_OK;
 }
@@ -1126,6 +1167,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
     p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1; p->d_cstamp = nullptr;
     p->g_enq = p->g_run = nullptr; p->id = next_plan_id(); p->vg.rccl = false; p->vg.exec = nullptr;
+    p->d_gstamp = nullptr; p->stamp_marks = false;
     // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
     // pieces for small launches were measured no faster, and slower where they stop
     // dividing the segment size (profiles/r01_min_pieces_ab.txt)
@@ -1413,7 +1455,7 @@ extern "C" int xg_plan_free(xg_plan *p)
     keep(hipStreamSynchronize(p->ctx->stream));
     keep(hipStreamSynchronize(p->ctx->side));
     for (void *q : {(void *)p->d_pieces, (void *)p->d_sb, (void *)p->d_epieces, (void *)p->d_engine,
-                    (void *)p->d_disp, (void *)p->d_solo, (void *)p->d_cstamp})
+                    (void *)p->d_disp, (void *)p->d_solo, (void *)p->d_cstamp, (void *)p->d_gstamp})
         if (q) keep(hipFree(q));
     if (p->db) keep(hipHostFree((void *)p->db));
     for (auto &e : p->ev) if (e) keep(hipEventDestroy(e));
@@ -1574,7 +1616,7 @@ static int enqueue_pre(xg_plan *p, int s, hipStream_t stream, hipStream_t side)
         const int n = pv.post_n + (st.fused_local ? st.local_n : 0) + st.pack_n;
         const int64_t b = pv.post_bytes + (st.fused_local ? st.local_bytes : 0) + st.pack_bytes;
         if ((rc = timed_copy(p, pv.post_b, n, b, stream, true))) return rc;
-        if (p->rec_ev) HIPCHK(hipEventRecord(p->ev[s - 1], stream));
+        if (p->rec_ev && (rc = mark(p, s - 1, stream))) return rc;
     }
     if (st.split) {
         HIPCHK(hipEventRecord(p->fork[s], stream));
@@ -1777,7 +1819,7 @@ static int enqueue_run(xg_plan *p, double *step_post)
 {
     xg_ctx *c = p->ctx;
     int rc;
-    HIPCHK(hipEventRecord(p->ev0, c->stream));
+    if ((rc = mark(p, -1, c->stream))) return rc;
     p->rec_ev = true;
     const bool chains = p->d_cstamp && !c->kt_mode;
     for (int s = 0; s < p->nsteps;) {
@@ -1806,7 +1848,10 @@ static int enqueue_run(xg_plan *p, double *step_post)
             }
             hipLaunchKernelGGL(xgk::clock_kernel, dim3(1), dim3(64), 0, c->stream, p->d_cstamp + ce - 1);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(p->ev[ce - 1], c->stream));
+            if ((rc = mark(p, ce - 1, c->stream))) {
+                p->rec_ev = false;
+                return rc;
+            }
             s = ce;
             continue;
         }
@@ -1816,7 +1861,10 @@ static int enqueue_run(xg_plan *p, double *step_post)
             return rc;
         }
         // a deferred step's unpacks run in the next step's fused launch, which records its event
-        if (gi >= 0 || !p->steps[s].deferred) HIPCHK(hipEventRecord(p->ev[e - 1], c->stream));
+        if ((gi >= 0 || !p->steps[s].deferred) && (rc = mark(p, e - 1, c->stream))) {
+            p->rec_ev = false;
+            return rc;
+        }
         if (step_post) {
             step_post[s] = xg_now() - tp;
             for (int t = s + 1; t < e; ++t) step_post[t] = 0;
@@ -1842,12 +1890,17 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     if (p->db && !c->kt_mode) return run_armed(p, step_done, step_post, wall);
     const bool chains = p->d_cstamp && !c->kt_mode;
     if (use_graph(p) && !p->g_run) {
-        // captured once: the grid engine's ticket counter restarts from zero in every replay
+        // captured once: the grid engine's ticket counter restarts from zero in every replay,
+        // the step boundaries are stamps (mark)
         p->engine_reset = true;
-        if ((rc = capture(c->stream, &p->g_run, [&] { return enqueue_run(p, nullptr); }))) return rc;
+        p->stamp_marks = true;
+        rc = capture(c->stream, &p->g_run, [&] { return enqueue_run(p, nullptr); });
+        p->stamp_marks = false;
+        if (rc) return rc;
     }
+    const bool graph = p->g_run && use_graph(p);
     const double t0 = xg_now();
-    if (p->g_run && use_graph(p)) {
+    if (graph) {
         HIPCHK(hipGraphLaunch(p->g_run, c->stream));
         if (step_post) {
             step_post[0] = xg_now() - t0;          // the whole run is posted by one graph launch
@@ -1862,18 +1915,21 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     if (!step_done) return XG_OK;
     std::vector<unsigned long long> st;
     if (!p->segs.empty() && (rc = read_stamps(p, st))) return rc;
-    std::vector<unsigned long long> cst;
+    std::vector<unsigned long long> cst, gs;
     if (chains) {
         cst.resize(p->nsteps);
         HIPCHK(hipMemcpy(cst.data(), p->d_cstamp, 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
+    }
+    if (graph) {
+        gs.resize((size_t)p->nsteps + 1);
+        HIPCHK(hipMemcpy(gs.data(), p->d_gstamp, 8 * gs.size(), hipMemcpyDeviceToHost));
     }
     for (int s = 0; s < p->nsteps;) {
         const int gi = p->seg_of[s];
         if (chains && p->chain_end[s]) {
             const int ce = p->chain_end[s];
-            float ms = 0;
-            HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[ce - 1]));
-            const double end = ms * 1e-3;
+            double end;
+            if ((rc = mark_elapsed(p, ce - 1, graph, gs, &end))) return rc;
             for (int t = s; t < ce; ++t) {
                 const double x = end - (double)(cst[ce - 1] - cst[t]) / c->wall_hz;
                 step_done[t] = t == ce - 1 ? end : (x > 0 ? x : 0);
@@ -1882,9 +1938,8 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
             continue;
         }
         const int e = gi >= 0 ? p->segs[gi].s1 : s + 1;
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[e - 1]));
-        const double end = ms * 1e-3;
+        double end;
+        if ((rc = mark_elapsed(p, e - 1, graph, gs, &end))) return rc;
         // inside a segment: the wall-clock stamps, anchored at the event after its launch
         // (the last step of a segment is drained, so its stamp is a delivered time)
         for (int t = s; t < e; ++t) {
@@ -1973,7 +2028,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
     };
     // the job's launches, RCCL groups and step events on plans[0]'s stream
     auto body = [&]() -> int {
-        HIPCHK(hipEventRecord(plans[0]->ev0, st));
+        if ((rc = mark(plans[0], -1, st))) return rc;
         size_t q0 = 0;
         for (int s = 0; s < nst; ++s) {
             for (int g = 0; g < n; ++g) {
@@ -2015,7 +2070,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
                 if (plans[g]->seg_of[s] < 0 && (rc = enqueue_post(plans[g], s, st))) return rc;
             if (rccl && plans[0]->steps[s].sync_after)
                 NCCLCHK(ncclAllReduce(c0->d_red, c0->d_red, 1, ncclFloat64, ncclMax, c0->comm, st));
-            HIPCHK(hipEventRecord(plans[0]->ev[s], st));
+            if ((rc = mark(plans[0], s, st))) return rc;
         }
         return XG_OK;
     };
@@ -2028,8 +2083,13 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
             if (vg.exec) HIPCHK(hipGraphExecDestroy(vg.exec));
             vg.exec = nullptr;
             if ((rc = pair_calls())) return rc;
-            for (int g = 0; g < n; ++g) plans[g]->engine_reset = true;
-            if ((rc = capture(st, &vg.exec, body))) return rc;
+            for (int g = 0; g < n; ++g) {
+                plans[g]->engine_reset = true;
+                plans[g]->stamp_marks = true;      // step boundaries as stamps in the graph
+            }
+            rc = capture(st, &vg.exec, body);
+            for (int g = 0; g < n; ++g) plans[g]->stamp_marks = false;
+            if (rc) return rc;
             vg.ids = ids;
             vg.rccl = rccl;
         }
@@ -2040,12 +2100,16 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
     HIPCHK(hipStreamSynchronize(st));
     for (int g = 0; g < n; ++g)
         if ((rc = xg_plan_check(plans[g]))) return rc;
-    if (step_done)
-        for (int s = 0; s < nst; ++s) {
-            float ms = 0;
-            HIPCHK(hipEventElapsedTime(&ms, plans[0]->ev0, plans[0]->ev[s]));
-            step_done[s] = ms * 1e-3;
+    if (step_done) {
+        const bool graph = c0->graph && !c0->kt_mode;
+        std::vector<unsigned long long> gs;
+        if (graph) {
+            gs.resize((size_t)nst + 1);
+            HIPCHK(hipMemcpy(gs.data(), plans[0]->d_gstamp, 8 * gs.size(), hipMemcpyDeviceToHost));
         }
+        for (int s = 0; s < nst; ++s)
+            if ((rc = mark_elapsed(plans[0], s, graph, gs, &step_done[s]))) return rc;
+    }
     return XG_OK;
 }
 

@@ -1,14 +1,15 @@
 #!/bin/bash
 # Cross-GPU step forms on the README configuration as a virtual 8-GPU job (RCCL self send/recv
 # on one MI355X), packed and direct, rocprofv3 kernel traces (launches the device saw):
-#   split           default round 2: local gather on the side stream (fork/join events)
-#   local_in_fused  XG_SPLIT_MIN=huge: the local part joins the step's (fused) pack launch
+#   split           round 2: local gather on the side stream (fork/join events): XG_SELF_MAX=0 XG_SPLIT_MIN=0
+#   local_in_fused  XG_SELF_MAX=0 XG_SPLIT_MIN=huge: the local part joins the step's (fused) pack launch
 #   self_in_group   XG_SELF_MAX=huge: the local part goes in the step's RCCL group as self send/recv
+#                   (the round-3 default at these sizes: local parts <= 256 KiB)
 #   *_graph         the same with XG_GRAPH=1: the job captured once into a hipGraph and replayed
 export TMPDIR=/tmp
 o=${1:-$PWD/gpurun_out/r03_hybrid}; mkdir -p $o
 for form in ${FORMS:-split local_in_fused self_in_group split_graph local_in_fused_graph self_in_group_graph}; do
-  unset XG_SPLIT_MIN XG_SELF_MAX XG_GRAPH
+  unset XG_GRAPH; export XG_SELF_MAX=0 XG_SPLIT_MIN=0
   case $form in local_in_fused*) export XG_SPLIT_MIN=1099511627776;; esac
   case $form in self_in_group*) export XG_SELF_MAX=1073741824;; esac
   case $form in *_graph) export XG_GRAPH=1;; esac
