@@ -1173,12 +1173,17 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     // dividing the segment size (profiles/r01_min_pieces_ab.txt)
     // bytes per piece = per workgroup: c->chunk (32 KiB), or less for a launch too small to
     // spread over min_wg workgroups -- a 4 MiB gather as 128 pieces of 32 KiB kept half the
-    // CUs idle (1.4 TB/s, profiles/r02/pack_virtual.txt); pieces stay >= 4 KiB, 16-B multiples
+    // CUs idle (1.4 TB/s, profiles/r02/pack_virtual.txt).  The smaller piece is a power of two
+    // (>= 4 KiB), so it still divides the power-of-two segment sizes without a ragged tail
+    // piece per segment (profiles/r01_min_pieces_ab.txt: 28 KiB pieces of 64 KiB segments +9 %)
     int64_t chunk = c->chunk;
     auto launch_chunk = [&](int64_t bytes) {
         chunk = c->chunk;
-        if (c->min_wg > 0 && bytes > 0 && bytes < (int64_t)c->min_wg * chunk)
-            chunk = std::min(c->chunk, std::max<int64_t>(4096, (bytes / c->min_wg + 15) & ~(int64_t)15));
+        if (c->min_wg > 0 && bytes > 0 && bytes < (int64_t)c->min_wg * chunk) {
+            int64_t ch = 4096;
+            while (2 * ch <= bytes / c->min_wg && 2 * ch <= c->chunk) ch *= 2;
+            chunk = std::min(c->chunk, ch);
+        }
     };
     auto copy_bytes = [&](int b, int n) {
         int64_t t = 0;
