@@ -435,8 +435,12 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     {
         int cus = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        env = getenv("XG_COPY_MIN_WG");       // 0: always chunk-sized pieces
-        c->min_wg = env ? atoi(env) : 2 * cus;
+        // > 0: a copy launch smaller than min_wg x chunk gets smaller (power-of-two) pieces.  Off:
+        // standalone launches of 3.5 / 14 MiB ran 3-7 % SLOWER with 2 x CUs pieces than with
+        // 32 KiB ones (profiles/r03/min_wg/summary.txt) -- a launch that small is ramp-bound
+        env = getenv("XG_COPY_MIN_WG");
+        c->min_wg = env ? atoi(env) : 0;
+        (void)cus;
     }
     env = getenv("XG_SOLO_MIN_STEPS");       // plans of fewer steps never run as an armed solo launch
     c->solo_min_steps = env ? atoi(env) : 1;  // profiles/r02/one_step/: armed beats the event-timed launch
