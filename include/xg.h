@@ -187,6 +187,7 @@ typedef struct {
     int proc_node;           /* -p (m17's node_robin_map)                                       */
     int barrier_type;        /* -b (m13)                                                        */
     xg_timer *rep_timers;    /* out, optional: hosted ranks x ntimes timers[m] (m13)            */
+    int64_t pack_min_bytes;  /* ... and pack only (step, peer) lists of >= this many bytes        */
 } xg_run_opts;
 
 void xg_run_opts_default(xg_run_opts *o);

@@ -190,6 +190,9 @@ int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf);
  * segments into one staging buffer when there are >= 2 and their mean length
  * is < pack_max_seg (0 = never pack); otherwise one RCCL op per segment. */
 xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg);
+/* The same, packing a (step, peer) transfer list only when it also moves >= pack_min bytes
+ * (smaller lists go one RCCL call per segment: cheaper than a pack and an unpack launch). */
+xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min);
 void xg_devplan_free(xg_devplan *p);
 
 /* ---------------------------------------------------------------- RCCL calls (calls.c)

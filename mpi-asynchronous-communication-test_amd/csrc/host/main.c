@@ -68,7 +68,7 @@ static void usage(const char *argv0)   /* mpi_test.c:41-69 */
 typedef struct {
     int P, A, d, c, ntimes, type, proc_node, barrier_type;
     int verify, fp_mode;
-    int64_t eager, pack_max;
+    int64_t eager, pack_max, pack_min;
     int *rank_list;
     const char *prefix;
 } opts_t;
@@ -88,6 +88,7 @@ static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
     timers = (xg_timer *)calloc(hi - lo + 1, sizeof(xg_timer));
     xg_run_opts_default(&ro);
     ro.verify = o->verify; ro.fingerprint = o->fp_mode; ro.eager_limit = o->eager; ro.pack_max_seg = o->pack_max;
+    ro.pack_min_bytes = o->pack_min;
     ro.proc_node = o->proc_node; ro.barrier_type = o->barrier_type;
     if ((method == 15 || method == 16) && g == 0)   /* static_node_assignment, lustre_driver_test.c:361-363 */
         printf("static node assignment for %d node ( %d processes per node) of type %d\n", o->P, o->proc_node, 0);
@@ -144,7 +145,7 @@ int main(int argc, char **argv)
     /* defaults of mpi_test.c:2121 */
     int cb_nodes = 1, method = 0, data_size = 0, proc_node = 1, i, comm_size = 200000000, iter = 1, ntimes = 1;
     int aggregator_type = 1, barrier_type = 0, procs = 0, verify = 0, fp_mode = XG_FP_REFERENCE;
-    int64_t eager = XG_MPICH_EAGER_LIMIT, pack_max = 4 << 20;
+    int64_t eager = XG_MPICH_EAGER_LIMIT, pack_max = 4 << 20, pack_min = 64 << 10;
     char prefix[200];
     int rank, nranks, device, ngpu_dev;
     unsigned char uid[XG_UNIQUE_ID_BYTES];
@@ -158,6 +159,7 @@ int main(int argc, char **argv)
         {"eager-limit", required_argument, 0, 1003},
         {"pack-max-seg", required_argument, 0, 1004},
         {"gpus", required_argument, 0, 1005},
+        {"pack-min", required_argument, 0, 1006},
         {0, 0, 0, 0}};
     int ngpus = xg_env_int("XG_GPUS", NULL, 1);
     prefix[0] = '\0';
@@ -170,6 +172,7 @@ int main(int argc, char **argv)
     if (getenv("XG_FINGERPRINT") && !strcmp(getenv("XG_FINGERPRINT"), "strong")) fp_mode = XG_FP_STRONG;
     if (getenv("XG_EAGER_LIMIT")) eager = atoll(getenv("XG_EAGER_LIMIT"));
     if (getenv("XG_PACK_MAX_SEG")) pack_max = atoll(getenv("XG_PACK_MAX_SEG"));
+    if (getenv("XG_PACK_MIN")) pack_min = atoll(getenv("XG_PACK_MIN"));
 
     while ((i = getopt_long(argc, argv, "hp:c:m:d:a:i:k:t:r:b:", longopts, NULL)) != EOF) {
         switch (i) {
@@ -189,6 +192,7 @@ int main(int argc, char **argv)
         case 1003: eager = atoll(optarg); break;
         case 1004: pack_max = atoll(optarg); break;
         case 1005: ngpus = atoi(optarg); break;
+        case 1006: pack_min = atoll(optarg); break;
         default:
             if (rank == 0) usage(argv[0]);
             return 0;
@@ -214,7 +218,7 @@ int main(int argc, char **argv)
     if (rank == 0 && rdzv_path[0]) unlink(rdzv_path);
 
     o.P = procs; o.A = cb_nodes; o.d = data_size; o.c = comm_size; o.ntimes = ntimes; o.type = aggregator_type;
-    o.proc_node = proc_node; o.verify = verify; o.fp_mode = fp_mode; o.eager = eager; o.pack_max = pack_max;
+    o.proc_node = proc_node; o.verify = verify; o.fp_mode = fp_mode; o.eager = eager; o.pack_max = pack_max; o.pack_min = pack_min;
     o.barrier_type = barrier_type; o.prefix = prefix;
     o.rank_list = (int *)malloc(sizeof(int) * cb_nodes);
     if (xg_aggregator_list(procs, cb_nodes, proc_node, aggregator_type, o.rank_list))

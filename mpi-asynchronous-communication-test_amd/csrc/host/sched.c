@@ -1759,10 +1759,12 @@ void xg_devplan_free(xg_devplan *p)
     free(p->copies); free(p->p2p); free(p->steps); free(p);
 }
 
-/* same decision on both ends of a (step, src gpu, dst gpu) transfer list */
-static int use_pack(int n, int64_t total, int64_t pack_max_seg)
+/* same decision on both ends of a (step, src gpu, dst gpu) transfer list: >= 2 segments, mean
+ * below pack_max_seg, and at least pack_min bytes (below that one RCCL call per segment costs
+ * less than the pack and unpack launches) */
+static int use_pack(int n, int64_t total, int64_t pack_max_seg, int64_t pack_min)
 {
-    return pack_max_seg > 0 && n >= 2 && total / n < pack_max_seg;
+    return pack_max_seg > 0 && n >= 2 && total / n < pack_max_seg && total >= pack_min;
 }
 
 /* region base of every rank hosted by the GPU the plan is for */
@@ -1810,6 +1812,11 @@ static void local_copy(xg_copy *c, const plan_bases *pb, const xg_msg *m)
 }
 
 xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg)
+{
+    return xg_devplan_build_ex(s, ngpus, g, pack_max_seg, 0);
+}
+
+xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min)
 {
     xg_devplan *dp = (xg_devplan *)calloc(1, sizeof *dp);
     int nst = s->nsteps, i, st, G = ngpus;
@@ -1871,7 +1878,7 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
         /* packs (into staging) join the pre-exchange copy launch */
         for (p = 0; p < G; ++p) {
             int64_t off = 0;
-            if (p == g || !bucket_n[p] || !use_pack(bucket_n[p], bucket_b[p], pack_max_seg)) continue;
+            if (p == g || !bucket_n[p] || !use_pack(bucket_n[p], bucket_b[p], pack_max_seg, pack_min)) continue;
             for (k = b; k < e; ++k) {
                 const xg_msg *m = &s->msgs[order[k]];
                 if (!moves(m) || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
@@ -1895,7 +1902,7 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
                 int pk;
                 if (p == g) continue;
                 if (bucket_n[p]) {
-                    pk = use_pack(bucket_n[p], bucket_b[p], pack_max_seg);
+                    pk = use_pack(bucket_n[p], bucket_b[p], pack_max_seg, pack_min);
                     if (pk) {
                         xg_p2p *o = ppush(&pp);
                         o->peer = p; o->is_send = 1; o->buf = XG_BUF_STAGE_SEND; o->off = soff; o->len = bucket_b[p];
@@ -1914,7 +1921,7 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
                     dp->remote_send_bytes += bucket_b[p];
                 }
                 if (bucket_n[G + p]) {
-                    pk = use_pack(bucket_n[G + p], bucket_b[G + p], pack_max_seg);
+                    pk = use_pack(bucket_n[G + p], bucket_b[G + p], pack_max_seg, pack_min);
                     if (pk) {
                         xg_p2p *o = ppush(&pp);
                         int64_t off = 0;

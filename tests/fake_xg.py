@@ -101,12 +101,12 @@ def make(real_xg):
             pass
 
     class MethodRun:
-        def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None):
+        def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None, pack_min=0):
             self.ctx, self.sched, self.pack_max_seg = ctx, sched, pack_max_seg
             G, g = ctx.nranks, ctx.rank
             if G > 1:     # as the real MethodRun: refuse calls RCCL would not pair
-                sched.check_pairing(G, pack_max_seg)
-            self.view = sched.devplan(G, g, pack_max_seg)
+                sched.check_pairing(G, pack_max_seg, pack_min)
+            self.view = sched.devplan(G, g, pack_max_seg, pack_min)
             # the RCCL calls this GPU's plan posts per run: per step its send/recv group and
             # its barrier (xg_devplan_step_calls), as a signature the ranks must agree on in
             # everything collective (the barriers) -- the p2p pairing is xg_devplans_match's

@@ -94,3 +94,31 @@ def test_random_plans_deliver_every_byte(xg, case):
     for pack in (0, 1 << 20):
         _views, regs = simulate(s, G, it=2, mode=1, pack=pack)
         check_recv(s, G, regs, it=2, mode=1)
+
+
+def test_pack_min_keeps_small_peer_lists_direct(xg):
+    """pack_min (the CLI default 64 KiB): a (step, peer) list of >= 2 segments is packed only
+    when it also moves >= pack_min bytes; both ends decide alike, so the plans still pair and
+    deliver every byte"""
+    P, A = 32, 14
+    rl = xg.aggregator_list(P, A)
+    for d, expect_packed in ((2048, False), (1 << 20, True)):
+        s = xg.Schedule(1, P, A, d, 200000000, rl)
+        G = 8
+        views = [s.devplan(G, g, 4 << 20, 64 << 10) for g in range(G)]
+        packed = any(o[2] == 2 for v in views for o in v.p2p)          # a send from STAGE_SEND
+        assert packed == expect_packed, d
+        s.check_pairing(G, 4 << 20, 64 << 10)
+    s = xg.Schedule(6, P, A, 40, 3, rl, ntimes=2)
+    _views, regs = simulate_min(s, 8)
+    check_recv(s, 8, regs)
+
+
+def simulate_min(s, G):
+    import plan_exec
+    orig = s.devplan
+    s.devplan = lambda ng, g, pack=1 << 20: orig(ng, g, pack, 64 << 10)
+    try:
+        return plan_exec.simulate(s, G)
+    finally:
+        s.devplan = orig
