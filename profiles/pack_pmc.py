@@ -12,7 +12,7 @@ import os
 import sys
 
 CHUNK = int(os.environ.get("XG_COPY_CHUNK", "32768"))
-CLASSES = {512: 4 << 20}          # workgroups -> bytes moved, where pieces are not CHUNK
+CLASSES = {int(k): int(v) for k, v in (kv.split("=") for kv in os.environ.get("PACK_CLASSES", "").split(",") if kv)}
 
 
 def per_class(path, counter):

@@ -7,7 +7,7 @@
 export TMPDIR=/tmp
 o=${1:-$PWD/gpurun_out/r03_pack}; mkdir -p $o
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $o/kt -o run --output-format csv -- python3 profiles/pack_virtual.py > $o/run.txt 2> $o/run.err || exit 1
-python3 profiles/pack_summary.py $(find $o/kt -name run_kernel_trace.csv) 512=4194304 > $o/summary.txt || exit 1
+python3 profiles/pack_summary.py $(find $o/kt -name run_kernel_trace.csv) > $o/summary.txt || exit 1
 rm -rf $o/kt
 for pack in 1073741824 0; do
   PACK=$pack RCCL=1 REPS=20 timeout -k 10 120 python3 profiles/pack_virtual.py > $o/time_rccl_$pack.txt 2>&1 || exit 1
