@@ -12,4 +12,6 @@ bash profiles/r03_pack.sh $PWD/$out/pack > /dev/null || exit 1
 cat $out/pack/summary.txt $out/pack/pmc.txt
 KINDS=0,1,8,9,14,15 SIZES_MIB=4,14,28,56,448 timeout -k 10 300 python3 -u profiles/copy_ceiling.py > $out/copy_ceiling_mid.txt 2>&1 || exit 1
 cat $out/copy_ceiling_mid.txt
+XG_SELF_COMM=1 timeout -k 10 120 python3 -u profiles/rccl_self_floor.py > $out/rccl_self_floor.txt 2>&1 || exit 1
+cat $out/rccl_self_floor.txt
 exit $rc
