@@ -286,6 +286,11 @@ int xg_solo_tables_g(const xg_span *xfer, const int *step_begin, int nsteps, int
  * the rail closed nothing there): out[t] = max over rails of the rail's latest stamp <= t. */
 void xg_solo_reduce_stamps(const uint64_t *stamps, int rails, int64_t stride, int s0, int s1, uint64_t *out);
 
+/* Piece (= workgroup) size of one copy launch over copies of lengths lens[n]: among chunk,
+ * chunk/2, ... >= 4 KiB (16-B multiples), the one whose busiest CU -- ceil(pieces / cus)
+ * pieces of (size + wg_cost) bytes -- has the least work; ties keep the larger (pieces.c). */
+int64_t xg_piece_size(const int64_t *lens, int n, int64_t chunk, int cus, int64_t wg_cost);
+
 /* fill: `nsegs` consecutive d-byte segments at `off` in the SEND region,
  * segment i = fingerprint(rank, seed0 + i, iter) (prepare_*_data loops). */
 typedef struct { int32_t rank, seed0; int64_t off; int32_t nsegs, pad; } xg_segrun;

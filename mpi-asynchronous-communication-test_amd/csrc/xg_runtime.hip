@@ -117,6 +117,9 @@ struct xg_ctx {
     int solo_min_steps;        // a whole plan of fewer steps stays a copy launch
     int64_t launch_max;        // copy launches above this many bytes go as back-to-back launches of ~this size
     int min_wg;                // a copy launch of fewer bytes than min_wg x chunk gets smaller pieces (>= 4 KiB)
+    int balance;               // 1: per launch, the piece size that least loads the busiest CU (launch_chunk)
+    int64_t wg_cost;           // ... a workgroup's fixed start, in bytes-equivalent
+    int cus;                   // compute units
     int solo_relay;            // armed solo: rail 0 alone polls the doorbell and relays the ring
     int step_chain;            // 1: time runs of one-launch local steps by in-kernel stamps (xg_plan_run)
     int piece_order;           // local pieces of a launch: 0 message order, 1 by destination, 2 by source
@@ -440,7 +443,11 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
         // 32 KiB ones (profiles/r03/min_wg/summary.txt) -- a launch that small is ramp-bound
         env = getenv("XG_COPY_MIN_WG");
         c->min_wg = env ? atoi(env) : 0;
-        (void)cus;
+        c->cus = cus > 0 ? cus : 256;
+        env = getenv("XG_COPY_BALANCE");
+        c->balance = !(env && !strcmp(env, "0"));
+        env = getenv("XG_COPY_WG_COST");
+        c->wg_cost = env ? atoll(env) : 2048;
     }
     env = getenv("XG_SOLO_MIN_STEPS");       // plans of fewer steps never run as an armed solo launch
     c->solo_min_steps = env ? atoi(env) : 1;  // profiles/r02/one_step/: armed beats the event-timed launch
@@ -1172,27 +1179,36 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1; p->d_cstamp = nullptr;
     p->g_enq = p->g_run = nullptr; p->id = next_plan_id(); p->vg.rccl = false; p->vg.exec = nullptr;
     p->d_gstamp = nullptr; p->stamp_marks = false;
-    // one piece per workgroup, c->chunk bytes (32 KiB: profiles/r01_copy_ab.txt); smaller
-    // pieces for small launches were measured no faster, and slower where they stop
-    // dividing the segment size (profiles/r01_min_pieces_ab.txt)
-    // bytes per piece = per workgroup: c->chunk (32 KiB), or less for a launch too small to
-    // spread over min_wg workgroups -- a 4 MiB gather as 128 pieces of 32 KiB kept half the
-    // CUs idle (1.4 TB/s, profiles/r02/pack_virtual.txt).  The smaller piece is a power of two
-    // (>= 4 KiB), so it still divides the power-of-two segment sizes without a ragged tail
-    // piece per segment (profiles/r01_min_pieces_ab.txt: 28 KiB pieces of 64 KiB segments +9 %)
+    // One piece per workgroup.  Bytes per piece, per launch (launch_chunk over the launch's
+    // copies): c->chunk (32 KiB: profiles/r01_copy_ab.txt) or c->chunk / 2, / 4, / 8 (>= 4 KiB;
+    // a halving keeps dividing the power-of-two segment sizes: no ragged tail piece per segment,
+    // profiles/r01_min_pieces_ab.txt), whichever gives the least work to the busiest CU: a
+    // launch of w pieces of c bytes puts ceil(w / CUs) pieces on some CU, each costing c bytes
+    // plus a fixed per-workgroup start (XG_COPY_WG_COST bytes-equivalent, default 2 KiB); ties
+    // keep the larger piece.  A 28 MiB pack of 256 KiB segments: 896 pieces of 32 KiB = 3.5
+    // per CU (the busiest 4 x 32 KiB) -> 1792 of 16 KiB = exactly 7 (7 x 16 KiB).  The bench's
+    // 448 MiB launches stay 32 KiB (56 per CU).  XG_COPY_BALANCE=0: always c->chunk;
+    // XG_COPY_MIN_WG > 0 (off): the older rule, >= min_wg pieces for a small launch.
     int64_t chunk = c->chunk;
-    auto launch_chunk = [&](int64_t bytes) {
+    auto launch_chunk = [&](std::initializer_list<std::pair<int, int>> ranges) {
         chunk = c->chunk;
-        if (c->min_wg > 0 && bytes > 0 && bytes < (int64_t)c->min_wg * chunk) {
-            int64_t ch = 4096;
-            while (2 * ch <= bytes / c->min_wg && 2 * ch <= c->chunk) ch *= 2;
-            chunk = std::min(c->chunk, ch);
+        int64_t bytes = 0;
+        for (const auto &rg : ranges)
+            for (int i = 0; i < rg.second; ++i) bytes += std::max<int64_t>(0, dp->copies[rg.first + i].len);
+        if (bytes <= 0) return;
+        if (c->min_wg > 0) {
+            if (bytes < (int64_t)c->min_wg * chunk) {
+                int64_t ch = 4096;
+                while (2 * ch <= bytes / c->min_wg && 2 * ch <= c->chunk) ch *= 2;
+                chunk = std::min(c->chunk, ch);
+            }
+            return;
         }
-    };
-    auto copy_bytes = [&](int b, int n) {
-        int64_t t = 0;
-        for (int i = 0; i < n; ++i) t += std::max<int64_t>(0, dp->copies[b + i].len);
-        return t;
+        if (!c->balance) return;
+        std::vector<int64_t> lens;
+        for (const auto &rg : ranges)
+            for (int i = 0; i < rg.second; ++i) lens.push_back(dp->copies[rg.first + i].len);
+        chunk = xg_piece_size(lens.data(), (int)lens.size(), c->chunk, c->cus, c->wg_cost);
     };
     std::vector<xgk::DCopy> pieces;
     DisplScan ds;
@@ -1307,10 +1323,12 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
                 first_pack = i;
                 break;
             }
-        const int64_t b_local = copy_bytes(sp.pre_begin + sp.stage_count, first_pack - sp.stage_count);
-        const int64_t b_pack = copy_bytes(sp.pre_begin + first_pack, sp.pre_count - first_pack);
-        const int64_t b_prev = st.fused ? copy_bytes(dp->steps[s - 1].post_begin, dp->steps[s - 1].post_count) : 0;
-        launch_chunk(copy_bytes(sp.pre_begin, sp.stage_count));
+        const std::pair<int, int> r_stage{sp.pre_begin, sp.stage_count},
+            r_local{sp.pre_begin + sp.stage_count, st.self_local ? 0 : first_pack - sp.stage_count},
+            r_pack{sp.pre_begin + first_pack, sp.pre_count - first_pack},
+            r_prev{st.fused ? dp->steps[s - 1].post_begin : 0, st.fused ? dp->steps[s - 1].post_count : 0},
+            r_post{sp.post_begin, sp.post_count};
+        launch_chunk({r_stage});
         st.stage_b = (int)pieces.size();
         for (int i = 0; i < sp.stage_count; ++i)
             if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
@@ -1318,12 +1336,12 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.stage_bytes = span(st.stage_b);
         // piece order: stage | local | [previous unpacks] | packs (split or not fused), or
         // stage | previous unpacks | local | packs (fused_local: one launch over all three)
-        const int64_t b_own = st.self_local ? 0 : b_local;
         if (st.fused_local) {
-            launch_chunk(b_prev + b_own + b_pack);
+            launch_chunk({r_prev, r_local, r_pack});
             if (!add_post(s - 1)) goto bad;
         } else {
-            launch_chunk(st.split ? b_own : b_own + b_pack);
+            if (st.split) launch_chunk({r_local});
+            else launch_chunk({r_local, r_pack});
         }
         st.local_b = (int)pieces.size();
         for (int i = sp.stage_count; i < first_pack && !st.self_local; ++i)
@@ -1331,7 +1349,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.local_n = (int)pieces.size() - st.local_b;
         st.local_bytes = span(st.local_b);
         if (!st.fused_local) {
-            if (st.split || st.fused) launch_chunk(b_prev + b_pack);
+            if (st.split || st.fused) launch_chunk({r_prev, r_pack});
             if (st.fused && !add_post(s - 1)) goto bad;
         }
         st.pack_b = (int)pieces.size();
@@ -1344,7 +1362,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.post_b = (int)pieces.size();
         st.post_n = 0;
         st.post_bytes = 0;
-        launch_chunk(copy_bytes(sp.post_begin, sp.post_count));
+        launch_chunk({r_post});
         if (!st.deferred && !add_post(s)) goto bad;
     }
     // order of a launch's local pieces (workgroup i copies piece i): by destination address

@@ -158,6 +158,8 @@ def host():
         h.xg_devplans_match.restype = C.c_int64
         h.xg_devplans_match.argtypes = [C.POINTER(C.POINTER(DevPlan)), C.c_int, C.c_int64, C.POINTER(CallPair),
                                         C.c_int64, C.c_char_p, C.c_size_t]
+        h.xg_piece_size.restype = C.c_int64
+        h.xg_piece_size.argtypes = [C.POINTER(C.c_int64), C.c_int, C.c_int64, C.c_int, C.c_int64]
         h.xg_fill_runs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(SegRun)]
         h.xg_verify_slots.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(Slot)]
         h.xg_engine_hazards.argtypes = [C.POINTER(Span), C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int)]
@@ -275,6 +277,12 @@ def devplans_match(plans, self_max=0):
     out = (CallPair * max(1, n))()
     host().xg_devplans_match(arr, G, self_max, out, n, err, 512)
     return _pairs(n, out)
+
+
+def piece_size(lens, chunk=32768, cus=256, wg_cost=2048):
+    """xg_piece_size: the workgroup piece size of one copy launch over copies of these lengths"""
+    arr = (C.c_int64 * max(1, len(lens)))(*lens)
+    return host().xg_piece_size(arr, len(lens), chunk, cus, wg_cost)
 
 
 def method_label(method):
