@@ -116,7 +116,6 @@ struct xg_ctx {
     int solo_waves;            // waves per rail: 16 (a workgroup) or 1
     int solo_min_steps;        // a whole plan of fewer steps stays a copy launch
     int64_t launch_max;        // copy launches above this many bytes go as back-to-back launches of ~this size
-    int min_wg;                // a copy launch of fewer bytes than min_wg x chunk gets smaller pieces (>= 4 KiB)
     int balance;               // 1: per launch, the piece size that least loads the busiest CU (launch_chunk)
     int64_t wg_cost;           // ... a workgroup's fixed start, in bytes-equivalent
     int cus;                   // compute units
@@ -438,11 +437,6 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     {
         int cus = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        // > 0: a copy launch smaller than min_wg x chunk gets smaller (power-of-two) pieces.  Off:
-        // standalone launches of 3.5 / 14 MiB ran 3-7 % SLOWER with 2 x CUs pieces than with
-        // 32 KiB ones (profiles/r03/min_wg/summary.txt) -- a launch that small is ramp-bound
-        env = getenv("XG_COPY_MIN_WG");
-        c->min_wg = env ? atoi(env) : 0;
         c->cus = cus > 0 ? cus : 256;
         env = getenv("XG_COPY_BALANCE");
         c->balance = !(env && !strcmp(env, "0"));
@@ -1187,8 +1181,9 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     // plus a fixed per-workgroup start (XG_COPY_WG_COST bytes-equivalent, default 2 KiB); ties
     // keep the larger piece.  A 28 MiB pack of 256 KiB segments: 896 pieces of 32 KiB = 3.5
     // per CU (the busiest 4 x 32 KiB) -> 1792 of 16 KiB = exactly 7 (7 x 16 KiB).  The bench's
-    // 448 MiB launches stay 32 KiB (56 per CU).  XG_COPY_BALANCE=0: always c->chunk;
-    // XG_COPY_MIN_WG > 0 (off): the older rule, >= min_wg pieces for a small launch.
+    // 448 MiB launches stay 32 KiB (56 per CU).  XG_COPY_BALANCE=0: always c->chunk.  (A rule
+    // forcing >= 2 x CUs pieces on small launches was measured 3-7 % slower and dropped:
+    // profiles/r03/min_wg/summary.txt.)
     int64_t chunk = c->chunk;
     auto launch_chunk = [&](std::initializer_list<std::pair<int, int>> ranges) {
         chunk = c->chunk;
@@ -1196,14 +1191,6 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         for (const auto &rg : ranges)
             for (int i = 0; i < rg.second; ++i) bytes += std::max<int64_t>(0, dp->copies[rg.first + i].len);
         if (bytes <= 0) return;
-        if (c->min_wg > 0) {
-            if (bytes < (int64_t)c->min_wg * chunk) {
-                int64_t ch = 4096;
-                while (2 * ch <= bytes / c->min_wg && 2 * ch <= c->chunk) ch *= 2;
-                chunk = std::min(c->chunk, ch);
-            }
-            return;
-        }
         if (!c->balance) return;
         std::vector<int64_t> lens;
         for (const auto &rg : ranges)

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: the XG_COPY_MIN_WG rule was measured slower and removed after this A/B; run it at commit daa5908 or earlier)
 # Piece size of small copy launches (XG_COPY_MIN_WG): standalone copy launches of m1 / m2 at
 # P32 A14 (one launch of 448 x d per -k repetition; step engine off, so every repetition is a
 # copy launch) for d = 8 KiB .. 128 KiB (3.5 .. 56 MiB per launch), rocprofv3 kernel durations

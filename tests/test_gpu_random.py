@@ -10,9 +10,14 @@ solo rails, grid engine, chains, single launches) and as virtual 2/3/4/8-GPU job
 (packed and direct cross-GPU segments).  Schedules the step compiler proves deadlocked
 under the reference's MPI (XG_ESCHED) are skipped, as the reference would hang there.
 """
+import os
 import random
 
 import pytest
+
+# XG_RANDOM_N1 / XG_RANDOM_NV: widen the sweep (one GPU / virtual jobs) for an evidence run
+N1 = int(os.environ.get("XG_RANDOM_N1", 120))
+NV = int(os.environ.get("XG_RANDOM_NV", 60))
 
 pytestmark = pytest.mark.gpu
 
@@ -64,7 +69,7 @@ def ctx(xg):
     c.close()
 
 
-@pytest.mark.parametrize("cfg", _configs(2026, 120), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
+@pytest.mark.parametrize("cfg", _configs(2026, N1), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
 def test_random_config_one_gpu(xg, ctx, cfg):
     s, rl = _schedule(xg, cfg)
     run = xg.MethodRun(ctx, s, it=cfg[-1], mode=1)
@@ -107,7 +112,7 @@ def worlds(xg):
             c.close()
 
 
-@pytest.mark.parametrize("cfg", _configs(7, 60), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
+@pytest.mark.parametrize("cfg", _configs(7, NV), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
 def test_random_config_virtual_gpus(xg, worlds, cfg):
     rng = random.Random(hash(cfg) & 0xffff)
     G = rng.choice([2, 3, 4, 8])
