@@ -1105,17 +1105,21 @@ static bool touches_unpacked(const xg_devplan *dp, int s)
 {
     const xg_stepplan &pv = dp->steps[s - 1], &sp = dp->steps[s];
     std::vector<std::pair<int64_t, int64_t>> w[XG_NBUF];      // unpack destinations [off, end)
+    std::vector<int64_t> reach[XG_NBUF];                       // running max of the ends, in start order
     for (int i = 0; i < pv.post_count; ++i) {
         const xg_copy &c = dp->copies[pv.post_begin + i];
         if (c.len > 0) w[c.dst_buf].push_back({c.dst_off, c.dst_off + c.len});
     }
-    for (auto &v : w) std::sort(v.begin(), v.end());
+    for (int k = 0; k < XG_NBUF; ++k) {
+        std::sort(w[k].begin(), w[k].end());
+        int64_t m = INT64_MIN;
+        for (const auto &iv : w[k]) reach[k].push_back(m = std::max(m, iv.second));
+    }
     auto hit = [&](int buf, int64_t a, int64_t b) {
+        // [a, b) meets an unpack interval iff some interval starting before b ends after a
         const auto &v = w[buf];
-        auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(b, (int64_t)0));
-        // intervals starting before b: the one just before may reach past a (they do not
-        // overlap each other: every unpack writes its own slot)
-        return it != v.begin() && std::prev(it)->second > a;
+        const size_t n = std::lower_bound(v.begin(), v.end(), std::make_pair(b, (int64_t)INT64_MIN)) - v.begin();
+        return n > 0 && reach[buf][n - 1] > a;
     };
     for (int i = sp.stage_count; i < sp.pre_count; ++i) {
         const xg_copy &c = dp->copies[sp.pre_begin + i];
