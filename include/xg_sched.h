@@ -290,6 +290,10 @@ void xg_solo_reduce_stamps(const uint64_t *stamps, int rails, int64_t stride, in
  * chunk/2, ... >= 4 KiB (16-B multiples), the one whose busiest CU -- ceil(pieces / cus)
  * pieces of (size + wg_cost) bytes -- has the least work; ties keep the larger (pieces.c). */
 int64_t xg_piece_size(const int64_t *lens, int n, int64_t chunk, int cus, int64_t wg_cost);
+/* 1 if a local gather/scatter copy of step s (after its stage copies, before its packs)
+ * reads or writes bytes that step s-1's unpacks write -- then the two may not share one copy
+ * launch; 0 if they may; -1 for a bad step (pieces.c). */
+int xg_step_local_meets_unpacks(const xg_devplan *dp, int s);
 
 /* fill: `nsegs` consecutive d-byte segments at `off` in the SEND region,
  * segment i = fingerprint(rank, seed0 + i, iter) (prepare_*_data loops). */

@@ -1099,37 +1099,6 @@ static int run_displ_scan(xg_plan *p, DisplScan &ds)
 extern "C" int xg_plan_free(xg_plan *p);
 static int launch_dispatches(const xg_plan *p, int b, int n, int64_t bytes);
 
-// Does any local copy of step s read or write bytes that step s-1's unpacks write?  (Then
-// they cannot share one launch: its workgroups run in any order.)  Intervals per region.
-static bool touches_unpacked(const xg_devplan *dp, int s)
-{
-    const xg_stepplan &pv = dp->steps[s - 1], &sp = dp->steps[s];
-    std::vector<std::pair<int64_t, int64_t>> w[XG_NBUF];      // unpack destinations [off, end)
-    std::vector<int64_t> reach[XG_NBUF];                       // running max of the ends, in start order
-    for (int i = 0; i < pv.post_count; ++i) {
-        const xg_copy &c = dp->copies[pv.post_begin + i];
-        if (c.len > 0) w[c.dst_buf].push_back({c.dst_off, c.dst_off + c.len});
-    }
-    for (int k = 0; k < XG_NBUF; ++k) {
-        std::sort(w[k].begin(), w[k].end());
-        int64_t m = INT64_MIN;
-        for (const auto &iv : w[k]) reach[k].push_back(m = std::max(m, iv.second));
-    }
-    auto hit = [&](int buf, int64_t a, int64_t b) {
-        // [a, b) meets an unpack interval iff some interval starting before b ends after a
-        const auto &v = w[buf];
-        const size_t n = std::lower_bound(v.begin(), v.end(), std::make_pair(b, (int64_t)INT64_MIN)) - v.begin();
-        return n > 0 && reach[buf][n - 1] > a;
-    };
-    for (int i = sp.stage_count; i < sp.pre_count; ++i) {
-        const xg_copy &c = dp->copies[sp.pre_begin + i];
-        if (c.dst_buf == XG_BUF_STAGE_SEND) break;
-        if (c.len > 0 && (hit(c.src_buf, c.src_off, c.src_off + c.len) || hit(c.dst_buf, c.dst_off, c.dst_off + c.len)))
-            return true;
-    }
-    return false;
-}
-
 // Device half of a plan load: the piece table, the step events, the displacement scan
 // and the engine segments.  On an error the caller frees the plan (xg_plan_free takes a
 // half-loaded one: every handle starts null).
@@ -1280,7 +1249,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.deferred = false;
         const bool prev_ok = c->fuse_unpack && s > 0 && npack > 0 && sp.stage_count == 0 &&
                              !p->steps[s - 1].sync_after && dp->steps[s - 1].post_count > 0;
-        st.fused = prev_ok && (st.split || nloc == 0 || !touches_unpacked(dp, s));
+        st.fused = prev_ok && (st.split || nloc == 0 || !xg_step_local_meets_unpacks(dp, s));
         st.fused_local = st.fused && !st.split && nloc > 0;
         if (st.fused) p->steps[s - 1].deferred = true;
     }

@@ -158,6 +158,7 @@ def host():
         h.xg_devplans_match.restype = C.c_int64
         h.xg_devplans_match.argtypes = [C.POINTER(C.POINTER(DevPlan)), C.c_int, C.c_int64, C.POINTER(CallPair),
                                         C.c_int64, C.c_char_p, C.c_size_t]
+        h.xg_step_local_meets_unpacks.argtypes = [C.POINTER(DevPlan), C.c_int]
         h.xg_piece_size.restype = C.c_int64
         h.xg_piece_size.argtypes = [C.POINTER(C.c_int64), C.c_int, C.c_int64, C.c_int, C.c_int64]
         h.xg_fill_runs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(SegRun)]
@@ -432,6 +433,10 @@ class DevicePlanView:
     @property
     def ptr(self):
         return self._p
+
+    def local_meets_unpacks(self, step):
+        """xg_step_local_meets_unpacks: may step's local copies share a launch with step-1's unpacks?"""
+        return host().xg_step_local_meets_unpacks(self._p, step)
 
     def calls(self, step, self_max=0):
         """xg_devplan_step_calls: [(kind, peer, buf, off, len)] this GPU posts in `step`"""

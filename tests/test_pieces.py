@@ -28,3 +28,63 @@ def test_rule_against_brute_force(xg):
                 best, bc = v, c
             c //= 2
         assert xg.piece_size(lens, chunk, cus, cost) == bc
+
+
+def _plan(xg, steps):
+    """a hand-made xg_devplan: steps = [(stage, local, packs, unpacks)], each a list of
+    (src_buf, src_off, dst_buf, dst_off, len)"""
+    import ctypes as C
+    copies, sp, posts = [], [], []
+    for stage, local, packs, _unp in steps:
+        b = len(copies)
+        copies += stage + local + packs
+        sp.append([b, len(stage) + len(local) + len(packs), 0, 0, 0, 0, 0, len(stage)])
+    for i, (_s, _l, _p, unp) in enumerate(steps):
+        sp[i][4], sp[i][5] = len(copies), len(unp)
+        copies += unp
+    arr = (xg.Copy * max(1, len(copies)))(*[xg.Copy(so, do, n, sb, db) for sb, so, db, do, n in copies])
+    st = (xg.StepPlan * len(sp))(*[xg.StepPlan(*x) for x in sp])
+    dp = xg.DevPlan()
+    dp.gpu, dp.ngpus, dp.nsteps = 0, 2, len(sp)
+    dp.ncopy, dp.np2p = len(copies), 0
+    dp.copies = C.cast(arr, C.POINTER(xg.Copy))
+    dp.steps = C.cast(st, C.POINTER(xg.StepPlan))
+    dp._keep = (arr, st)
+    return dp
+
+
+def test_local_meets_unpacks(xg):
+    import ctypes as C
+    S, R, SS, SR = xg.BUF_SEND, xg.BUF_RECV, xg.BUF_STAGE_SEND, xg.BUF_STAGE_RECV
+    unp = [(SR, 0, R, 1000, 100), (SR, 100, R, 5000, 50)]           # step 0 writes RECV [1000,1100), [5000,5050)
+    cases = [
+        ([(S, 0, R, 2000, 64)], 0),              # disjoint
+        ([(S, 0, R, 1099, 1)], 1),               # writes the last byte an unpack writes
+        ([(S, 0, R, 900, 100)], 0),              # ends exactly where the unpack starts
+        ([(R, 5049, S, 0, 8)], 1),               # reads a byte an unpack writes
+        ([(S, 0, R, 4000, 1001)], 1),            # covers a whole unpack
+        ([(S, 0, R, 0, 16), (S, 16, R, 1050, 4)], 1),
+    ]
+    for local, want in cases:
+        dp = _plan(xg, [([], [], [(S, 0, SS, 0, 150)], unp), ([], local, [(S, 0, SS, 0, 8)], [])])
+        assert xg.host().xg_step_local_meets_unpacks(C.byref(dp), 1) == want, (local, want)
+    dp = _plan(xg, [([], [], [], unp)])
+    assert xg.host().xg_step_local_meets_unpacks(C.byref(dp), 0) == -1
+
+
+def test_real_plans_never_meet_their_unpacks(xg):
+    """every golden-shape plan on 2 and 8 GPUs, packed: no local copy touches the previous
+    step's unpacked bytes (so the fused launch may take a small local part)"""
+    from conftest import golden_configs, load_golden
+    for cfg in golden_configs():
+        meta, _, _ = load_golden(cfg)
+        for m in meta["method_list"]:
+            s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], meta["aggregators"], ntimes=meta["ntimes"],
+                            proc_node=meta["proc_node"], barrier_type=meta["barrier"])
+            for G in (2, 8):
+                if G > meta["P"]:
+                    continue
+                for g in range(G):
+                    v = s.devplan(G, g, 1 << 30)
+                    for st in range(1, v.nsteps):
+                        assert v.local_meets_unpacks(st) == 0, (cfg, m, G, g, st)
