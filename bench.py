@@ -359,6 +359,17 @@ def main():
     ctx.barrier()
     if rdzv:
         os.unlink(rdzv)
+    if world > 1:
+        # every rank plans every GPU's RCCL calls from its own arguments: ranks started with
+        # different ones would post calls nobody pairs and hang in RCCL -- compare first
+        import hashlib
+        keys = sorted(k for k in os.environ if k.startswith("XG_") and k not in ("XG_RDZV_KEY", "XG_DEVICE"))
+        blob = repr((vars(a), [(k, os.environ[k]) for k in keys])).encode()
+        h = int.from_bytes(hashlib.sha256(blob).digest()[:8], "little")
+        parts = [float((h >> (16 * i)) & 0xffff) for i in range(4)]
+        got = ctx.allreduce_max(parts + [-x for x in parts])
+        if any(got[i] != -got[4 + i] for i in range(4)):
+            raise SystemExit("bench: the ranks were started with different arguments or XG_* settings")
     if a.copy_variant >= 0 or a.chunk:
         ctx.set_copy_params(a.chunk, a.copy_variant)
     arch, cus, hbm = ctx.info()

@@ -7,6 +7,7 @@
  */
 #include <stdio.h>
 #include <stdlib.h>
+#include <stdint.h>
 #include <string.h>
 
 #include "xg.h"
@@ -42,6 +43,45 @@ static int pairing_ok(const xg_sched *s, int G, int64_t pack_max_seg, int64_t pa
     return ok;
 }
 
+/* Every GPU of a job must plan from the same inputs: each derives every GPU's RCCL calls from
+ * them, and a rank that planned from others would post calls nobody pairs -- the job would
+ * hang in RCCL.  Before anything that could diverge (a schedule refused on one rank only), the
+ * ranks compare a digest of the inputs (FNV-1a, in four 16-bit parts: exact as doubles) by one
+ * MAX reduction of the parts and their negations; unequal inputs fail alike on every rank. */
+static uint64_t fnv(uint64_t h, const void *p, size_t n)
+{
+    const unsigned char *b = (const unsigned char *)p;
+    size_t i;
+    for (i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+
+static int inputs_agree(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list,
+                        int comm_size, int iter, int ntimes, const xg_run_opts *o, char *err, size_t errlen)
+{
+    int64_t v[12];
+    double red[8];
+    uint64_t h = 0xcbf29ce484222325ull;
+    int i, rc;
+    v[0] = method; v[1] = procs; v[2] = cb_nodes; v[3] = data_size; v[4] = comm_size; v[5] = iter;
+    v[6] = ntimes; v[7] = o->eager_limit; v[8] = o->pack_max_seg; v[9] = o->pack_min_bytes;
+    v[10] = o->proc_node; v[11] = o->barrier_type;
+    h = fnv(h, v, sizeof v);
+    h = fnv(h, rank_list, sizeof(int) * (size_t)cb_nodes);
+    for (i = 0; i < 4; ++i) {
+        red[i] = (double)((h >> (16 * i)) & 0xffff);
+        red[4 + i] = -red[i];
+    }
+    if ((rc = xg_allreduce_max(ctx, red, 8))) return rc;
+    for (i = 0; i < 4; ++i)
+        if (red[i] != -red[4 + i]) {
+            snprintf(err, errlen, "the GPU processes planned method %d from different inputs (arguments or "
+                     "options differ between ranks)", method);
+            return XG_EARG;
+        }
+    return XG_OK;
+}
+
 int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list,
                   int comm_size, xg_timer *timers, int iter, int ntimes, const xg_run_opts *opts,
                   int64_t *bad_slots, char *err, size_t errlen)
@@ -61,6 +101,9 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
     if (!opts) { xg_run_opts_default(&dflt); opts = &dflt; }
     if (!err) { err = ebuf; errlen = sizeof ebuf; }
     if (bad_slots) *bad_slots = 0;
+    if (G > 1 && (rc = inputs_agree(ctx, method, procs, cb_nodes, data_size, rank_list, comm_size, iter, ntimes, opts,
+                                    err, errlen)))
+        return rc;
     s = xg_sched_build_iter(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, opts->proc_node,
                             opts->barrier_type, opts->eager_limit, iter, err, errlen);
     if (!s) return XG_ESCHED;

@@ -214,3 +214,19 @@ def test_self_calls_carry_the_local_part(xg, cfg):
                             [t for cp in local for t in ((1, cp[0], cp[1], cp[4]), (2, cp[2], cp[3], cp[4]))]
                         assert [x for x in c if x[0] == 3 or x[1] != g] == v.calls(st)   # cross calls + barrier as before
                         assert not own or c.index(own[0]) == len(v.calls(st)) - v.sync_after[st]   # after the cross calls
+
+
+def test_bench_ranks_with_different_arguments_refuse_alike(tmp_path):
+    """ranks started with different arguments would plan different RCCL calls and hang: every
+    rank compares a digest of its arguments (one MAX reduction) and all stop with the reason"""
+    key = "calls_args_%s" % tmp_path.name
+    procs = []
+    for r, steps in ((0, "2"), (1, "3")):
+        argv = ["--gpus", "2", "--steps", steps, "--warmup", "1", "--no-cpu-baseline", "--watchdog", "120"]
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", XG_RDZV_KEY=key,
+                   XG_FAKE_BARRIER_DIR=str(tmp_path))
+        procs.append(subprocess.Popen([sys.executable, "-c", DRIVER.format(repo=REPO, argv=argv)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (_o, e) in zip(procs, outs):
+        assert p.returncode != 0 and "different arguments" in e, e[-2000:]
