@@ -215,6 +215,34 @@ int main(int argc, char **argv)
     ngpu_dev = device;
     XGCALL(xg_init(&ctx, rank, nranks, ngpu_dev, uid));
     XGCALL(xg_barrier(ctx));
+    if (nranks > 1) {
+        /* every process plans every GPU's RCCL calls from its own command line: processes
+         * started with different ones would post calls nobody pairs and hang -- compare a
+         * digest (FNV-1a of argv and the planning settings, in 16-bit parts) first */
+        static const char *keys[] = {"XG_PROCS", "XG_VERIFY", "XG_FINGERPRINT", "XG_EAGER_LIMIT", "XG_PACK_MAX_SEG",
+                                     "XG_PACK_MIN", NULL};
+        uint64_t h = 0xcbf29ce484222325ull;
+        double red[8];
+        int k;
+        for (k = 1; k <= argc; ++k) {
+            const char *str = k < argc ? argv[k] : "";
+            size_t j, n = strlen(str) + 1;
+            for (j = 0; j < n; ++j) h = (h ^ (unsigned char)str[j]) * 0x100000001b3ull;
+        }
+        for (k = 0; keys[k]; ++k) {
+            const char *v = getenv(keys[k]);
+            size_t j, n = v ? strlen(v) + 1 : 0;
+            for (j = 0; j < n; ++j) h = (h ^ (unsigned char)v[j]) * 0x100000001b3ull;
+            h = (h ^ (unsigned char)(k + 1)) * 0x100000001b3ull;
+        }
+        for (k = 0; k < 4; ++k) {
+            red[k] = (double)((h >> (16 * k)) & 0xffff);
+            red[4 + k] = -red[k];
+        }
+        XGCALL(xg_allreduce_max(ctx, red, 8));
+        for (k = 0; k < 4; ++k)
+            if (red[k] != -red[4 + k]) DIE("the GPU processes were started with different arguments or settings");
+    }
     if (rank == 0 && rdzv_path[0]) unlink(rdzv_path);
 
     o.P = procs; o.A = cb_nodes; o.d = data_size; o.c = comm_size; o.ntimes = ntimes; o.type = aggregator_type;
