@@ -520,16 +520,31 @@ extern "C" int xg_init_virtual(xg_ctx **out, int rank, int nranks, int device)
 extern "C" int xg_finalize(xg_ctx *c)
 {
     if (!c) return XG_OK;
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->comm) NCCLCHK(ncclCommDestroy(c->comm));
-    for (auto &e : c->kev) HIPCHK(hipEventDestroy(e));
-    HIPCHK(hipFree(c->d_red));
-    HIPCHK(hipStreamSynchronize(c->side));
-    HIPCHK(hipStreamDestroy(c->side));
-    HIPCHK(hipStreamDestroy(c->stream));
+    // release everything even after an error; report the first
+    int rc = XG_OK;
+    auto keep = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == XG_OK) {
+            fprintf(stderr, "xg: HIP error %s in xg_finalize (%s)\n", hipGetErrorString(e), what);
+            rc = XG_EHIP;
+        }
+    };
+    keep(hipSetDevice(c->device), "hipSetDevice");
+    keep(hipStreamSynchronize(c->stream), "stream");
+    keep(hipStreamSynchronize(c->side), "side stream");
+    if (c->comm) {
+        const ncclResult_t r = ncclCommDestroy(c->comm);
+        if (r != ncclSuccess && rc == XG_OK) {
+            fprintf(stderr, "xg: RCCL error %s in ncclCommDestroy\n", ncclGetErrorString(r));
+            rc = XG_ERCCL;
+        }
+    }
+    for (auto &e : c->kev) keep(hipEventDestroy(e), "event");
+    keep(hipFree(c->d_red), "scratch");
+    keep(hipStreamDestroy(c->side), "side stream");
+    keep(hipStreamDestroy(c->stream), "stream");
+    (void)hipGetLastError();
     delete c;
-    return XG_OK;
+    return rc;
 }
 
 extern "C" int xg_rank(const xg_ctx *c) { return c->rank; }
