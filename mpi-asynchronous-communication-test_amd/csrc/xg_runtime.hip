@@ -366,6 +366,8 @@ extern "C" int xg_get_unique_id(void *uid)
     return XG_OK;
 }
 
+static int init_ctx(xg_ctx *c, const void *uid);
+
 extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const void *uid)
 {
     int ndev = 0;
@@ -384,6 +386,21 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
     HIPCHK(hipSetDevice(device));
     xg_ctx *c = new xg_ctx();
     c->rank = rank; c->nranks = nranks; c->device = device; c->comm = nullptr; c->virt = false;
+    c->stream = c->side = nullptr; c->d_red = nullptr;
+    const int rc = init_ctx(c, uid);
+    if (rc) {
+        xg_finalize(c);                     // frees what init_ctx got to
+        return rc;
+    }
+    *out = c;
+    return XG_OK;
+}
+
+// the rest of xg_init: tuning knobs, streams, scratch, the communicator
+static int init_ctx(xg_ctx *c, const void *uid)
+{
+    const int device = c->device, rank = c->rank, nranks = c->nranks;
+    (void)rank;
     c->chunk = 32768; c->variant = 0; c->kt_mode = 0; c->nk = 0; c->kt_bytes = 0;   // profiles/r01_copy_ab.txt
     const char *env = getenv("XG_COPY_CHUNK");
     if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
@@ -494,7 +511,6 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
         NCCLCHK(ncclGetUniqueId(&id));
         NCCLCHK(ncclCommInitRank(&c->comm, 1, id, 0));
     }
-    *out = c;
     return XG_OK;
 }
 
@@ -529,8 +545,8 @@ extern "C" int xg_finalize(xg_ctx *c)
         }
     };
     keep(hipSetDevice(c->device), "hipSetDevice");
-    keep(hipStreamSynchronize(c->stream), "stream");
-    keep(hipStreamSynchronize(c->side), "side stream");
+    if (c->stream) keep(hipStreamSynchronize(c->stream), "stream");
+    if (c->side) keep(hipStreamSynchronize(c->side), "side stream");
     if (c->comm) {
         const ncclResult_t r = ncclCommDestroy(c->comm);
         if (r != ncclSuccess && rc == XG_OK) {
@@ -539,9 +555,9 @@ extern "C" int xg_finalize(xg_ctx *c)
         }
     }
     for (auto &e : c->kev) keep(hipEventDestroy(e), "event");
-    keep(hipFree(c->d_red), "scratch");
-    keep(hipStreamDestroy(c->side), "side stream");
-    keep(hipStreamDestroy(c->stream), "stream");
+    if (c->d_red) keep(hipFree(c->d_red), "scratch");
+    if (c->side) keep(hipStreamDestroy(c->side), "side stream");
+    if (c->stream) keep(hipStreamDestroy(c->stream), "stream");
     (void)hipGetLastError();
     delete c;
     return rc;
