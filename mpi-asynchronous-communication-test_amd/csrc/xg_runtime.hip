@@ -127,7 +127,7 @@ struct xg_ctx {
     int64_t split_min;         // ... when it moves >= this many bytes (smaller: in the pack / fused launch)
     int64_t self_max;          // a cross-GPU step's local part of <= this many bytes goes in its RCCL group
     int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
-    int graph;                 // 1: multi-step runs are captured once into a hipGraph and replayed (XG_GRAPH)
+    int graph;                 // hipGraph replay of multi-launch runs: 1 always, 0 never, -1 latency-bound one-GPU runs
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
     int64_t nt_min;         // variant 0: launches moving >= this many bytes use non-temporal loads/stores
@@ -239,6 +239,7 @@ struct xg_plan {
     // writes the wall clock to d_gstamp[i + 1] (i = -1: the start) where it would record ev[i]
     unsigned long long *d_gstamp;
     bool stamp_marks;              // mark() stamps (graph capture) instead of recording events
+    bool graph_auto;               // XG_GRAPH unset: this plan replays as a graph (latency-bound, one GPU)
     uint64_t id;                   // unique per loaded plan (keys the virtual runner's graphs)
     struct VGraph {
         std::vector<uint64_t> ids;
@@ -486,8 +487,10 @@ static int init_ctx(xg_ctx *c, const void *uid)
     c->self_max = env ? atoll(env) : (int64_t)256 << 10;
     env = getenv("XG_FUSE_UNPACK");          // "0": unpacks and the next step's packs apart
     c->fuse_unpack = !(env && !strcmp(env, "0"));
-    env = getenv("XG_GRAPH");                // "1": replay captured runs (hipGraph)
-    c->graph = env && !strcmp(env, "1");
+    // hipGraph replay: "1" every multi-launch run (and virtual job), "0" never; default (-1):
+    // one-GPU latency-bound runs only (xg_plan.graph_auto)
+    env = getenv("XG_GRAPH");
+    c->graph = env ? (!strcmp(env, "1") ? 1 : 0) : -1;
     {
         int khz = 0;
         HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
@@ -1150,7 +1153,7 @@ static int plan_upload(xg_plan *p, const std::vector<xgk::DCopy> &pieces, DisplS
             HIPCHK(hipEventCreateWithFlags(&p->join[s], hipEventDisableTiming));
         }
     HIPCHK(hipEventCreate(&p->ev0));
-    if (p->ctx->graph) HIPCHK(hipMalloc(&p->d_gstamp, 8 * ((size_t)p->nsteps + 1)));
+    if (p->ctx->graph) HIPCHK(hipMalloc(&p->d_gstamp, 8 * ((size_t)p->nsteps + 1)));   // 1 or auto
     if ((rc = run_displ_scan(p, ds)) || (rc = build_segments(p, pieces))) return rc;
     return XG_OK;
 }
@@ -1176,7 +1179,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
     p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1; p->d_cstamp = nullptr;
     p->g_enq = p->g_run = nullptr; p->id = next_plan_id(); p->vg.rccl = false; p->vg.exec = nullptr;
-    p->d_gstamp = nullptr; p->stamp_marks = false;
+    p->d_gstamp = nullptr; p->stamp_marks = false; p->graph_auto = false;
     // One piece per workgroup.  Bytes per piece, per launch (launch_chunk over the launch's
     // copies): c->chunk (32 KiB: profiles/r01_copy_ab.txt) or c->chunk / 2, / 4, / 8 (>= 4 KiB;
     // a halving keeps dividing the power-of-two segment sizes: no ragged tail piece per segment,
@@ -1419,6 +1422,11 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         int64_t run = 0;
         for (const StepR &st : p->steps) run += st.stage_bytes + st.local_bytes + st.pack_bytes + st.post_bytes;
         p->streaming = 2 * run > ((int64_t)256 << 20);
+        // a one-GPU run of several small launches is bound by launching them, not by their
+        // bytes: replayed as one graph (README TAM chains 17-19 -> 15-16 us,
+        // profiles/r03/readme_cli/summary.txt).  Multi-GPU and virtual runs stay launched:
+        // graphs of RCCL and cross-stream nodes replayed 1.1-5x slower (profiles/r03/hybrid/)
+        p->graph_auto = c->nranks == 1 && !c->virt && run <= ((int64_t)16 << 20);
     }
     p->chain_end.assign(p->nsteps, 0);
     if (c->step_chain) {
@@ -1897,7 +1905,8 @@ static int enqueue_run(xg_plan *p, double *step_post)
 // events are host bookkeeping), and a plan of more than one launch
 static bool use_graph(const xg_plan *p)
 {
-    return p->ctx->graph && !p->ctx->kt_mode && p->nlaunch > 1;
+    const int g = p->ctx->graph;
+    return (g == 1 || (g < 0 && p->graph_auto)) && !p->ctx->kt_mode && p->nlaunch > 1 && p->d_gstamp;
 }
 
 extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
@@ -2092,7 +2101,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
         }
         return XG_OK;
     };
-    if (c0->graph && !c0->kt_mode) {
+    if (c0->graph == 1 && !c0->kt_mode) {
         // XG_GRAPH=1: the job captured once (per set of plans and transport) and replayed
         std::vector<uint64_t> ids(n);
         for (int g = 0; g < n; ++g) ids[g] = plans[g]->id;
@@ -2119,7 +2128,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
     for (int g = 0; g < n; ++g)
         if ((rc = xg_plan_check(plans[g]))) return rc;
     if (step_done) {
-        const bool graph = c0->graph && !c0->kt_mode;
+        const bool graph = c0->graph == 1 && !c0->kt_mode;
         std::vector<unsigned long long> gs;
         if (graph) {
             gs.resize((size_t)nst + 1);
