@@ -7,7 +7,7 @@
 #               started by the host's doorbell ring (the launch stays outside the time)
 #   grid_launch XG_ENGINE_SOLO=0 (grid-barrier engine), launched
 #   copy1       XG_SOLO_MIN_STEPS=2: a one-step plan runs as an event-timed copy launch
-#   graph       XG_GRAPH=1: multi-launch plans (TAM chains) captured once and replayed
+#   nograph     XG_GRAPH=0: launch-bound one-GPU runs (TAM chains) launched, not replayed as a graph
 # usage: profiles/chain_modes.sh <outdir> [reps]
 out=${1:-gpurun_out/chain}; reps=${2:-3}; mkdir -p $out
 args="-a 14 -d 2048 -c 3 -m 0 -i 2 -k 1"
@@ -18,7 +18,7 @@ for r in $(seq 1 $reps); do
   XG_ENGINE_ARM=1 timeout -k 10 120 $bin --procs 32 $args > armed_$r.txt 2>> err.txt || exit 1
   XG_ENGINE_SOLO=0 timeout -k 10 120 $bin --procs 32 $args > grid_launch_$r.txt 2>> err.txt || exit 1
   XG_SOLO_MIN_STEPS=2 timeout -k 10 120 $bin --procs 32 $args > copy1_$r.txt 2>> err.txt || exit 1
-  XG_GRAPH=1 timeout -k 10 120 $bin --procs 32 $args > graph_$r.txt 2>> err.txt || exit 1
+  XG_GRAPH=0 timeout -k 10 120 $bin --procs 32 $args > nograph_$r.txt 2>> err.txt || exit 1
 done
 if [ -x $repo/oracle/_ref/test ] && [ -z "$NOREF" ]; then
   for r in $(seq 1 $reps); do

@@ -20,7 +20,7 @@ def parse(path):
 
 
 def main(d):
-    modes = [m for m in ["launch", "armed", "grid_launch", "copy1", "graph", "solo_armed", "solo1_armed", "grid_armed",
+    modes = [m for m in ["launch", "armed", "grid_launch", "copy1", "graph", "nograph", "solo_armed", "solo1_armed", "grid_armed",
                          "solo_launch"] if glob.glob(os.path.join(d, m + "_*.txt"))]
     runs = {m: [parse(f) for f in sorted(glob.glob(os.path.join(d, m + "_*.txt")))] for m in modes}
     refs = [parse(f) for f in sorted(glob.glob(os.path.join(d, "ref*.txt")))]   # ref.txt or ref_<r>.txt
