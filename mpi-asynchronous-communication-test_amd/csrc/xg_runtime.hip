@@ -1923,7 +1923,10 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
         p->stamp_marks = true;
         rc = capture(c->stream, &p->g_run, [&] { return enqueue_run(p, nullptr); });
         p->stamp_marks = false;
-        if (rc) return rc;
+        if (rc) {
+            p->engine_reset = true;      // the host's ticket base moved for launches that never ran
+            return rc;
+        }
     }
     const bool graph = p->g_run && use_graph(p);
     const double t0 = xg_now();
@@ -1990,7 +1993,10 @@ extern "C" int xg_plan_enqueue(xg_plan *p)
     if (!use_graph(p)) return body();
     if (!p->g_enq) {
         p->engine_reset = true;
-        if ((rc = capture(p->ctx->stream, &p->g_enq, body))) return rc;
+        if ((rc = capture(p->ctx->stream, &p->g_enq, body))) {
+            p->engine_reset = true;      // the host's ticket base moved for launches that never ran
+            return rc;
+        }
     }
     HIPCHK(hipGraphLaunch(p->g_enq, p->ctx->stream));
     return XG_OK;
@@ -2115,7 +2121,10 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
                 plans[g]->stamp_marks = true;      // step boundaries as stamps in the graph
             }
             rc = capture(st, &vg.exec, body);
-            for (int g = 0; g < n; ++g) plans[g]->stamp_marks = false;
+            for (int g = 0; g < n; ++g) {
+                plans[g]->stamp_marks = false;
+                if (rc) plans[g]->engine_reset = true;   // ticket bases moved for launches that never ran
+            }
             if (rc) return rc;
             vg.ids = ids;
             vg.rccl = rccl;
