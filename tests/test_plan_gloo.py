@@ -1,6 +1,9 @@
 """world_size-2 run of the multi-GPU exchange on CPU: each process executes its
-GPU's device plan on numpy regions and moves every p2p op with torch.distributed
-(gloo), in the same per-peer issue order RCCL matches on.  Same bytes as the oracle."""
+GPU's device plan on numpy regions and posts exactly the calls the runtime posts
+(xg_devplan_step_calls: cross-GPU sends/receives with torch.distributed (gloo) in the
+per-peer issue order RCCL matches on, self send/recv pairs as local copies, the in-loop
+barrier as dist.barrier), with and without the local part in the group (self_max).
+Same bytes as the oracle."""
 import os
 import socket
 
@@ -41,20 +44,29 @@ def _worker(rank, world, port, results):
                                    (16, 5, 24, 3, 1, 16)]:
             rl = xg.aggregator_list(P, A)
             s = xg.Schedule(m, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2, iteration=2)
-            for pack in (0, 1 << 20):
+            for pack, self_max in ((0, 0), (1 << 20, 0), (0, 1 << 30), (1 << 20, 1 << 30)):
                 v = s.devplan(world, rank, pack)
                 reg = make_regions(s, v, world, rank, 2, 1)
                 seq = {}
                 for st in range(v.nsteps):
-                    stage, pre, p2p, post = step_parts(v, st)
+                    stage, pre, _p2p, post = step_parts(v, st)
+                    # exactly the calls the runtime posts (xg_devplan_step_calls): with self_max the
+                    # step's local copies travel in the group as self send/recv pairs instead
+                    calls = v.calls(st, self_max)
+                    selfs = [c for c in calls if c[0] != 3 and c[1] == rank]
                     copies(reg, stage)
-                    copies(reg, pre)
+                    copies(reg, [cp for cp in pre if cp[2] == 2] if selfs else pre)   # packs only
                     reqs, bufs = [], []
-                    for peer, is_send, buf, off, ln in p2p:
-                        key = (peer, is_send)
+                    for (s_kind, _, sb, so, sl), (r_kind, _, rb, ro, rl_) in zip(selfs[0::2], selfs[1::2]):
+                        assert (s_kind, r_kind) == (1, 2) and sl == rl_      # send then receive, one copy
+                        bufs.append((torch.from_numpy(reg[sb][so:so + sl].copy()), rb, ro, rl_))
+                    for kind, peer, buf, off, ln in calls:
+                        if kind == 3 or peer == rank:
+                            continue
+                        key = (peer, kind == 1)
                         tag = seq.get(key, 0)
                         seq[key] = tag + 1
-                        if is_send:
+                        if kind == 1:
                             t = torch.from_numpy(reg[buf][off:off + ln].copy())
                             reqs.append(dist.isend(t, dst=peer, tag=tag))
                         else:
@@ -66,6 +78,8 @@ def _worker(rank, world, port, results):
                     for t, buf, off, ln in bufs:
                         reg[buf][off:off + ln] = t.numpy()
                     copies(reg, post)
+                    if calls and calls[-1][0] == 3:                # the step's in-loop barrier
+                        dist.barrier()
                 exp = O.expected_recv(m, P, A, d, rl, 2, 1)
                 lo, hi = s.block_range(world, rank)
                 for r in range(lo, hi):
