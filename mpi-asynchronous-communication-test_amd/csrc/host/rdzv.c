@@ -79,7 +79,9 @@ int xg_env_int(const char *a, const char *b, int dflt)
     return v ? atoi(v) : dflt;
 }
 
-/* environment of child r: this process's, with the rank variables replaced */
+/* environment of child r: this process's, with the rank variables replaced (the last
+ * CHILD_VARS entries are its own: free_child_env releases them) */
+#define CHILD_VARS 5
 static char **child_env(int r, int n, const char *key)
 {
     size_t m = 0, i, k = 0;
@@ -102,6 +104,14 @@ static char **child_env(int r, int n, const char *key)
     return env;
 }
 
+static void free_child_env(char **env)
+{
+    size_t k = 0, i;
+    while (env[k]) k++;
+    for (i = k - CHILD_VARS; i < k; ++i) free(env[i]);
+    free(env);
+}
+
 int xg_spawn_ranks(int ngpus, char **argv)
 {
     pid_t *pid;
@@ -120,6 +130,7 @@ int xg_spawn_ranks(int ngpus, char **argv)
             failed = 1;
             worst = 1;
         }
+        free_child_env(env);
     }
     for (left = 0, r = 0; r < ngpus; ++r) left += pid[r] > 0;
     while (left > 0) {

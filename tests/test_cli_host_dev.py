@@ -1,0 +1,137 @@
+"""The CLI's multi-process path on the CPU: bin/test and bin/pt2pt_test built from their own
+sources (main.c / pt2pt.c, rdzv.c, methods.c and the host sources) against tests/host_dev.c, a
+CPU stand-in for the device half of the ABI that runs each device plan step by step and moves
+every call of xg_devplan_step_calls through files (RCCL's per-peer FIFO).  Under AddressSanitizer
+and UndefinedBehaviorSanitizer, with --gpus N the process spawns the N ranks itself, hands over
+the unique id, compares the argument digest, checks every method's RCCL pairing, runs the plans
+and reports -- exactly the code an N-GPU run executes above the device library.  Every received
+byte is verified against the reference's fingerprint (MAP_DATA, mpi_test.c:23, :71-77) or the
+strong one."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HOST = os.path.join(REPO, "mpi-asynchronous-communication-test_amd", "csrc", "host")
+HOST_SRCS = ["sched.c", "report.c", "hazard.c", "solo.c", "calls.c", "pieces.c"]
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all"]
+
+pytestmark = pytest.mark.skipif(not shutil.which("gcc"), reason="gcc not found")
+
+
+def _build(out, mains):
+    cmd = ["gcc", "-O1", "-g", *SAN, "-std=c99", "-D_POSIX_C_SOURCE=200809L", "-Wall", "-Wextra", "-Werror",
+           "-I", os.path.join(REPO, "include"), "-I", HOST, "-o", out,
+           *[os.path.join(HOST, m) for m in mains], os.path.join(REPO, "tests", "host_dev.c"),
+           *[os.path.join(HOST, s) for s in HOST_SRCS], "-lm"]
+    subprocess.run(cmd, check=True)
+    return out
+
+
+@pytest.fixture(scope="module")
+def exes(tmp_path_factory):
+    d = tmp_path_factory.mktemp("host_dev_bin")
+    return {"test": _build(str(d / "test"), ["main.c", "rdzv.c", "methods.c"]),
+            "pt2pt": _build(str(d / "pt2pt_test"), ["pt2pt.c", "rdzv.c"])}
+
+
+def _env(tmp_path, **kw):
+    env = {k: v for k, v in os.environ.items()
+           if not k.startswith("XG_") and k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PMI_RANK", "PMI_SIZE",
+                                                     "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    msg = tmp_path / "msgs"
+    msg.mkdir(parents=True, exist_ok=True)
+    env.update(XG_HOST_DEV_DIR=str(msg), XG_RDZV_DIR=str(tmp_path), XG_HOST_DEV_TIMEOUT="30",
+               ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="print_stacktrace=1")
+    env.update({k: str(v) for k, v in kw.items()})
+    return env
+
+
+def _run(exe, args, tmp_path, timeout=120, **env):
+    cwd = tmp_path / "cwd"
+    cwd.mkdir(parents=True, exist_ok=True)
+    return subprocess.run([exe, *map(str, args)], cwd=cwd, env=_env(tmp_path, **env), capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def _normalise(text):
+    """the report with every number that is a time or a rate blanked"""
+    return [re.sub(r"\d+\.\d+", "#", ln) for ln in text.splitlines()]
+
+
+ARGS = ["-m", 0, "-a", 3, "-d", 3000, "--procs", 7, "--verify"]
+
+
+@pytest.mark.parametrize("G", [2, 3, 4])
+@pytest.mark.parametrize("variant", ["default", "pack_all", "strong_k3", "barrier_k2", "no_self", "all_self"])
+def test_every_method_verifies_on_n_processes(exes, tmp_path, G, variant):
+    """-m 0 (all 20 methods) as G processes: every received byte right, the same report lines as
+    the one-process run (numbers aside)."""
+    extra, env = {"default": ([], {}), "pack_all": (["--pack-min", 0], {}),
+                  "strong_k3": (["--fingerprint", "strong", "-k", 3], {}), "barrier_k2": (["-b", 1, "-k", 2], {}),
+                  "no_self": ([], {"XG_SELF_MAX": 0}), "all_self": ([], {"XG_SELF_MAX": 1 << 30})}[variant]
+    p = _run(exes["test"], ARGS + extra + ["--gpus", G], tmp_path, **env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    ok = [ln for ln in p.stdout.splitlines() if "verify = OK" in ln]
+    assert len(ok) == 20 and "FAILED" not in p.stdout, p.stdout[-3000:]
+    one = _run(exes["test"], ARGS + extra, tmp_path / "one", **env)
+    assert one.returncode == 0, one.stderr[-3000:]
+    assert _normalise(p.stdout) == _normalise(one.stdout)
+
+
+def test_results_csv_and_timing_csvs_match_one_process(exes, tmp_path):
+    """results.csv (summarize_results, mpi_test.c:2068-2118) and m13's save_all_timing CSVs
+    (:2008-2066, gathered over the processes) have the one-process run's shape."""
+    args = ["-m", 13, "-a", 2, "-d", 2048, "--procs", 6, "-k", 3, "-r", "pre_"]
+    rows = {}
+    for G in (1, 3):
+        base = tmp_path / f"g{G}"
+        base.mkdir()
+        p = _run(exes["test"], args + ["--gpus", G], base)
+        assert p.returncode == 0, p.stderr[-3000:]
+        files = sorted(os.listdir(base / "cwd"))
+        rows[G] = {f: [len(ln.split(",")) for ln in open(base / "cwd" / f).read().splitlines()] for f in files}
+    assert rows[1] == rows[3] and "results.csv" in rows[1] and len(rows[1]) == 5, rows
+
+
+def test_corrupted_message_is_reported(exes, tmp_path):
+    p = _run(exes["test"], ["-m", 1, "-a", 3, "-d", 3000, "--procs", 7, "--verify", "--gpus", 2], tmp_path,
+             XG_HOST_DEV_CORRUPT=1)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "verify = FAILED" in p.stdout and "message is wrong" in p.stderr
+
+
+@pytest.mark.parametrize("differ", ["argv", "env"])
+def test_processes_started_differently_refuse(exes, tmp_path, differ):
+    """ranks launched by hand (RANK / WORLD_SIZE) with another -d or XG_PACK_MIN: both stop
+    before any exchange instead of posting calls nobody pairs"""
+    procs = []
+    for r in range(2):
+        d = 3000 if differ == "env" or r == 0 else 4000
+        env = _env(tmp_path, RANK=r, WORLD_SIZE=2, LOCAL_RANK=r, XG_RDZV_KEY="differ")
+        if differ == "env" and r == 1:
+            env["XG_PACK_MIN"] = "0"
+        (tmp_path / "cwd").mkdir(exist_ok=True)
+        procs.append(subprocess.Popen([exes["test"], "-m", "1", "-a", "3", "-d", str(d), "--procs", "7"],
+                                      cwd=tmp_path / "cwd", env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    for p in procs:
+        out, err = p.communicate(timeout=60)
+        assert p.returncode == 1 and "different arguments" in err, (out, err)
+        assert "max total time" not in out
+
+
+def test_pt2pt_two_processes(exes, tmp_path):
+    """pt2pt_test -d -k -i as two processes (mpi_sendrecv_test.c): k measurements in
+    sendrecv_results.csv and the reference's summary line"""
+    p = _run(exes["pt2pt"], ["-d", 65536, "-k", 4, "-i", 3], tmp_path, XG_GPUS=2)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert re.search(r"^rank 0, mean = \d+\.\d+, std = \d+\.\d+, ntimes = 4, total_timing = \d+\.\d+, "
+                     r"mean\*ntimes = \d+\.\d+$", p.stdout, re.M), p.stdout
+    assert p.stdout.count("status = 1, statuses = 1") == 2
+    rows = open(tmp_path / "cwd" / "sendrecv_results.csv").read().split()
+    assert len(rows) == 4 and all(float(x) > 0 for x in rows)
