@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--methods", default="1,2,3,4")
     ap.add_argument("--pack-max-seg", type=int, default=4 << 20)
     ap.add_argument("--tune-pack", type=int, default=-1,
-                    help="1/0: time direct vs packed cross-GPU plans per method and keep the faster "
+                    help="1/0: time direct vs packed (one-/two-sided) cross-GPU plans per method and keep the fastest "
                          "(default: on when N > 1 and --pack-max-seg is left at its default)")
     ap.add_argument("--copy-variant", type=int, default=-1)
     ap.add_argument("--chunk", type=int, default=0)
@@ -389,16 +389,19 @@ def main():
         return ctx.allreduce_max([time.perf_counter() - t0])[0] / reps
 
     # N > 1: per method, pick by measurement whether cross-GPU segments go to RCCL
-    # one op per segment (direct) or packed into one staging buffer per peer
-    # (pack + unpack launches).  Every GPU sees the same MAX times -> same choice.
+    # one op per segment (direct), in runs contiguous at one end with the rest staged on
+    # the other (packed one-sided), or packed into one staging buffer per peer (pack +
+    # unpack launches, two-sided).  Every GPU sees the same MAX times -> same choice.
     tune_on = a.tune_pack == 1 or (a.tune_pack < 0 and world > 1 and a.pack_max_seg == 4 << 20)
-    cands = [0, 4 << 20] if tune_on else [a.pack_max_seg]
+    names = {(0, -1): "direct", (4 << 20, xg.PACK_ONE_SIDED): "packed_one_sided",
+             (4 << 20, xg.PACK_TWO_SIDED): "packed_two_sided"}
+    cands = list(names) if tune_on else [(a.pack_max_seg, -1)]
     for m in methods:
         phase("method %d: verify + plan choice" % m)
         s = xg.Schedule(m, a.procs, a.aggs, a.size, a.comm_size, rl, ntimes=1)
         best = None
-        for pk in cands:
-            r = xg.MethodRun(ctx, s, it=0, mode=0, pack_max_seg=pk)
+        for pk, form in cands:
+            r = xg.MethodRun(ctx, s, it=0, mode=0, pack_max_seg=pk, pack_form=form)
             # parity gate + the reference's own timing report for this method
             ctx.barrier()
             done, post, _wall = r.run_timed()
@@ -418,15 +421,15 @@ def main():
             tmax = ctx.allreduce_max([sorted(tw)[1]])[0]
             t = timed_reps(r, 5) if len(cands) > 1 else 0.0
             if len(cands) > 1:
-                tune.setdefault(str(m), {})["packed_ms" if pk else "direct_ms"] = round(t * 1e3, 4)
+                tune.setdefault(str(m), {})[names[(pk, form)] + "_ms"] = round(t * 1e3, 4)
             if best is None or t < best[0]:
                 if best is not None:
                     best[1].close()
-                best = (t, r, tmax, pk)
+                best = (t, r, tmax, (pk, form))
             else:
                 r.close()
         if len(cands) > 1:
-            tune[str(m)]["chosen"] = "packed" if best[3] else "direct"
+            tune[str(m)]["chosen"] = names[best[3]]
         max_total[str(m)] = best[2]
         runs.append(best[1])
 

@@ -188,6 +188,7 @@ typedef struct {
     int barrier_type;        /* -b (m13)                                                        */
     xg_timer *rep_timers;    /* out, optional: hosted ranks x ntimes timers[m] (m13)            */
     int64_t pack_min_bytes;  /* ... and pack only (step, peer) lists of >= this many bytes        */
+    int pack_form;           /* XG_PACK_ONE_SIDED / XG_PACK_TWO_SIDED (xg_devplan_build_form)   */
 } xg_run_opts;
 
 void xg_run_opts_default(xg_run_opts *o);

@@ -193,6 +193,22 @@ xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_m
 /* The same, packing a (step, peer) transfer list only when it also moves >= pack_min bytes
  * (smaller lists go one RCCL call per segment: cheaper than a pack and an unpack launch). */
 xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min);
+/* The same with the form of a packed list chosen (the two above use XG_PACK_FORM_DEFAULT):
+ *   XG_PACK_TWO_SIDED  one staging buffer per peer per direction: the sender packs every
+ *                      segment, one RCCL call, the receiver unpacks every segment;
+ *   XG_PACK_ONE_SIDED  the list in destination (or source) order, merged into runs that are
+ *                      contiguous there: one RCCL call per run, straight into (out of) the
+ *                      slots; only the runs not contiguous on the other side are staged, by
+ *                      the sender (or the receiver) -- each byte copied on one side at most.
+ *                      Of the two orders the one with fewer copied bytes + XG_RUN_CALL_BYTES
+ *                      per call; ties: destination order (sched.c, oneside).
+ * Any other form value means XG_PACK_FORM_DEFAULT.  The alltoallw translate this replaces:
+ * mpi_test.c:233-302. */
+enum { XG_PACK_TWO_SIDED = 0, XG_PACK_ONE_SIDED = 1 };
+#define XG_PACK_FORM_DEFAULT XG_PACK_ONE_SIDED
+#define XG_RUN_CALL_BYTES (1 << 20)
+xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
+                                  int form);
 void xg_devplan_free(xg_devplan *p);
 
 /* ---------------------------------------------------------------- RCCL calls (calls.c)

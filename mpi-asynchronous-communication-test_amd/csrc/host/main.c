@@ -67,7 +67,7 @@ static void usage(const char *argv0)   /* mpi_test.c:41-69 */
 
 typedef struct {
     int P, A, d, c, ntimes, type, proc_node, barrier_type;
-    int verify, fp_mode;
+    int verify, fp_mode, pack_form;
     int64_t eager, pack_max, pack_min;
     int *rank_list;
     const char *prefix;
@@ -89,6 +89,7 @@ static void run_method(xg_ctx *ctx, const opts_t *o, int method, int iter)
     xg_run_opts_default(&ro);
     ro.verify = o->verify; ro.fingerprint = o->fp_mode; ro.eager_limit = o->eager; ro.pack_max_seg = o->pack_max;
     ro.pack_min_bytes = o->pack_min;
+    ro.pack_form = o->pack_form;
     ro.proc_node = o->proc_node; ro.barrier_type = o->barrier_type;
     if ((method == 15 || method == 16) && g == 0)   /* static_node_assignment, lustre_driver_test.c:361-363 */
         printf("static node assignment for %d node ( %d processes per node) of type %d\n", o->P, o->proc_node, 0);
@@ -145,6 +146,7 @@ int main(int argc, char **argv)
     /* defaults of mpi_test.c:2121 */
     int cb_nodes = 1, method = 0, data_size = 0, proc_node = 1, i, comm_size = 200000000, iter = 1, ntimes = 1;
     int aggregator_type = 1, barrier_type = 0, procs = 0, verify = 0, fp_mode = XG_FP_REFERENCE;
+    int pack_form = XG_PACK_FORM_DEFAULT;
     int64_t eager = XG_MPICH_EAGER_LIMIT, pack_max = 4 << 20, pack_min = 64 << 10;
     char prefix[200];
     int rank, nranks, device, ngpu_dev;
@@ -160,6 +162,7 @@ int main(int argc, char **argv)
         {"pack-max-seg", required_argument, 0, 1004},
         {"gpus", required_argument, 0, 1005},
         {"pack-min", required_argument, 0, 1006},
+        {"pack-form", required_argument, 0, 1007},
         {0, 0, 0, 0}};
     int ngpus = xg_env_int("XG_GPUS", NULL, 1);
     prefix[0] = '\0';
@@ -173,6 +176,7 @@ int main(int argc, char **argv)
     if (getenv("XG_EAGER_LIMIT")) eager = atoll(getenv("XG_EAGER_LIMIT"));
     if (getenv("XG_PACK_MAX_SEG")) pack_max = atoll(getenv("XG_PACK_MAX_SEG"));
     if (getenv("XG_PACK_MIN")) pack_min = atoll(getenv("XG_PACK_MIN"));
+    pack_form = xg_env_int("XG_PACK_FORM", NULL, pack_form);
 
     while ((i = getopt_long(argc, argv, "hp:c:m:d:a:i:k:t:r:b:", longopts, NULL)) != EOF) {
         switch (i) {
@@ -193,6 +197,7 @@ int main(int argc, char **argv)
         case 1004: pack_max = atoll(optarg); break;
         case 1005: ngpus = atoi(optarg); break;
         case 1006: pack_min = atoll(optarg); break;
+        case 1007: pack_form = atoi(optarg); break;
         default:
             if (rank == 0) usage(argv[0]);
             return 0;
@@ -220,7 +225,7 @@ int main(int argc, char **argv)
          * started with different ones would post calls nobody pairs and hang -- compare a
          * digest (FNV-1a of argv and the planning settings, in 16-bit parts) first */
         static const char *keys[] = {"XG_PROCS", "XG_VERIFY", "XG_FINGERPRINT", "XG_EAGER_LIMIT", "XG_PACK_MAX_SEG",
-                                     "XG_PACK_MIN", NULL};
+                                     "XG_PACK_MIN", "XG_PACK_FORM", NULL};
         uint64_t h = 0xcbf29ce484222325ull;
         double red[8];
         int k;
@@ -247,6 +252,7 @@ int main(int argc, char **argv)
 
     o.P = procs; o.A = cb_nodes; o.d = data_size; o.c = comm_size; o.ntimes = ntimes; o.type = aggregator_type;
     o.proc_node = proc_node; o.verify = verify; o.fp_mode = fp_mode; o.eager = eager; o.pack_max = pack_max; o.pack_min = pack_min;
+    o.pack_form = pack_form;
     o.barrier_type = barrier_type; o.prefix = prefix;
     o.rank_list = (int *)malloc(sizeof(int) * cb_nodes);
     if (xg_aggregator_list(procs, cb_nodes, proc_node, aggregator_type, o.rank_list))

@@ -23,19 +23,21 @@ void xg_run_opts_default(xg_run_opts *o)
     o->barrier_type = 0;
     o->rep_timers = NULL;
     o->pack_min_bytes = 64 << 10;   /* latency-bound steps: one RCCL launch (profiles/r03/hybrid/) */
+    o->pack_form = XG_PACK_FORM_DEFAULT;
 }
 
 #define TRY(x) do { rc = (x); if (rc) goto out; } while (0)
 
 /* A G-GPU job's RCCL calls pair step by step as RCCL pairs them (xg_devplans_match over
  * every GPU's plan, calls.c); otherwise err says which call would not. */
-static int pairing_ok(const xg_sched *s, int G, int64_t pack_max_seg, int64_t pack_min, char *err, size_t errlen)
+static int pairing_ok(const xg_sched *s, int G, int64_t pack_max_seg, int64_t pack_min, int form, char *err,
+                      size_t errlen)
 {
     xg_devplan **plans = (xg_devplan **)calloc(G, sizeof *plans);
     int g, ok = 0;
     char why[400];
     if (!plans) return 0;
-    for (g = 0; g < G; ++g) plans[g] = xg_devplan_build_ex(s, G, g, pack_max_seg, pack_min);
+    for (g = 0; g < G; ++g) plans[g] = xg_devplan_build_form(s, G, g, pack_max_seg, pack_min, form);
     if (xg_devplans_match((const xg_devplan *const *)plans, G, 0, NULL, 0, why, sizeof why) >= 0) ok = 1;
     else snprintf(err, errlen, "the GPUs' RCCL calls do not pair: %s", why);
     for (g = 0; g < G; ++g) xg_devplan_free(plans[g]);
@@ -59,13 +61,13 @@ static uint64_t fnv(uint64_t h, const void *p, size_t n)
 static int inputs_agree(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list,
                         int comm_size, int iter, int ntimes, const xg_run_opts *o, char *err, size_t errlen)
 {
-    int64_t v[12];
+    int64_t v[13];
     double red[8];
     uint64_t h = 0xcbf29ce484222325ull;
     int i, rc;
     v[0] = method; v[1] = procs; v[2] = cb_nodes; v[3] = data_size; v[4] = comm_size; v[5] = iter;
     v[6] = ntimes; v[7] = o->eager_limit; v[8] = o->pack_max_seg; v[9] = o->pack_min_bytes;
-    v[10] = o->proc_node; v[11] = o->barrier_type;
+    v[10] = o->proc_node; v[11] = o->barrier_type; v[12] = o->pack_form;
     h = fnv(h, v, sizeof v);
     h = fnv(h, rank_list, sizeof(int) * (size_t)cb_nodes);
     for (i = 0; i < 4; ++i) {
@@ -107,13 +109,13 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
     s = xg_sched_build_iter(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, opts->proc_node,
                             opts->barrier_type, opts->eager_limit, iter, err, errlen);
     if (!s) return XG_ESCHED;
-    if (G > 1 && !pairing_ok(s, G, opts->pack_max_seg, opts->pack_min_bytes, err, errlen)) {
+    if (G > 1 && !pairing_ok(s, G, opts->pack_max_seg, opts->pack_min_bytes, opts->pack_form, err, errlen)) {
         /* every GPU derives every GPU's calls from the same schedule, so every GPU refuses
          * alike -- before any of them posts a call that could wait forever */
         xg_sched_free(s);
         return XG_EARG;
     }
-    dp = xg_devplan_build_ex(s, G, g, opts->pack_max_seg, opts->pack_min_bytes);
+    dp = xg_devplan_build_form(s, G, g, opts->pack_max_seg, opts->pack_min_bytes, opts->pack_form);
     TRY(xg_regions_alloc(ctx, dp->region_bytes, &reg));
     nruns = xg_fill_runs(s, G, g, NULL);
     runs = (xg_segrun *)malloc(sizeof(xg_segrun) * (nruns + 1));

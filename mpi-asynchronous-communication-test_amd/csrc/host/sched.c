@@ -1813,10 +1813,122 @@ static void local_copy(xg_copy *c, const plan_bases *pb, const xg_msg *m)
 
 xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg)
 {
-    return xg_devplan_build_ex(s, ngpus, g, pack_max_seg, 0);
+    return xg_devplan_build_form(s, ngpus, g, pack_max_seg, 0, XG_PACK_FORM_DEFAULT);
 }
 
 xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min)
+{
+    return xg_devplan_build_form(s, ngpus, g, pack_max_seg, pack_min, XG_PACK_FORM_DEFAULT);
+}
+
+/* One-sided form of one packed (step, src GPU -> dst GPU) transfer list (XG_PACK_ONE_SIDED).
+ * The messages are put in destination order (by_src = 0) or source order (by_src = 1) and
+ * merged into RUNS, each contiguous on that side: one RCCL call per run.  A run that is
+ * contiguous on the other side as well moves straight between the regions; any other one is
+ * gathered into staging by the sender (destination order) or scattered out of it by the
+ * receiver (source order) -- so every byte is copied on ONE side at most, where the two-sided
+ * form packs and unpacks all of them.  This is the transpose the alltoallw datatypes of m5/m8
+ * describe (mpi_test.c:233-302): e.g. all-to-many at P64 A16 on 8 GPUs, per peer the 16
+ * segments of 8 senders for 2 aggregators -- 2 runs of 2 MiB, one per aggregator's receive
+ * slots, gathered on the sending GPU; nothing is unpacked.  Of the two orders the one with
+ * fewer copied bytes + XG_RUN_CALL_BYTES per call wins (ties: destination order).  Both GPUs
+ * of the pair derive it from the same message list, so their calls pair one to one. */
+typedef struct {
+    int n, nrun, by_src;
+    int *idx;                 /* message indices, run order */
+    int *run_b;               /* run r = idx[run_b[r] .. run_b[r + 1]) */
+    unsigned char *staged;    /* run r goes through staging */
+} oneside;
+
+static const xg_msg *os_msg(const xg_sched *s, const oneside *o, int i) { return &s->msgs[o->idx[i]]; }
+
+typedef struct { int64_t off; int32_t buf, idx; } os_key;
+static int os_cmp(const void *a, const void *b)
+{
+    const os_key *x = (const os_key *)a, *y = (const os_key *)b;
+    if (x->buf != y->buf) return x->buf < y->buf ? -1 : 1;
+    if (x->off != y->off) return x->off < y->off ? -1 : 1;
+    return x->idx < y->idx ? -1 : x->idx > y->idx;      /* equal addresses: message order */
+}
+
+/* runs of `o` in the order by_src; returns the cost (copied bytes + calls) */
+static int64_t os_layout(const xg_sched *s, const plan_bases *pb, oneside *o, int by_src)
+{
+    int i, r;
+    int64_t cost = 0;
+    os_key *key = (os_key *)xmalloc(sizeof(os_key) * ((size_t)o->n + 1));
+    o->by_src = by_src;
+    for (i = 0; i < o->n; ++i) {
+        const xg_msg *m = os_msg(s, o, i);
+        key[i].buf = by_src ? m->sbuf : m->dbuf;
+        key[i].off = by_src ? src_off(pb, m) : dst_off(pb, m);
+        key[i].idx = o->idx[i];
+    }
+    qsort(key, (size_t)o->n, sizeof(os_key), os_cmp);
+    for (i = 0; i < o->n; ++i) o->idx[i] = key[i].idx;
+    free(key);
+    o->nrun = 0;
+    for (i = 0; i < o->n; ++i) {
+        const xg_msg *m = os_msg(s, o, i);
+        if (i > 0) {
+            const xg_msg *q = os_msg(s, o, i - 1);
+            const int contiguous = by_src ? (m->sbuf == q->sbuf && src_off(pb, m) == src_off(pb, q) + q->len)
+                                          : (m->dbuf == q->dbuf && dst_off(pb, m) == dst_off(pb, q) + q->len);
+            if (contiguous) continue;
+        }
+        o->run_b[o->nrun++] = i;
+    }
+    o->run_b[o->nrun] = o->n;
+    for (r = 0; r < o->nrun; ++r) {
+        int64_t bytes = 0;
+        int other = 1;      /* contiguous on the other side too */
+        for (i = o->run_b[r]; i < o->run_b[r + 1]; ++i) {
+            const xg_msg *m = os_msg(s, o, i);
+            bytes += m->len;
+            if (i > o->run_b[r]) {
+                const xg_msg *q = os_msg(s, o, i - 1);
+                other &= by_src ? (m->dbuf == q->dbuf && dst_off(pb, m) == dst_off(pb, q) + q->len)
+                                : (m->sbuf == q->sbuf && src_off(pb, m) == src_off(pb, q) + q->len);
+            }
+        }
+        o->staged[r] = !other;
+        cost += (other ? 0 : bytes) + XG_RUN_CALL_BYTES;
+    }
+    return cost;
+}
+
+/* the one-sided form of the messages of step [b, e) from GPU gs to GPU gd */
+static void os_build(const xg_sched *s, const plan_bases *pb, const int *order, int b, int e, int G, int gs,
+                     int gd, oneside *o)
+{
+    int k;
+    int64_t cost_d, cost_s;
+    o->n = 0;
+    for (k = b; k < e; ++k) {
+        const xg_msg *m = &s->msgs[order[k]];
+        if (moves(m) && xg_gpu_of(s->P, G, m->src) == gs && xg_gpu_of(s->P, G, m->dst) == gd) o->n++;
+    }
+    o->idx = (int *)xmalloc(sizeof(int) * ((size_t)o->n + 1));
+    o->run_b = (int *)xmalloc(sizeof(int) * ((size_t)o->n + 2));
+    o->staged = (unsigned char *)xmalloc((size_t)o->n + 1);
+    o->n = 0;
+    for (k = b; k < e; ++k) {
+        const xg_msg *m = &s->msgs[order[k]];
+        if (moves(m) && xg_gpu_of(s->P, G, m->src) == gs && xg_gpu_of(s->P, G, m->dst) == gd) o->idx[o->n++] = order[k];
+    }
+    cost_s = os_layout(s, pb, o, 1);
+    cost_d = os_layout(s, pb, o, 0);
+    if (cost_s < cost_d) os_layout(s, pb, o, 1);
+}
+
+static void os_free(oneside *o)
+{
+    free(o->idx); free(o->run_b); free(o->staged);
+    memset(o, 0, sizeof *o);
+}
+
+xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
+                                  int form)
 {
     xg_devplan *dp = (xg_devplan *)calloc(1, sizeof *dp);
     int nst = s->nsteps, i, st, G = ngpus;
@@ -1826,7 +1938,9 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
     int64_t stage_s_max = 0, stage_r_max = 0;
     int *bucket_n = (int *)calloc((size_t)G * 2, sizeof(int));
     int64_t *bucket_b = (int64_t *)calloc((size_t)G * 2, sizeof(int64_t));
+    oneside *os_out = (oneside *)calloc((size_t)G, sizeof(oneside)), *os_in = (oneside *)calloc((size_t)G, sizeof(oneside));
     plan_bases pb;
+    if (form != XG_PACK_TWO_SIDED && form != XG_PACK_ONE_SIDED) form = XG_PACK_FORM_DEFAULT;
     plan_bases_init(&pb, s, G, g);
     dp->gpu = g; dp->ngpus = G; dp->nsteps = nst;
     dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan));
@@ -1875,10 +1989,36 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
                 bucket_n[G + gs]++; bucket_b[G + gs] += m->len;
             }
         }
+        /* the one-sided layout of every packed list of this GPU's, both directions */
+        if (form == XG_PACK_ONE_SIDED)
+            for (p = 0; p < G; ++p) {
+                if (p == g) continue;
+                if (bucket_n[p] && use_pack(bucket_n[p], bucket_b[p], pack_max_seg, pack_min))
+                    os_build(s, &pb, order, b, e, G, g, p, &os_out[p]);
+                if (bucket_n[G + p] && use_pack(bucket_n[G + p], bucket_b[G + p], pack_max_seg, pack_min))
+                    os_build(s, &pb, order, b, e, G, p, g, &os_in[p]);
+            }
         /* packs (into staging) join the pre-exchange copy launch */
         for (p = 0; p < G; ++p) {
             int64_t off = 0;
             if (p == g || !bucket_n[p] || !use_pack(bucket_n[p], bucket_b[p], pack_max_seg, pack_min)) continue;
+            if (form == XG_PACK_ONE_SIDED) {
+                const oneside *o = &os_out[p];
+                int r;
+                for (r = 0; r < o->nrun; ++r) {
+                    if (o->by_src || !o->staged[r]) continue;     /* sent as it lies */
+                    for (k = o->run_b[r]; k < o->run_b[r + 1]; ++k) {
+                        const xg_msg *m = os_msg(s, o, k);
+                        xg_copy *c = cpush(&pre);
+                        c->src_buf = m->sbuf; c->src_off = src_off(&pb, m);
+                        c->dst_buf = XG_BUF_STAGE_SEND; c->dst_off = sbase + off;
+                        c->len = m->len;
+                        off += m->len;
+                    }
+                }
+                sbase += off;
+                continue;
+            }
             for (k = b; k < e; ++k) {
                 const xg_msg *m = &s->msgs[order[k]];
                 if (!moves(m) || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
@@ -1903,7 +2043,23 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
                 if (p == g) continue;
                 if (bucket_n[p]) {
                     pk = use_pack(bucket_n[p], bucket_b[p], pack_max_seg, pack_min);
-                    if (pk) {
+                    if (pk && form == XG_PACK_ONE_SIDED) {
+                        const oneside *o = &os_out[p];
+                        int r;
+                        for (r = 0; r < o->nrun; ++r) {
+                            xg_p2p *q = ppush(&pp);
+                            int64_t len = 0;
+                            for (k = o->run_b[r]; k < o->run_b[r + 1]; ++k) len += os_msg(s, o, k)->len;
+                            q->peer = p; q->is_send = 1; q->len = len;
+                            if (!o->by_src && o->staged[r]) {
+                                q->buf = XG_BUF_STAGE_SEND; q->off = soff;
+                                soff += len;
+                            } else {
+                                const xg_msg *m = os_msg(s, o, o->run_b[r]);
+                                q->buf = m->sbuf; q->off = src_off(&pb, m);
+                            }
+                        }
+                    } else if (pk) {
                         xg_p2p *o = ppush(&pp);
                         o->peer = p; o->is_send = 1; o->buf = XG_BUF_STAGE_SEND; o->off = soff; o->len = bucket_b[p];
                         soff += bucket_b[p];
@@ -1922,7 +2078,32 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
                 }
                 if (bucket_n[G + p]) {
                     pk = use_pack(bucket_n[G + p], bucket_b[G + p], pack_max_seg, pack_min);
-                    if (pk) {
+                    if (pk && form == XG_PACK_ONE_SIDED) {
+                        const oneside *o = &os_in[p];
+                        int r;
+                        for (r = 0; r < o->nrun; ++r) {
+                            xg_p2p *q = ppush(&pp);
+                            int64_t len = 0;
+                            for (k = o->run_b[r]; k < o->run_b[r + 1]; ++k) len += os_msg(s, o, k)->len;
+                            q->peer = p; q->is_send = 0; q->len = len;
+                            if (o->by_src && o->staged[r]) {
+                                int64_t off = 0;
+                                q->buf = XG_BUF_STAGE_RECV; q->off = rbase;
+                                for (k = o->run_b[r]; k < o->run_b[r + 1]; ++k) {
+                                    const xg_msg *m = os_msg(s, o, k);
+                                    xg_copy *c = cpush(&post);
+                                    c->src_buf = XG_BUF_STAGE_RECV; c->src_off = rbase + off;
+                                    c->dst_buf = m->dbuf; c->dst_off = dst_off(&pb, m);
+                                    c->len = m->len;
+                                    off += m->len;
+                                }
+                                rbase += len;
+                            } else {
+                                const xg_msg *m = os_msg(s, o, o->run_b[r]);
+                                q->buf = m->dbuf; q->off = dst_off(&pb, m);
+                            }
+                        }
+                    } else if (pk) {
                         xg_p2p *o = ppush(&pp);
                         int64_t off = 0;
                         o->peer = p; o->is_send = 0; o->buf = XG_BUF_STAGE_RECV; o->off = rbase; o->len = bucket_b[G + p];
@@ -1958,7 +2139,12 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
         sp->post_count = post.n - sp->post_begin;
         if (sbase > stage_s_max) stage_s_max = sbase;
         if (rbase > stage_r_max) stage_r_max = rbase;
+        for (p = 0; p < G; ++p) {
+            os_free(&os_out[p]);
+            os_free(&os_in[p]);
+        }
     }
+    free(os_out); free(os_in);
     /* post copies are stored after the pre copies in one array */
     dp->ncopy = pre.n + post.n;
     dp->copies = (xg_copy *)xmalloc(sizeof(xg_copy) * (dp->ncopy + 1));

@@ -94,6 +94,7 @@ class Slot(C.Structure):
 
 A2M, M2A = 0, 1
 BUF_SEND, BUF_RECV, BUF_STAGE_SEND, BUF_STAGE_RECV, BUF_SCRATCH = 0, 1, 2, 3, 4
+PACK_TWO_SIDED, PACK_ONE_SIDED = 0, 1   # xg_devplan_build_form
 MSG_COPY, MSG_COLL, MSG_CTRL = 1, 2, 4
 TAM_METHODS = (15, 16)
 MPICH_EAGER_LIMIT = 65424
@@ -149,6 +150,8 @@ def host():
         h.xg_devplan_build.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64]
         h.xg_devplan_build_ex.restype = C.POINTER(DevPlan)
         h.xg_devplan_build_ex.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_int64]
+        h.xg_devplan_build_form.restype = C.POINTER(DevPlan)
+        h.xg_devplan_build_form.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int]
         h.xg_devplan_free.argtypes = [C.POINTER(DevPlan)]
         h.xg_devplan_step_calls.argtypes = [C.POINTER(DevPlan), C.c_int, C.c_int64, C.POINTER(Call)]
         h.xg_devplan_step_self_calls.argtypes = [C.POINTER(DevPlan), C.c_int, C.c_int64]
@@ -378,14 +381,15 @@ class Schedule:
     def region_bytes(self, ngpus, g, buf):
         return host().xg_region_bytes(self._h, ngpus, g, buf)
 
-    def devplan(self, ngpus, g, pack_max_seg=4 << 20, pack_min=0):
-        return DevicePlanView(self, ngpus, g, pack_max_seg, pack_min)
+    def devplan(self, ngpus, g, pack_max_seg=4 << 20, pack_min=0, pack_form=-1):
+        return DevicePlanView(self, ngpus, g, pack_max_seg, pack_min, pack_form)
 
-    def check_pairing(self, ngpus, pack_max_seg=4 << 20, pack_min=0):
+    def check_pairing(self, ngpus, pack_max_seg=4 << 20, pack_min=0, pack_form=-1):
         """Refuse (XGError) a job whose GPUs' RCCL calls RCCL would not pair step by step
         (xg_devplans_match over every GPU's plan, built in C); returns the number of pairs."""
         h = host()
-        plans = [h.xg_devplan_build_ex(self._h, ngpus, g, pack_max_seg, pack_min) for g in range(ngpus)]
+        plans = [h.xg_devplan_build_form(self._h, ngpus, g, pack_max_seg, pack_min, pack_form)
+                 for g in range(ngpus)]
         try:
             arr = (C.POINTER(DevPlan) * ngpus)(*plans)
             err = C.create_string_buffer(512)
@@ -414,9 +418,10 @@ class Schedule:
 class DevicePlanView:
     """Python view of xg_devplan (host memory), used by the CPU plan tests."""
 
-    def __init__(self, sched, ngpus, g, pack_max_seg, pack_min=0):
+    def __init__(self, sched, ngpus, g, pack_max_seg, pack_min=0, pack_form=-1):
         self.sched = sched
-        self._p = host().xg_devplan_build_ex(sched.handle, ngpus, g, pack_max_seg, pack_min)
+        # pack_form: PACK_TWO_SIDED, PACK_ONE_SIDED, or -1 = the library's default (xg_sched.h)
+        self._p = host().xg_devplan_build_form(sched.handle, ngpus, g, pack_max_seg, pack_min, pack_form)
         p = self._p.contents
         self.gpu, self.ngpus, self.nsteps = p.gpu, p.ngpus, p.nsteps
         self.region_bytes = list(p.region_bytes)
@@ -634,16 +639,16 @@ class MethodRun:
     HBM regions, fingerprint fill (untimed), plan upload.  regions: a Regions
     object to use (re-poisoned here, not freed by close()) instead of new ones."""
 
-    def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None, pack_min=0):
+    def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None, pack_min=0, pack_form=-1):
         d = device()
         self.ctx, self.sched, self.it, self.mode, self.pack_max_seg = ctx, sched, it, mode, pack_max_seg
-        self.pack_min = pack_min
+        self.pack_min, self.pack_form = pack_min, pack_form
         G, g = ctx.nranks, ctx.rank
         if G > 1 and not getattr(ctx, "is_virtual", False):
             # a real multi-GPU job: refuse, on every rank alike, calls RCCL would not pair
             # step by step, before any rank posts one (xg_devplans_match)
-            sched.check_pairing(G, pack_max_seg, pack_min)
-        self.view = sched.devplan(G, g, pack_max_seg, pack_min)
+            sched.check_pairing(G, pack_max_seg, pack_min, pack_form)
+        self.view = sched.devplan(G, g, pack_max_seg, pack_min, pack_form)
         self._shared = regions is not None
         if regions is not None:
             if not regions.fits(self.view.region_bytes):

@@ -12,7 +12,8 @@ import types
 def make(real_xg):
     fake = types.ModuleType("xg")
     for name in ("aggregator_list", "Schedule", "XGError", "NBUF", "BUF_SEND", "BUF_RECV",
-                 "BUF_STAGE_SEND", "BUF_STAGE_RECV", "BUF_SCRATCH", "method_label", "host"):
+                 "BUF_STAGE_SEND", "BUF_STAGE_RECV", "BUF_SCRATCH", "PACK_TWO_SIDED", "PACK_ONE_SIDED",
+                 "method_label", "host"):
         setattr(fake, name, getattr(real_xg, name))
     calls = {"p2p_bench": 0, "ktime": [], "runs": 0}
     fake.calls = calls
@@ -101,12 +102,12 @@ def make(real_xg):
             pass
 
     class MethodRun:
-        def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None, pack_min=0):
+        def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None, pack_min=0, pack_form=-1):
             self.ctx, self.sched, self.pack_max_seg = ctx, sched, pack_max_seg
             G, g = ctx.nranks, ctx.rank
             if G > 1:     # as the real MethodRun: refuse calls RCCL would not pair
-                sched.check_pairing(G, pack_max_seg, pack_min)
-            self.view = sched.devplan(G, g, pack_max_seg, pack_min)
+                sched.check_pairing(G, pack_max_seg, pack_min, pack_form)
+            self.view = sched.devplan(G, g, pack_max_seg, pack_min, pack_form)
             # the RCCL calls this GPU's plan posts per run: per step its send/recv group and
             # its barrier (xg_devplan_step_calls), as a signature the ranks must agree on in
             # everything collective (the barriers) -- the p2p pairing is xg_devplans_match's

@@ -59,8 +59,8 @@ def step_parts(view, st):
             view.copies[ob:ob + oc])
 
 
-def simulate(s, G, it=0, mode=0, pack=1 << 20):
-    views = [s.devplan(G, g, pack) for g in range(G)]
+def simulate(s, G, it=0, mode=0, pack=1 << 20, form=-1):
+    views = [s.devplan(G, g, pack, 0, form) for g in range(G)]
     regs = [make_regions(s, v, G, g, it, mode) for g, v in enumerate(views)]
     for st in range(views[0].nsteps):
         parts = [step_parts(v, st) for v in views]

@@ -9,6 +9,9 @@ import pytest
 import xg_oracle as O
 from plan_exec import check_recv, simulate
 
+# direct (one call per segment), packed two-sided (pack + unpack), packed one-sided (runs)
+FORMS = ((0, -1), (1 << 20, 0), (1 << 20, 1))
+
 CASES = [  # P, A, d, c, ntimes, type, proc_node
     (32, 14, 40, 3, 2, 1, 1),      # README shape (reduced d), throttled
     (20, 6, 24, 7, 3, 1, 1),
@@ -28,8 +31,8 @@ def test_plans_deliver_every_byte(xg, case, G):
     rl = xg.aggregator_list(P, A, pn, t)
     for m in O.METHODS:
         s = xg.Schedule(m, P, A, d, c, rl, ntimes=k, proc_node=pn, barrier_type=(m * G) % 3)
-        for pack in (0, 1 << 20):
-            views, regs = simulate(s, G, it=1, mode=1, pack=pack)
+        for pack, form in FORMS:
+            views, regs = simulate(s, G, it=1, mode=1, pack=pack, form=form)
             check_recv(s, G, regs, it=1, mode=1)
             if G > 1 and m in (13, 17, 19):     # in-loop barriers become device-side barriers
                 assert all(v.sync_after == views[0].sync_after for v in views)
@@ -37,14 +40,15 @@ def test_plans_deliver_every_byte(xg, case, G):
 
 
 def test_pack_decision_and_volume(xg):
-    """Packing: >= 2 segments to a peer with mean < pack_max_seg -> one RCCL op per peer."""
+    """Two-sided packing: >= 2 segments to a peer with mean < pack_max_seg -> one RCCL op per
+    peer and direction."""
     P, A, d = 32, 14, 1024
     rl = xg.aggregator_list(P, A)
     s = xg.Schedule(1, P, A, d, 200000000, rl)
     G = 8
     tot_local = tot_remote = 0
     for g in range(G):
-        packed = s.devplan(G, g, pack_max_seg=1 << 20)
+        packed = s.devplan(G, g, pack_max_seg=1 << 20, pack_form=xg.PACK_TWO_SIDED)
         direct = s.devplan(G, g, pack_max_seg=0)
         peers = {o[0] for o in packed.p2p}
         # one send and one recv per peer in the single step when packed
@@ -91,8 +95,8 @@ def test_random_plans_deliver_every_byte(xg, case):
         s = xg.Schedule(m, P, A, d, c, rl, ntimes=k, proc_node=pn, barrier_type=b, iteration=2)
     except xg.XGError as e:
         pytest.skip("refused schedule: %s" % e)
-    for pack in (0, 1 << 20):
-        _views, regs = simulate(s, G, it=2, mode=1, pack=pack)
+    for pack, form in FORMS:
+        _views, regs = simulate(s, G, it=2, mode=1, pack=pack, form=form)
         check_recv(s, G, regs, it=2, mode=1)
 
 
@@ -117,8 +121,63 @@ def test_pack_min_keeps_small_peer_lists_direct(xg):
 def simulate_min(s, G):
     import plan_exec
     orig = s.devplan
-    s.devplan = lambda ng, g, pack=1 << 20: orig(ng, g, pack, 64 << 10)
+    s.devplan = lambda ng, g, pack=1 << 20, _pm=0, form=-1: orig(ng, g, pack, 64 << 10, form)
     try:
         return plan_exec.simulate(s, G)
     finally:
         s.devplan = orig
+
+
+def _copied(view):
+    """bytes a plan copies through staging: (packed, unpacked)"""
+    return (sum(c[4] for c in view.copies if c[2] == 2), sum(c[4] for c in view.copies if c[0] == 3))
+
+
+@pytest.mark.parametrize("m", [5, 8, 1, 2])
+def test_one_sided_runs_at_configs2(xg, m):
+    """configs[2] (P64 A16, -d 256 KiB) on 8 GPUs: the one-sided form sends, per peer, one run per
+    receiving aggregator (all-to-many: 8 senders' segments land contiguous in its slots) or per
+    sending aggregator (many-to-all), copies every cross-GPU byte on ONE side only -- half the
+    two-sided form's pack + unpack bytes -- and still delivers every byte."""
+    P, A, d, G = 64, 16, 256 << 10, 8
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(m, P, A, d, 200000000, rl)
+    a2m = m in (1, 8)
+    for g in range(G):
+        one = s.devplan(G, g, 4 << 20, 0, xg.PACK_ONE_SIDED)
+        two = s.devplan(G, g, 4 << 20, 0, xg.PACK_TWO_SIDED)
+        assert one.remote_send_bytes == two.remote_send_bytes == 7 * 8 * 2 * d
+        pk1, up1 = _copied(one)
+        pk2, up2 = _copied(two)
+        assert pk2 == up2 == one.remote_send_bytes
+        # a2m: gathered by the sender, received straight into the slots; m2a: sent straight
+        # from the aggregator's segments, scattered by the receiver
+        assert (pk1, up1) == ((one.remote_send_bytes, 0) if a2m else (0, one.remote_send_bytes))
+        for peer in range(G):
+            if peer == g:
+                continue
+            sends = [o for o in one.p2p if o[0] == peer and o[1]]
+            recvs = [o for o in one.p2p if o[0] == peer and not o[1]]
+            # 2 aggregators per GPU: 2 runs of 8 segments (2 MiB) each way
+            assert [o[4] for o in sends] == [o[4] for o in recvs] == [8 * d, 8 * d]
+            assert all(o[2] == (2 if a2m else 0) for o in sends)
+            assert all(o[2] == (1 if a2m else 3) for o in recvs)
+    s.check_pairing(G, 4 << 20, 0, xg.PACK_ONE_SIDED)
+    _views, regs = simulate(s, G, it=1, mode=1, pack=4 << 20, form=xg.PACK_ONE_SIDED)
+    check_recv(s, G, regs, it=1, mode=1)
+
+
+def test_one_sided_moves_contiguous_runs_without_copies(xg):
+    """A run contiguous at both ends moves as one call straight between the regions: one
+    aggregator (rank 0) and 8 ranks on 2 GPUs -- GPU 1's four senders hold their one segment
+    each back to back, and they land in four consecutive slots of the aggregator."""
+    P, A, d, G = 8, 1, 4096, 2
+    rl = xg.aggregator_list(P, A)
+    for m in (8, 1):
+        s = xg.Schedule(m, P, A, d, 200000000, rl)
+        v0, v1 = (s.devplan(G, g, 4 << 20, 0, xg.PACK_ONE_SIDED) for g in range(G))
+        assert _copied(v0) == _copied(v1) == (0, 0)
+        assert [o[1:] for o in v1.p2p] == [(1, 0, 0, 4 * d)]                      # SEND, offset 0
+        assert [o[1:] for o in v0.p2p] == [(0, 1, s.recv_offset(G, 0) + 4 * d, 4 * d)]
+        _views, regs = simulate(s, G, it=0, mode=1, pack=4 << 20, form=xg.PACK_ONE_SIDED)
+        check_recv(s, G, regs, it=0, mode=1)

@@ -121,8 +121,8 @@ def test_random_config_virtual_gpus(xg, worlds, cfg):
     if G == 1:
         pytest.skip("one rank: no cross-GPU job")
     s, rl = _schedule(xg, cfg)
-    for pack in (0, 1 << 30):
-        runs = [xg.MethodRun(c, s, it=cfg[-1], mode=1, pack_max_seg=pack) for c in worlds[G]]
+    for pack, form in ((0, -1), (1 << 30, rng.choice([0, 1]))):      # direct; packed one- or two-sided
+        runs = [xg.MethodRun(c, s, it=cfg[-1], mode=1, pack_max_seg=pack, pack_form=form) for c in worlds[G]]
         try:
             done = xg.run_virtual(runs, rccl=rng.random() < 0.5)
             assert all(y >= x for x, y in zip(done, done[1:]))

@@ -20,6 +20,9 @@ from conftest import golden_configs, load_golden
 pytestmark = pytest.mark.gpu
 
 GPUS = (2, 3, 8)
+# (pack_max_seg, pack form): never pack / pack every multi-segment peer list one-sided (runs,
+# staged on one side) / two-sided (one staging buffer per peer and direction)
+PACKINGS = ((0, -1), (1 << 30, 1), (1 << 30, 0))
 
 
 @pytest.fixture(scope="module")
@@ -31,8 +34,8 @@ def worlds(xg):
             c.close()
 
 
-def _run_job(xg, ctxs, s, it, mode, pack, rccl=False, reps=1):
-    runs = [xg.MethodRun(c, s, it=it, mode=mode, pack_max_seg=pack) for c in ctxs]
+def _run_job(xg, ctxs, s, it, mode, pack, rccl=False, reps=1, form=-1):
+    runs = [xg.MethodRun(c, s, it=it, mode=mode, pack_max_seg=pack, pack_form=form) for c in ctxs]
     try:
         for rep in range(reps):           # reps > 1: a replay (graph mode) must deliver again
             if rep:
@@ -74,31 +77,33 @@ def _golden_job(xg, worlds, cfg, G, rccl):
         direction = O.direction(method)
         s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=meta["proc_node"],
                         barrier_type=meta.get("barrier", 0), iteration=it)
-        for pack in (0, 1 << 30):          # never pack / pack every multi-segment peer transfer
-            res = _run_job(xg, worlds[G], s, it, 0, pack, rccl)
+        for pack, form in PACKINGS:
+            res = _run_job(xg, worlds[G], s, it, 0, pack, rccl, form=form)
             assert len(res) == sum(1 for key in data[direction] if key[0] == it), (cfg, method, G)
             for (src, seed, dst, off), ck, nb, fb in res:
-                assert nb == 0, "%s G%d m%d pack%d %d->%d: %d bad bytes from %d" % (cfg, G, method, pack, src, dst,
-                                                                                     nb, fb)
+                assert nb == 0, "%s G%d m%d pack%d/%d %d->%d: %d bad bytes from %d" % (
+                    cfg, G, method, pack, form, src, dst, nb, fb)
                 glen, gchk = data[direction][(it, src, dst)]
-                assert ck == gchk, (cfg, G, method, pack, src, dst, hex(ck), hex(gchk))
+                assert ck == gchk, (cfg, G, method, pack, form, src, dst, hex(ck), hex(gchk))
 
 
 @pytest.mark.parametrize("G", GPUS)
 @pytest.mark.parametrize("method", list(range(1, 21)))
 def test_strong_fingerprint_multi_gpu(xg, worlds, G, method):
-    """Collision-free fingerprint across GPU boundaries (unaligned d, packed staging)."""
+    """Collision-free fingerprint across GPU boundaries (unaligned d, packed staging, one- and
+    two-sided)."""
     import xg_oracle as O
     P, A, d, c, k, it = 20, 6, 1000, 7, 2, 3
     rl = xg.aggregator_list(P, A)
     s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2, iteration=it)
     exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
-    res = _run_job(xg, worlds[G], s, it, 1, 1 << 20)
-    assert res
-    for (src, seed, dst, off), ck, nb, _fb in res:
-        assert nb == 0, (method, G, src, dst)
-        local = off - s.recv_offset(G, dst)
-        assert ck == O.chk64(exp[dst][local: local + d]), (method, G, src, dst)
+    for form in (1, 0):
+        res = _run_job(xg, worlds[G], s, it, 1, 1 << 20, form=form)
+        assert res
+        for (src, seed, dst, off), ck, nb, _fb in res:
+            assert nb == 0, (method, G, form, src, dst)
+            local = off - s.recv_offset(G, dst)
+            assert ck == O.chk64(exp[dst][local: local + d]), (method, G, form, src, dst)
 
 
 @pytest.mark.parametrize("G", (2, 8))
@@ -112,12 +117,12 @@ def test_config2_full_size_through_rccl(xg, worlds, G, method):
     P, A, d, it = 64, 16, 256 << 10, 2
     rl = xg.aggregator_list(P, A)
     s = xg.Schedule(method, P, A, d, 200000000, rl, ntimes=1, iteration=it)
-    for pack in (0, 1 << 30):
-        res = _run_job(xg, worlds[G], s, it, 1, pack, rccl=True)
+    for pack, form in PACKINGS:
+        res = _run_job(xg, worlds[G], s, it, 1, pack, rccl=True, form=form)
         assert len(res) == P * A
-        assert all(nb == 0 for _slot, _ck, nb, _fb in res), (method, G, pack)
+        assert all(nb == 0 for _slot, _ck, nb, _fb in res), (method, G, pack, form)
         for (src, seed, _dst, _off), ck, _nb, _fb in res[:: max(1, len(res) // 6)]:
-            assert ck == O.chk64(O.fingerprint(1, src, seed, it, d)), (method, G, pack, src, seed)
+            assert ck == O.chk64(O.fingerprint(1, src, seed, it, d)), (method, G, pack, form, src, seed)
 
 
 STEP_FORMS = {
@@ -155,12 +160,12 @@ def test_cross_gpu_step_forms(xg, form, rccl, G):
         for method in range(1, 21):
             s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2, iteration=it)
             exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
-            for pack in (0, 1 << 20):
-                res = _run_job(xg, ctxs, s, it, 1, pack, rccl=rccl, reps=2 if "graph" in form else 1)
+            for pack, pform in PACKINGS:
+                res = _run_job(xg, ctxs, s, it, 1, pack, rccl=rccl, reps=2 if "graph" in form else 1, form=pform)
                 for (src, seed, dst, off), ck, nb, _fb in res:
-                    assert nb == 0, (form, method, G, pack, src, dst)
+                    assert nb == 0, (form, method, G, pack, pform, src, dst)
                     local = off - s.recv_offset(G, dst)
-                    assert ck == O.chk64(exp[dst][local: local + d]), (form, method, G, pack, src, dst)
+                    assert ck == O.chk64(exp[dst][local: local + d]), (form, method, G, pack, pform, src, dst)
     finally:
         for cx in ctxs:
             cx.close()

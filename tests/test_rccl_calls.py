@@ -15,7 +15,9 @@ import pytest
 from conftest import REPO, golden_configs, load_golden
 
 CONFIGS = golden_configs()
-PACKS = (0, 4 << 20)          # direct (one call per segment) and the default packed plan
+# direct (one call per segment), packed one-sided (runs; the default packed form), packed
+# two-sided (one staging buffer per peer and direction)
+PACKS = ((0, -1), (4 << 20, 1), (4 << 20, 0))
 
 
 def _ref_pairs(views):
@@ -49,9 +51,9 @@ def test_golden_jobs_pair_step_by_step(xg, cfg):
         s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, ntimes=meta["ntimes"],
                         proc_node=meta["proc_node"], barrier_type=meta["barrier"])
         for G in range(2, min(8, meta["P"]) + 1):
-            for pack in PACKS:
-                n = s.check_pairing(G, pack)
-                views = [s.devplan(G, g, pack) for g in range(G)]
+            for pack, form in PACKS:
+                n = s.check_pairing(G, pack, 0, form)
+                views = [s.devplan(G, g, pack, 0, form) for g in range(G)]
                 assert n == sum(1 for v in views for st in range(v.nsteps) for c in v.calls(st) if c[0] == 1)
                 assert all(v.sync_after == views[0].sync_after for v in views)
 
@@ -67,8 +69,8 @@ def test_pairs_equal_the_per_step_rule(xg, cfg):
         for G in (2, 3, 8):
             if G > meta["P"]:
                 continue
-            for pack in PACKS:
-                views = [s.devplan(G, g, pack) for g in range(G)]
+            for pack, form in PACKS:
+                views = [s.devplan(G, g, pack, 0, form) for g in range(G)]
                 for v in views:
                     for st in range(v.nsteps):
                         c = v.calls(st)
@@ -78,7 +80,7 @@ def test_pairs_equal_the_per_step_rule(xg, cfg):
                         assert [x[0] for x in c].count(3) == v.sync_after[st]
                         assert all(x[0] != 3 for x in c[:-1])          # the barrier is the step's last call
                 pairs = xg.devplans_match(views)
-                assert pairs == _ref_pairs(views), (cfg, m, G, pack)
+                assert pairs == _ref_pairs(views), (cfg, m, G, pack, form)
                 assert sum(p[5] for p in pairs) == sum(v.remote_send_bytes for v in views)
 
 
@@ -99,8 +101,8 @@ def test_baseline_configs_pair_on_2_to_8_gpus(xg, case):
         for c in cs:
             s = xg.Schedule(m, P, A, d, c, rl)
             for G in (2, 3, 4, 8):
-                for pack in PACKS:
-                    assert s.check_pairing(G, pack) > 0
+                for pack, form in PACKS:
+                    assert s.check_pairing(G, pack, 0, form) > 0
 
 
 # ---------------------------------------------------------------- the matcher's refusals
@@ -178,7 +180,7 @@ def test_bench_ranks_issue_the_same_collectives(tmp_path, world):
     for r in range(1, world):
         assert traces[r] == traces[0], "rank %d's collective sequence differs from rank 0's" % r
     kinds = [t[0] for t in traces[0]]
-    assert kinds.count("plan") == 8               # 4 methods x {direct, packed} tuning candidates
+    assert kinds.count("plan") == 12              # 4 methods x {direct, packed one-sided, two-sided} candidates
     assert "p2p_bench" in kinds and "allreduce_max" in kinds
     line = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
     assert line["n_gpus"] == world and line["pack_autotune_ms_per_run"]
@@ -194,8 +196,8 @@ def test_self_calls_carry_the_local_part(xg, cfg):
         s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], meta["aggregators"], ntimes=meta["ntimes"],
                         proc_node=meta["proc_node"], barrier_type=meta["barrier"])
         for G in (2, 8):
-            for pack in PACKS:
-                views = [s.devplan(G, g, pack) for g in range(G)]
+            for pack, form in PACKS:
+                views = [s.devplan(G, g, pack, 0, form) for g in range(G)]
                 pairs = xg.devplans_match(views, self_max=1 << 30)
                 cross = xg.devplans_match(views)
                 assert [(p[0], p[1], p[2], p[5]) for p in pairs if p[1] != p[2]] == \
