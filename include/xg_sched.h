@@ -202,10 +202,14 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
  *                      the sender (or the receiver) -- each byte copied on one side at most.
  *                      Of the two orders the one with fewer copied bytes + XG_RUN_CALL_BYTES
  *                      per call; ties: destination order (sched.c, oneside).
- * Any other form value means XG_PACK_FORM_DEFAULT.  The alltoallw translate this replaces:
- * mpi_test.c:233-302. */
+ * One-sided halves the copied bytes but posts more calls (configs[2] on 8 GPUs: 2 per peer and
+ * direction instead of 1).  On one MI355X, where a virtual 8-GPU job moves every pair as an
+ * RCCL self send/recv and those serialize at ~3 us per call, two-sided is the faster form
+ * (profiles/r03/pack_forms/), so it is the default; bench.py times direct, one-sided and
+ * two-sided per method at N > 1 and keeps the fastest.  Any other form value means
+ * XG_PACK_FORM_DEFAULT.  The alltoallw translate this replaces: mpi_test.c:233-302. */
 enum { XG_PACK_TWO_SIDED = 0, XG_PACK_ONE_SIDED = 1 };
-#define XG_PACK_FORM_DEFAULT XG_PACK_ONE_SIDED
+#define XG_PACK_FORM_DEFAULT XG_PACK_TWO_SIDED
 #define XG_RUN_CALL_BYTES (1 << 20)
 xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
                                   int form);

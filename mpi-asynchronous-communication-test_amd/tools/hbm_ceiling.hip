@@ -18,6 +18,10 @@
 //   kind 16 many-to-all gather, copy_kernel_g<4, nt>: 14 source blocks of 32 x 1 MiB segments at a
 //           32 MiB stride, destination segment (r, a) at (r * 14 + a) MiB, pieces in destination order
 //   kind 17 the same with the source blocks 32 MiB + 64 KiB apart (stride off a power of two)
+//   kind 18 one GPU's pack launch of configs[2] m8 on 8 GPUs (28 MiB gathered out of 32 MiB of
+//           256 KiB segments, one-sided order), copy_kernel_g<4> over 16 KiB pieces (the product)
+//   kind 19 the same pieces, copy_kernel_p<4> (512 persistent 1024-lane workgroups)
+//   kind 20 copy_kernel_p<2>, 512 workgroups    kind 21 copy_kernel_p<8>, 256 workgroups
 // *gbps = counted bytes / average launch time (a copy counts read + write).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -66,6 +70,42 @@ __global__ __launch_bounds__(xgk::kThreads) void copy_kernel_b(const xgk::DCopy 
         xgk::realign_copy(c.src, c.dst, c.len, lds);
 }
 
+
+// copy_kernel_p<U>: a probe of a persistent piece copy (kinds 19-20) -- W workgroups of 1024
+// lanes, workgroup w copies pieces w, w + W, w + 2W, ... of exactly 16 KiB (one 16-B access
+// per lane): U pieces' loads in flight per lane, the store of piece k interleaved with the
+// loads of piece k + U*W (no launch-wide load burst followed by a store burst).
+template <int U>
+__global__ __launch_bounds__(1024) void copy_kernel_p(const xgk::DCopy *__restrict__ pieces, int np)
+{
+    const int W = (int)gridDim.x, lane = (int)threadIdx.x * 16;
+    xgk::u32x4 v[U];
+    uint8_t *dst[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = (int)blockIdx.x + u * W;
+        dst[u] = nullptr;
+        if (i < np) {
+            const xgk::DCopy c = pieces[i];
+            v[u] = *(const xgk::g_cu4 *)(c.src + lane);
+            dst[u] = c.dst;
+        }
+    }
+    for (int base = (int)blockIdx.x; base < np; base += U * W) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * W;
+            if (i >= np) break;
+            *(xgk::g_u4 *)(dst[u] + lane) = v[u];
+            const int j = i + U * W;
+            if (j < np) {
+                const xgk::DCopy c = pieces[j];
+                v[u] = *(const xgk::g_cu4 *)(c.src + lane);
+                dst[u] = c.dst;
+            }
+        }
+    }
+}
 
 __global__ __launch_bounds__(xgk::kThreads) void gridstride_copy(const xgk::u32x4 *__restrict__ s,
                                                                  xgk::u32x4 *__restrict__ t, int64_t n4)
@@ -140,7 +180,7 @@ __global__ __launch_bounds__(xgk::kThreads) void gridstride_copy_mix(const xgk::
 extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, double *gbps)
 {
     bytes &= ~(int64_t)32767;
-    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 17) return 3;
+    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 21) return 3;
     CK(hipSetDevice(device));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -150,7 +190,7 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipMalloc(&b, bytes));
     CK(hipMalloc(&sink, 4));
     CK(hipMemsetAsync(a, 1, bytes, st));
-    const int64_t piece = kind == 7 ? 262144 : (kind == 8 ? 65536 : 32768);
+    const int64_t piece = kind == 7 ? 262144 : (kind == 8 ? 65536 : kind >= 18 ? 16384 : 32768);
     std::vector<xgk::DCopy> pieces;
     if (kind == 16 || kind == 17) {            // bytes ignored: 14 x 32 one-MiB segments
         const int64_t seg = 1 << 20, stride = 32 * seg + (kind == 17 ? 65536 : 0);
@@ -159,6 +199,16 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
             for (int g = 0; g < 14; ++g)
                 for (int64_t o = 0; o < seg; o += piece)
                     pieces.push_back({a + g * stride + r * seg + o, b + (int64_t)(r * 14 + g) * seg + o, piece});
+    } else if (kind >= 18) {                   // bytes ignored: one GPU's pack launch of configs[2] m8
+        // on 8 GPUs: 8 ranks x 16 segments of 256 KiB (rank-major, 32 MiB), the 112 bound for the
+        // 7 peers gathered in the one-sided order (per peer, per aggregator, the 8 senders)
+        const int64_t seg = 256 << 10;
+        if (32 * seg * 4 > bytes) return 3;
+        int64_t t = 0;
+        for (int p = 1; p < 8; ++p)
+            for (int ag = 2 * p; ag < 2 * p + 2; ++ag)
+                for (int s = 0; s < 8; ++s, t += seg)
+                    for (int64_t o = 0; o < seg; o += piece) pieces.push_back({a + (s * 16 + ag) * seg + o, b + t + o, piece});
     } else {
         for (int64_t o = 0; o < bytes; o += piece) pieces.push_back({a + o, b + o, std::min<int64_t>(piece, bytes - o)});
     }
@@ -196,6 +246,9 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
         case 15: hipLaunchKernelGGL((xgk::copy_kernel_g<2, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         case 16:
         case 17: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
+        case 19: hipLaunchKernelGGL((copy_kernel_p<4>), dim3(512), dim3(1024), 0, st, dp, (int)np); break;
+        case 20: hipLaunchKernelGGL((copy_kernel_p<2>), dim3(512), dim3(1024), 0, st, dp, (int)np); break;
+        case 21: hipLaunchKernelGGL((copy_kernel_p<8>), dim3(256), dim3(1024), 0, st, dp, (int)np); break;
         default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         }
         CK(hipGetLastError());
@@ -204,7 +257,7 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    const double moved = kind == 16 || kind == 17 ? 448.0 * (1 << 20) : (double)bytes;
+    const double moved = kind == 16 || kind == 17 ? 448.0 * (1 << 20) : kind >= 18 ? 28.0 * (1 << 20) : (double)bytes;
     *gbps = (kind == 3 || kind == 4 || kind == 10 || kind == 11 ? 1.0 : 2.0) * moved * reps / (ms * 1e-3) / 1e9;
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
