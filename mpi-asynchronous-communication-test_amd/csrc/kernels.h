@@ -276,6 +276,87 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_g(const DCopy *__restric
         realign_copy(c.src, c.dst, c.len, lds);
 }
 
+// Wave-persistent piece copy: copy_kernel_w<J, NT>.  Every wave of the grid copies pieces
+// wv, wv + NW, wv + 2 NW, ... (NW = waves in the grid), each of at most J KiB and 16-B
+// aligned: J 16-B buffer accesses per lane, instruction j covering the piece's j-th KiB.
+// While it stores piece k, the loads of piece k + 1 are in flight (two register buffers),
+// so a wave never idles between pieces the way a one-piece workgroup does (exit, the next
+// workgroup's dispatch, its descriptor load, then its first data load).  The descriptors
+// come 64 at a time (lane l holds the wave's piece b + l) and are broadcast per piece with
+// readlane; a piece's length is its buffer resources' range, so a short piece needs no branch.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int AUX>
+__device__ __forceinline__ u32x4 bload16a(brsrc r, int off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+}
+
+template <int J, bool NT = false>
+__global__ __launch_bounds__(kThreads) void copy_kernel_w(const DCopy *__restrict__ pieces, int np,
+                                                          unsigned long long *start)
+{
+    constexpr int AUX = NT ? kAuxNT : kAuxPlain;
+    if (start && blockIdx.x == 0 && threadIdx.x == 0) *start = (unsigned long long)wall_clock64();
+    const int lane = (int)(threadIdx.x & 63);
+    const int NW = (int)gridDim.x * (kThreads / 64);
+    // the wave's index, made provably wave-uniform (readfirstlane): every branch below is then
+    // scalar, and the buffer resources stay in SGPRs (no waterfall loop around an access, and
+    // the waitcnt pass can count the loads of the next piece past the stores of this one)
+    const int wv = __builtin_amdgcn_readfirstlane((int)blockIdx.x * (kThreads / 64) + (int)(threadIdx.x >> 6));
+    if (wv >= np) return;
+    const int n = (np - 1 - wv) / NW + 1;                  // pieces of this wave
+    uint64_t ds = 0, dd = 0;
+    int dl = 0;
+    auto fetch = [&](int b) {                              // descriptors of pieces b .. b + 63
+        const int k = b + lane;
+        if (k < n) {
+            const DCopy c = pieces[wv + (int64_t)k * NW];
+            ds = (uint64_t)c.src; dd = (uint64_t)c.dst; dl = (int)c.len;
+        }
+    };
+    struct Rs { brsrc s, d; };
+    auto piece = [&](int k) -> Rs {
+        const int l = k & 63, len = __builtin_amdgcn_readlane(dl, l);
+        return {make_rsrc((const void *)readlane64(ds, l), len), make_rsrc((const void *)readlane64(dd, l), len)};
+    };
+    auto load = [&](u32x4 *v, const Rs &p) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) v[j] = bload16a<AUX>(p.s, lane * 16 + j * 1024);
+    };
+    auto store = [&](const u32x4 *v, const Rs &p) {
+#pragma unroll
+        for (int j = 0; j < J; ++j) bstore16<AUX>(p.d, lane * 16 + j * 1024, v[j]);
+    };
+    auto next = [&](int k) -> Rs {                         // piece k's resources (k < n)
+        if ((k & 63) == 0) fetch(k);
+        return piece(k);
+    };
+    u32x4 a[J], b[J];
+    fetch(0);
+    Rs pa = piece(0), pb;
+    load(a, pa);
+    for (int k = 0;; k += 2) {
+        if (k + 1 < n) {
+            pb = next(k + 1);
+            load(b, pb);
+        }
+        store(a, pa);
+        if (k + 1 >= n) break;
+        if (k + 2 < n) {
+            pa = next(k + 2);
+            load(a, pa);
+        }
+        store(b, pb);
+        if (k + 2 >= n) break;
+    }
+}
+
 // the wall clock after everything before it on the stream: closes a chain of step launches
 __global__ void clock_kernel(unsigned long long *t)
 {

@@ -22,6 +22,9 @@
 //           256 KiB segments, one-sided order), copy_kernel_g<4> over 16 KiB pieces (the product)
 //   kind 19 the same pieces, copy_kernel_p<4> (512 persistent 1024-lane workgroups)
 //   kind 20 copy_kernel_p<2>, 512 workgroups    kind 21 copy_kernel_p<8>, 256 workgroups
+//   kind 22 the kind-18 gather in 8 KiB pieces, copy_kernel_w<8> (wave-persistent, resident grid)
+//   kind 23 the kind-16 gather (448 MiB) in 8 KiB pieces, copy_kernel_w<8, nt>
+//   kind 24 the same in 4 KiB pieces, copy_kernel_w<4, nt>   kind 25 16 KiB pieces, copy_kernel_w<16, nt>
 // *gbps = counted bytes / average launch time (a copy counts read + write).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -180,7 +183,7 @@ __global__ __launch_bounds__(xgk::kThreads) void gridstride_copy_mix(const xgk::
 extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, double *gbps)
 {
     bytes &= ~(int64_t)32767;
-    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 21) return 3;
+    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 25) return 3;
     CK(hipSetDevice(device));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -190,16 +193,17 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipMalloc(&b, bytes));
     CK(hipMalloc(&sink, 4));
     CK(hipMemsetAsync(a, 1, bytes, st));
-    const int64_t piece = kind == 7 ? 262144 : (kind == 8 ? 65536 : kind >= 18 ? 16384 : 32768);
+    const int64_t piece = kind == 7 ? 262144 : kind == 8 ? 65536 : kind == 22 || kind == 23 ? 8192 : kind == 24 ? 4096
+                        : kind == 25 ? 16384 : kind >= 18 ? 16384 : 32768;
     std::vector<xgk::DCopy> pieces;
-    if (kind == 16 || kind == 17) {            // bytes ignored: 14 x 32 one-MiB segments
+    if (kind == 16 || kind == 17 || kind == 23 || kind == 24 || kind == 25) {   // bytes ignored: 14 x 32 one-MiB segments
         const int64_t seg = 1 << 20, stride = 32 * seg + (kind == 17 ? 65536 : 0);
         if (14 * stride > bytes) return 3;
         for (int r = 0; r < 32; ++r)
             for (int g = 0; g < 14; ++g)
                 for (int64_t o = 0; o < seg; o += piece)
                     pieces.push_back({a + g * stride + r * seg + o, b + (int64_t)(r * 14 + g) * seg + o, piece});
-    } else if (kind >= 18) {                   // bytes ignored: one GPU's pack launch of configs[2] m8
+    } else if (kind >= 18 && kind <= 22) {     // bytes ignored: one GPU's pack launch of configs[2] m8
         // on 8 GPUs: 8 ranks x 16 segments of 256 KiB (rank-major, 32 MiB), the 112 bound for the
         // 7 peers gathered in the one-sided order (per peer, per aggregator, the 8 senders)
         const int64_t seg = 256 << 10;
@@ -220,6 +224,15 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipEventCreate(&e1));
     const int64_t n4 = bytes / 16;
     const unsigned np = (unsigned)pieces.size();
+    // wave-persistent kinds: as many workgroups as are resident at once (occupancy x CUs)
+    int occ = 1, cus = 1;
+    if (kind == 22) CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xgk::copy_kernel_w<8, false>, xgk::kThreads, 0));
+    if (kind == 23) CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xgk::copy_kernel_w<8, true>, xgk::kThreads, 0));
+    if (kind == 24) CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xgk::copy_kernel_w<4, true>, xgk::kThreads, 0));
+    if (kind == 25) CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xgk::copy_kernel_w<16, true>, xgk::kThreads, 0));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    const unsigned wgrid = (unsigned)std::max(1, std::min<int>(occ * cus, ((int)np + 3) / 4));
+    if (kind >= 22) fprintf(stderr, "xgt kind %d: %u pieces, %d resident workgroups per CU -> grid %u\n", kind, np, occ, wgrid);
     for (int r = -2; r < reps; ++r) {          // 2 warm-up launches
         if (r == 0) CK(hipEventRecord(e0, st));
         switch (kind) {
@@ -249,6 +262,14 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
         case 19: hipLaunchKernelGGL((copy_kernel_p<4>), dim3(512), dim3(1024), 0, st, dp, (int)np); break;
         case 20: hipLaunchKernelGGL((copy_kernel_p<2>), dim3(512), dim3(1024), 0, st, dp, (int)np); break;
         case 21: hipLaunchKernelGGL((copy_kernel_p<8>), dim3(256), dim3(1024), 0, st, dp, (int)np); break;
+        case 22: hipLaunchKernelGGL((xgk::copy_kernel_w<8, false>), dim3(wgrid), dim3(xgk::kThreads), 0, st, dp,
+                                    (int)np, nullptr); break;
+        case 23: hipLaunchKernelGGL((xgk::copy_kernel_w<8, true>), dim3(wgrid), dim3(xgk::kThreads), 0, st, dp,
+                                    (int)np, nullptr); break;
+        case 24: hipLaunchKernelGGL((xgk::copy_kernel_w<4, true>), dim3(wgrid), dim3(xgk::kThreads), 0, st, dp,
+                                    (int)np, nullptr); break;
+        case 25: hipLaunchKernelGGL((xgk::copy_kernel_w<16, true>), dim3(wgrid), dim3(xgk::kThreads), 0, st, dp,
+                                    (int)np, nullptr); break;
         default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         }
         CK(hipGetLastError());
@@ -257,7 +278,8 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    const double moved = kind == 16 || kind == 17 ? 448.0 * (1 << 20) : kind >= 18 ? 28.0 * (1 << 20) : (double)bytes;
+    const double moved = kind == 16 || kind == 17 || kind >= 23 ? 448.0 * (1 << 20) : kind >= 18 ? 28.0 * (1 << 20)
+                                                                                               : (double)bytes;
     *gbps = (kind == 3 || kind == 4 || kind == 10 || kind == 11 ? 1.0 : 2.0) * moved * reps / (ms * 1e-3) / 1e9;
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
