@@ -297,6 +297,8 @@ __device__ __forceinline__ u32x4 bload16a(brsrc r, int off)
     return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
 }
 
+constexpr int kWaveKiB = 8;       // the product's copy_kernel_w: pieces of <= 8 KiB, 8 accesses per lane
+
 template <int J, bool NT = false>
 __global__ __launch_bounds__(kThreads) void copy_kernel_w(const DCopy *__restrict__ pieces, int np,
                                                           unsigned long long *start)

@@ -117,6 +117,9 @@ struct xg_ctx {
     int solo_min_steps;        // a whole plan of fewer steps stays a copy launch
     int64_t launch_max;        // copy launches above this many bytes go as back-to-back launches of ~this size
     int balance;               // 1: per launch, the piece size that least loads the busiest CU (launch_chunk)
+    int wave;                  // 1: cross-GPU steps' plain copy launches run copy_kernel_w (launch_chunk)
+    int64_t wave_min;          // ... when they move >= this many bytes
+    int wave_grid;             // copy_kernel_w workgroups resident at once (occupancy x CUs)
     int64_t wg_cost;           // ... a workgroup's fixed start, in bytes-equivalent
     int cus;                   // compute units
     int solo_relay;            // armed solo: rail 0 alone polls the doorbell and relays the ring
@@ -229,6 +232,7 @@ struct xg_plan {
     std::vector<int> chain_end;
     unsigned long long *d_cstamp;  // nsteps wall-clock stamps of chained steps
     std::vector<int64_t> plen;     // prefix sums of the piece lengths (npieces + 1), host side
+    std::vector<char> wave_at;     // npieces + 1: 1 at the first piece of a copy_kernel_w launch
     // hipGraph replay (XG_GRAPH=1): the launches of one xg_plan_enqueue / one timed xg_plan_run,
     // captured at first use and replayed after (a launch-bound multi-step run then costs one
     // graph launch of host time instead of a launch, an event and an RCCL group per step)
@@ -460,6 +464,17 @@ static int init_ctx(xg_ctx *c, const void *uid)
         c->balance = !(env && !strcmp(env, "0"));
         env = getenv("XG_COPY_WG_COST");
         c->wg_cost = env ? atoll(env) : 2048;
+        // the wave-persistent copy for the launches of cross-GPU steps (packs, unpacks, the
+        // local part): profiles/r03/wave_copy/ -- one GPU's configs[2] pack launch 5.8 ->
+        // 6.25 TB/s; the 448 MiB non-temporal launches stay copy_kernel_g (6.0 vs 5.5-5.8)
+        env = getenv("XG_COPY_WAVE");
+        c->wave = !(env && !strcmp(env, "0"));
+        env = getenv("XG_COPY_WAVE_MIN");
+        c->wave_min = env ? atoll(env) : (int64_t)1 << 20;
+        int per_cu = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, xgk::copy_kernel_w<xgk::kWaveKiB>, xgk::kThreads,
+                                                            0));
+        c->wave_grid = c->cus * (per_cu < 1 ? 1 : per_cu);
     }
     env = getenv("XG_SOLO_MIN_STEPS");       // plans of fewer steps never run as an armed solo launch
     c->solo_min_steps = env ? atoi(env) : 1;  // profiles/r02/one_step/: armed beats the event-timed launch
@@ -1191,20 +1206,39 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     // 448 MiB launches stay 32 KiB (56 per CU).  XG_COPY_BALANCE=0: always c->chunk.  (A rule
     // forcing >= 2 x CUs pieces on small launches was measured 3-7 % slower and dropped:
     // profiles/r03/min_wg/summary.txt.)
+    // A launch of a cross-GPU step (packs, unpacks, its local part) that copies with plain
+    // loads and stores, every transfer 16-B aligned, of >= wave_min bytes: copy_kernel_w over
+    // pieces of kWaveKiB (wave_at marks its first piece; profiles/r03/wave_copy/).
     int64_t chunk = c->chunk;
-    auto launch_chunk = [&](std::initializer_list<std::pair<int, int>> ranges) {
+    std::vector<xgk::DCopy> pieces;
+    std::vector<char> wave_at;
+    auto launch_chunk = [&](std::initializer_list<std::pair<int, int>> ranges, bool cross = false,
+                            bool reread = false) {
         chunk = c->chunk;
+        const size_t first = pieces.size();
+        if (wave_at.size() <= first) wave_at.resize(first + 1, 0);
+        wave_at[first] = 0;
         int64_t bytes = 0;
+        uint64_t bits = 0;
         for (const auto &rg : ranges)
-            for (int i = 0; i < rg.second; ++i) bytes += std::max<int64_t>(0, dp->copies[rg.first + i].len);
+            for (int i = 0; i < rg.second; ++i) {
+                const xg_copy &cp = dp->copies[rg.first + i];
+                if (cp.len <= 0) continue;
+                bytes += cp.len;
+                bits |= (uint64_t)cp.src_off | (uint64_t)cp.dst_off | (uint64_t)cp.len;
+            }
         if (bytes <= 0) return;
+        if (cross && c->wave && bytes >= c->wave_min && (bits & 15) == 0 && copy_variant(p, bytes, reread) == 1) {
+            chunk = (int64_t)xgk::kWaveKiB << 10;
+            wave_at[first] = 1;
+            return;
+        }
         if (!c->balance) return;
         std::vector<int64_t> lens;
         for (const auto &rg : ranges)
             for (int i = 0; i < rg.second; ++i) lens.push_back(dp->copies[rg.first + i].len);
         chunk = xg_piece_size(lens.data(), (int)lens.size(), c->chunk, c->cus, c->wg_cost);
     };
-    std::vector<xgk::DCopy> pieces;
     DisplScan ds;
     int rc;
     // side: -1 plain copy; 0 pack (destination in STAGE_SEND, displacement from the
@@ -1288,6 +1322,21 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         if (st.fused) p->steps[s - 1].deferred = true;
     }
     p->call_begin.push_back((int32_t)p->calls.size());
+    {
+        // the bytes one run copies (as the StepR totals below add them up): whether the plan
+        // streams past the Infinity Cache decides each launch's variant (copy_variant)
+        int64_t run = 0;
+        for (int s = 0; s < dp->nsteps; ++s) {
+            const xg_stepplan &sp = dp->steps[s];
+            for (int i = 0; i < sp.pre_count; ++i) {
+                const xg_copy &cp = dp->copies[sp.pre_begin + i];
+                const bool local = i >= sp.stage_count && cp.dst_buf != XG_BUF_STAGE_SEND;
+                if (!(local && p->steps[s].self_local)) run += std::max<int64_t>(0, cp.len);
+            }
+            for (int i = 0; i < sp.post_count; ++i) run += std::max<int64_t>(0, dp->copies[sp.post_begin + i].len);
+        }
+        p->streaming = 2 * run > ((int64_t)256 << 20);
+    }
     // pass 2: the piece table, each launch's pieces contiguous (a fused launch: the
     // previous step's unpacks, then this step's packs)
     for (int s = 0; s < dp->nsteps; ++s) {
@@ -1331,11 +1380,11 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         // piece order: stage | local | [previous unpacks] | packs (split or not fused), or
         // stage | previous unpacks | local | packs (fused_local: one launch over all three)
         if (st.fused_local) {
-            launch_chunk({r_prev, r_local, r_pack});
+            launch_chunk({r_prev, r_local, r_pack}, true, true);
             if (!add_post(s - 1)) goto bad;
         } else {
-            if (st.split) launch_chunk({r_local});
-            else launch_chunk({r_local, r_pack});
+            if (st.split) launch_chunk({r_local}, true);
+            else launch_chunk({r_local, r_pack}, st.p2p_n > 0 || r_pack.second > 0, r_pack.second > 0);
         }
         st.local_b = (int)pieces.size();
         for (int i = sp.stage_count; i < first_pack && !st.self_local; ++i)
@@ -1343,7 +1392,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.local_n = (int)pieces.size() - st.local_b;
         st.local_bytes = span(st.local_b);
         if (!st.fused_local) {
-            if (st.split || st.fused) launch_chunk({r_prev, r_pack});
+            if (st.split || st.fused) launch_chunk({r_prev, r_pack}, true, true);
             if (st.fused && !add_post(s - 1)) goto bad;
         }
         st.pack_b = (int)pieces.size();
@@ -1356,7 +1405,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         st.post_b = (int)pieces.size();
         st.post_n = 0;
         st.post_bytes = 0;
-        launch_chunk({r_post});
+        launch_chunk({r_post}, true);
         if (!st.deferred && !add_post(s)) goto bad;
     }
     // order of a launch's local pieces (workgroup i copies piece i): by destination address
@@ -1392,6 +1441,8 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         }
     }
     p->npieces = (int)pieces.size();
+    wave_at.resize(pieces.size() + 1, 0);
+    p->wave_at.swap(wave_at);
     p->plen.assign(pieces.size() + 1, 0);
     for (size_t i = 0; i < pieces.size(); ++i) p->plen[i + 1] = p->plen[i] + pieces[i].len;
     if ((rc = plan_upload(p, pieces, ds))) {
@@ -1571,7 +1622,10 @@ static int launch_dispatches(const xg_plan *p, int b, int n, int64_t bytes)
 static int launch_one(xg_plan *p, int b, int n, int v, hipStream_t st, unsigned long long *start)
 {
     const xgk::DCopy *pc = p->d_pieces + b;
-    if (v == 6) hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start);
+    if (v == 1 && p->wave_at[b]) {       // pieces of <= kWaveKiB, 16-B aligned (launch_chunk)
+        const int w = std::max(1, std::min(p->ctx->wave_grid, (n + 3) / 4));
+        hipLaunchKernelGGL((xgk::copy_kernel_w<xgk::kWaveKiB>), dim3(w), dim3(xgk::kThreads), 0, st, pc, n, start);
+    } else if (v == 6) hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start);
     else hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start);
     HIPCHK(hipGetLastError());
     return XG_OK;
