@@ -25,6 +25,8 @@
 //   kind 22 the kind-18 gather in 8 KiB pieces, copy_kernel_w<8> (wave-persistent, resident grid)
 //   kind 23 the kind-16 gather (448 MiB) in 8 KiB pieces, copy_kernel_w<8, nt>
 //   kind 24 the same in 4 KiB pieces, copy_kernel_w<4, nt>   kind 25 16 KiB pieces, copy_kernel_w<16, nt>
+//   kind 26 the kind-18 pack in the two-sided order (per peer, per sender), copy_kernel_g<4> 16 KiB
+//   kind 27 the same, copy_kernel_w<8> over 8 KiB pieces (the product since call K)
 // *gbps = counted bytes / average launch time (a copy counts read + write).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -183,7 +185,7 @@ __global__ __launch_bounds__(xgk::kThreads) void gridstride_copy_mix(const xgk::
 extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, double *gbps)
 {
     bytes &= ~(int64_t)32767;
-    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 25) return 3;
+    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 27) return 3;
     CK(hipSetDevice(device));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -193,7 +195,7 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipMalloc(&b, bytes));
     CK(hipMalloc(&sink, 4));
     CK(hipMemsetAsync(a, 1, bytes, st));
-    const int64_t piece = kind == 7 ? 262144 : kind == 8 ? 65536 : kind == 22 || kind == 23 ? 8192 : kind == 24 ? 4096
+    const int64_t piece = kind == 7 ? 262144 : kind == 8 ? 65536 : kind == 22 || kind == 23 || kind == 27 ? 8192 : kind == 24 ? 4096
                         : kind == 25 ? 16384 : kind >= 18 ? 16384 : 32768;
     std::vector<xgk::DCopy> pieces;
     if (kind == 16 || kind == 17 || kind == 23 || kind == 24 || kind == 25) {   // bytes ignored: 14 x 32 one-MiB segments
@@ -203,6 +205,14 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
             for (int g = 0; g < 14; ++g)
                 for (int64_t o = 0; o < seg; o += piece)
                     pieces.push_back({a + g * stride + r * seg + o, b + (int64_t)(r * 14 + g) * seg + o, piece});
+    } else if (kind == 26 || kind == 27) {     // the same pack in the two-sided order (per peer, per sender)
+        const int64_t seg = 256 << 10;
+        if (32 * seg * 4 > bytes) return 3;
+        int64_t t = 0;
+        for (int p = 1; p < 8; ++p)
+            for (int s = 0; s < 8; ++s)
+                for (int ag = 2 * p; ag < 2 * p + 2; ++ag, t += seg)
+                    for (int64_t o = 0; o < seg; o += piece) pieces.push_back({a + (s * 16 + ag) * seg + o, b + t + o, piece});
     } else if (kind >= 18 && kind <= 22) {     // bytes ignored: one GPU's pack launch of configs[2] m8
         // on 8 GPUs: 8 ranks x 16 segments of 256 KiB (rank-major, 32 MiB), the 112 bound for the
         // 7 peers gathered in the one-sided order (per peer, per aggregator, the 8 senders)
@@ -226,13 +236,13 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     const unsigned np = (unsigned)pieces.size();
     // wave-persistent kinds: as many workgroups as are resident at once (occupancy x CUs)
     int occ = 1, cus = 1;
-    if (kind == 22) CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xgk::copy_kernel_w<8, false>, xgk::kThreads, 0));
+    if (kind == 22 || kind == 27) CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xgk::copy_kernel_w<8, false>, xgk::kThreads, 0));
     if (kind == 23) CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xgk::copy_kernel_w<8, true>, xgk::kThreads, 0));
     if (kind == 24) CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xgk::copy_kernel_w<4, true>, xgk::kThreads, 0));
     if (kind == 25) CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, xgk::copy_kernel_w<16, true>, xgk::kThreads, 0));
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     const unsigned wgrid = (unsigned)std::max(1, std::min<int>(occ * cus, ((int)np + 3) / 4));
-    if (kind >= 22) fprintf(stderr, "xgt kind %d: %u pieces, %d resident workgroups per CU -> grid %u\n", kind, np, occ, wgrid);
+    if (kind >= 22 && kind != 26) fprintf(stderr, "xgt kind %d: %u pieces, %d resident workgroups per CU -> grid %u\n", kind, np, occ, wgrid);
     for (int r = -2; r < reps; ++r) {          // 2 warm-up launches
         if (r == 0) CK(hipEventRecord(e0, st));
         switch (kind) {
@@ -270,6 +280,8 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
                                     (int)np, nullptr); break;
         case 25: hipLaunchKernelGGL((xgk::copy_kernel_w<16, true>), dim3(wgrid), dim3(xgk::kThreads), 0, st, dp,
                                     (int)np, nullptr); break;
+        case 27: hipLaunchKernelGGL((xgk::copy_kernel_w<8, false>), dim3(wgrid), dim3(xgk::kThreads), 0, st, dp,
+                                    (int)np, nullptr); break;
         default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         }
         CK(hipGetLastError());
@@ -278,7 +290,7 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    const double moved = kind == 16 || kind == 17 || kind >= 23 ? 448.0 * (1 << 20) : kind >= 18 ? 28.0 * (1 << 20)
+    const double moved = kind == 16 || kind == 17 || (kind >= 23 && kind <= 25) ? 448.0 * (1 << 20) : kind >= 18 ? 28.0 * (1 << 20)
                                                                                                : (double)bytes;
     *gbps = (kind == 3 || kind == 4 || kind == 10 || kind == 11 ? 1.0 : 2.0) * moved * reps / (ms * 1e-3) / 1e9;
     CK(hipEventDestroy(e0));
