@@ -1206,9 +1206,10 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     // 448 MiB launches stay 32 KiB (56 per CU).  XG_COPY_BALANCE=0: always c->chunk.  (A rule
     // forcing >= 2 x CUs pieces on small launches was measured 3-7 % slower and dropped:
     // profiles/r03/min_wg/summary.txt.)
-    // A launch of a cross-GPU step (packs, unpacks, its local part) that copies with plain
-    // loads and stores, every transfer 16-B aligned, of >= wave_min bytes: copy_kernel_w over
-    // pieces of kWaveKiB (wave_at marks its first piece; profiles/r03/wave_copy/).
+    // A launch of a cross-GPU step (packs, unpacks, its local part), or of a GPU-local step too
+    // large for the step engine, that copies with plain loads and stores, every transfer 16-B
+    // aligned, of >= wave_min bytes: copy_kernel_w over pieces of kWaveKiB (wave_at marks its
+    // first piece; profiles/r03/wave_copy/).
     int64_t chunk = c->chunk;
     std::vector<xgk::DCopy> pieces;
     std::vector<char> wave_at;
@@ -1383,8 +1384,13 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             launch_chunk({r_prev, r_local, r_pack}, true, true);
             if (!add_post(s - 1)) goto bad;
         } else {
+            // a GPU-local step's launch too, when it cannot be an engine step (larger than
+            // engine_max_step, or the engine off): one large one-off launch
+            int64_t b_local = 0;
+            for (int i = 0; i < r_local.second; ++i) b_local += std::max<int64_t>(0, dp->copies[r_local.first + i].len);
+            const bool big_local = c->engine_max_step <= 0 || b_local > c->engine_max_step;
             if (st.split) launch_chunk({r_local}, true);
-            else launch_chunk({r_local, r_pack}, st.p2p_n > 0 || r_pack.second > 0, r_pack.second > 0);
+            else launch_chunk({r_local, r_pack}, st.p2p_n > 0 || r_pack.second > 0 || big_local, r_pack.second > 0);
         }
         st.local_b = (int)pieces.size();
         for (int i = sp.stage_count; i < first_pack && !st.self_local; ++i)
