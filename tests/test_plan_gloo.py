@@ -44,8 +44,9 @@ def _worker(rank, world, port, results):
                                    (16, 5, 24, 3, 1, 16)]:
             rl = xg.aggregator_list(P, A)
             s = xg.Schedule(m, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2, iteration=2)
-            for pack, self_max in ((0, 0), (1 << 20, 0), (0, 1 << 30), (1 << 20, 1 << 30)):
-                v = s.devplan(world, rank, pack)
+            for pack, self_max, form in ((0, 0, -1), (1 << 20, 0, 0), (0, 1 << 30, -1), (1 << 20, 1 << 30, 0),
+                                         (1 << 20, 0, 1), (1 << 20, 1 << 30, 1)):   # form 1: one-sided packing
+                v = s.devplan(world, rank, pack, 0, form)
                 reg = make_regions(s, v, world, rank, 2, 1)
                 seq = {}
                 for st in range(v.nsteps):
