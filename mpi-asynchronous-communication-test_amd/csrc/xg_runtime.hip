@@ -1336,7 +1336,12 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             }
             for (int i = 0; i < sp.post_count; ++i) run += std::max<int64_t>(0, dp->copies[sp.post_begin + i].len);
         }
-        p->streaming = 2 * run > ((int64_t)256 << 20);
+        // ... and whether its regions could hold in it at all: -k repetitions re-copy the same
+        // bytes, so a run of many small repetitions (P32 A14 -d 64 KiB -k 50: 56 MiB of
+        // regions, 2.8 GB copied) stays cache-resident and copies with plain stores
+        int64_t foot = 0;
+        for (int i = 0; i < XG_NBUF; ++i) foot += std::max<int64_t>(0, dp->region_bytes[i]);
+        p->streaming = std::min(2 * run, foot) > ((int64_t)256 << 20);
     }
     // pass 2: the piece table, each launch's pieces contiguous (a fused launch: the
     // previous step's unpacks, then this step's packs)
@@ -1478,7 +1483,6 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     {
         int64_t run = 0;
         for (const StepR &st : p->steps) run += st.stage_bytes + st.local_bytes + st.pack_bytes + st.post_bytes;
-        p->streaming = 2 * run > ((int64_t)256 << 20);
         // a one-GPU run of several small launches is bound by launching them, not by their
         // bytes: replayed as one graph (README TAM chains 17-19 -> 15-16 us,
         // profiles/r03/readme_cli/summary.txt).  Multi-GPU and virtual runs stay launched:
