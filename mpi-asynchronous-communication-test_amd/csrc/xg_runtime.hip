@@ -118,7 +118,7 @@ struct xg_ctx {
     int64_t launch_max;        // copy launches above this many bytes go as back-to-back launches of ~this size
     int balance;               // 1: per launch, the piece size that least loads the busiest CU (launch_chunk)
     int wave;                  // 1: cross-GPU steps' plain copy launches run copy_kernel_w (launch_chunk)
-    int64_t wave_min;          // ... when they move >= this many bytes
+    int64_t wave_min, wave_max;   // ... when they move between this many bytes and that many
     int wave_grid;             // copy_kernel_w workgroups resident at once (occupancy x CUs)
     int64_t wg_cost;           // ... a workgroup's fixed start, in bytes-equivalent
     int cus;                   // compute units
@@ -471,6 +471,10 @@ static int init_ctx(xg_ctx *c, const void *uid)
         c->wave = !(env && !strcmp(env, "0"));
         env = getenv("XG_COPY_WAVE_MIN");
         c->wave_min = env ? atoll(env) : (int64_t)1 << 20;
+        // above ~32 MiB the one-piece-per-workgroup launch is as fast or faster
+        // (profiles/r03/wave_local/: 28 MiB 9.3 vs 9.9 us, 56 MiB 18.7 vs 18.2, 112 MiB equal)
+        env = getenv("XG_COPY_WAVE_MAX");
+        c->wave_max = env ? atoll(env) : (int64_t)32 << 20;
         int per_cu = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, xgk::copy_kernel_w<xgk::kWaveKiB>, xgk::kThreads,
                                                             0));
@@ -1229,7 +1233,8 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
                 bits |= (uint64_t)cp.src_off | (uint64_t)cp.dst_off | (uint64_t)cp.len;
             }
         if (bytes <= 0) return;
-        if (cross && c->wave && bytes >= c->wave_min && (bits & 15) == 0 && copy_variant(p, bytes, reread) == 1) {
+        if (cross && c->wave && bytes >= c->wave_min && bytes <= c->wave_max && (bits & 15) == 0 &&
+            copy_variant(p, bytes, reread) == 1) {
             chunk = (int64_t)xgk::kWaveKiB << 10;
             wave_at[first] = 1;
             return;
