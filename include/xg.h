@@ -141,6 +141,11 @@ int xg_vplans_run(xg_plan *const *plans, int n, double *step_done);
  * in issue order) and ncclAllReduce for the in-loop barriers -- RCCL's calls on
  * the real plan buffers with one GPU. */
 int xg_vplans_run_rccl(xg_plan *const *plans, int n, double *step_done);
+/* Test hook: a virtual GPU's plan run ALONE by xg_plan_run / xg_plan_enqueue -- its copy
+ * launches only, its RCCL calls and in-loop barriers left out (its received-from-peer slots
+ * keep the poison) -- so one GPU's share of a job too large to emulate whole on one device
+ * executes at full size.  XG_EARG for a non-virtual context or a plan with self calls. */
+int xg_plan_set_local_only(xg_plan *p, int on);
 /* Kernel timing session.  mode 1: every copy / engine launch of any plan on this
  * context is bracketed by HIP events on the stream it runs on (at most
  * max_launches); mode 2: one event pair on the main stream around the whole

@@ -244,6 +244,8 @@ struct xg_plan {
     unsigned long long *d_gstamp;
     bool stamp_marks;              // mark() stamps (graph capture) instead of recording events
     bool graph_auto;               // XG_GRAPH unset: this plan replays as a graph (latency-bound, one GPU)
+    bool local_only;               // test hook (xg_plan_set_local_only): a virtual GPU runs its share alone,
+                                   // its RCCL calls and in-loop barriers left out
     uint64_t id;                   // unique per loaded plan (keys the virtual runner's graphs)
     struct VGraph {
         std::vector<uint64_t> ids;
@@ -1198,7 +1200,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
     p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1; p->d_cstamp = nullptr;
     p->g_enq = p->g_run = nullptr; p->id = next_plan_id(); p->vg.rccl = false; p->vg.exec = nullptr;
-    p->d_gstamp = nullptr; p->stamp_marks = false; p->graph_auto = false;
+    p->d_gstamp = nullptr; p->stamp_marks = false; p->graph_auto = false; p->local_only = false;
     // One piece per workgroup.  Bytes per piece, per launch (launch_chunk over the launch's
     // copies): c->chunk (32 KiB: profiles/r01_copy_ab.txt) or c->chunk / 2, / 4, / 8 (>= 4 KiB;
     // a halving keeps dividing the power-of-two segment sizes: no ragged tail piece per segment,
@@ -1742,11 +1744,12 @@ static int enqueue_step(xg_plan *p, int s)
     xg_ctx *c = p->ctx;
     const StepR &st = p->steps[s];
     int rc;
-    if (c->virt && (st.p2p_n || st.sync_after)) {
+    if (c->virt && (st.p2p_n || st.sync_after) && !p->local_only) {
         fprintf(stderr, "xg: a virtual GPU's cross-GPU step runs only through xg_vplans_run\n");
         return XG_EARG;
     }
     if ((rc = enqueue_pre(p, s, c->stream, c->side))) return rc;
+    if (p->local_only) return enqueue_post(p, s, c->stream);
     // the step's send/recv calls, in the order libxghost lists them (xg_devplan_step_calls),
     // as one group; the barrier call, if any, is the step's last and follows the unpacks
     const xg_call *cl = p->calls.data() + st.call_b;
@@ -2047,6 +2050,21 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
         }
         s = e;
     }
+    return XG_OK;
+}
+
+// Test hook: GPU g of a G-GPU job (a virtual context) runs its own share alone -- every copy
+// launch of its plan (stage, local gather/scatter, packs, unpacks) with its RCCL calls and
+// in-loop barriers left out, so a share too large to put all G GPUs on one device (configs[4]
+// at its stated size: 256 GiB per GPU) still executes, its local slots verifiable.  Refused
+// (XG_EARG) for a plan whose local copies travel as self send/recv in an RCCL group
+// (XG_SELF_MAX): leaving the group out would drop them.
+extern "C" int xg_plan_set_local_only(xg_plan *p, int on)
+{
+    if (!p || !p->ctx->virt) return XG_EARG;
+    for (const StepR &st : p->steps)
+        if (on && st.self_local) return XG_EARG;
+    p->local_only = on != 0;
     return XG_OK;
 }
 

@@ -470,6 +470,7 @@ def device():
         d.xg_init_virtual.argtypes = [C.POINTER(vp), ip, ip, ip]
         d.xg_vplans_run.argtypes = [C.POINTER(vp), ip, C.POINTER(C.c_double)]
         d.xg_vplans_run_rccl.argtypes = [C.POINTER(vp), ip, C.POINTER(C.c_double)]
+        d.xg_plan_set_local_only.argtypes = [vp, ip]
         d.xg_barrier.argtypes = [vp]
         d.xg_sync.argtypes = [vp]
         d.xg_device_sync.argtypes = [vp]
@@ -713,6 +714,11 @@ class MethodRun:
 
     def poison(self):
         _check(_dev.xg_regions_poison(self._r), "xg_regions_poison")
+
+    def set_local_only(self, on=True):
+        """test hook (virtual GPU): run this GPU's share alone -- copy launches only, its RCCL
+        calls and in-loop barriers left out (xg_plan_set_local_only)"""
+        _check(_dev.xg_plan_set_local_only(self._p, 1 if on else 0), "xg_plan_set_local_only")
 
     def verify(self):
         ns = max(1, self.nslots)

@@ -205,3 +205,46 @@ def test_wave_copy_on_every_cross_gpu_launch(xg, rccl, G):
     finally:
         for cx in ctxs:
             cx.close()
+
+
+@pytest.mark.parametrize("method", [7, 11, 12, 5, 8])
+def test_one_gpu_share_alone(xg, method):
+    """xg_plan_set_local_only: GPU 0 of an 8-GPU job runs its share alone (copy launches only,
+    no RCCL).  Every slot whose source lives on GPU 0 is delivered bit-exact; every slot whose
+    source is another GPU stays unwritten -- so the hook really leaves the exchange out (the
+    full-size configs[4] share in profiles/ rests on this)."""
+    import os
+    import xg_oracle as O
+    old = os.environ.get("XG_SELF_MAX")
+    os.environ["XG_SELF_MAX"] = "0"           # local parts as copy launches, not self calls
+    try:
+        ctx = xg.Context.virtual(0, 8, device=0)
+    finally:
+        if old is None:
+            del os.environ["XG_SELF_MAX"]
+        else:
+            os.environ["XG_SELF_MAX"] = old
+    try:
+        P, A, d, c, it, G = 64, 16, 65536, 3, 1, 8
+        rl = xg.aggregator_list(P, A)
+        s = xg.Schedule(method, P, A, d, c, rl, ntimes=1, iteration=it)
+        for pack in (0, 1 << 30):
+            run = xg.MethodRun(ctx, s, it=it, mode=1, pack_max_seg=pack)
+            try:
+                run.set_local_only()
+                done, _post, wall = run.run_timed()
+                assert all(0 <= a <= b for a, b in zip(done, done[1:])) and done[-1] <= wall + 1e-4
+                chk, bad, _first = run.verify()
+                lo, hi = s.block_range(G, 0)
+                local = [lo <= src < hi for (src, _seed, _dst, _off) in run.slots]
+                assert any(local) and not all(local)
+                for (src, seed, dst, off), ck, nb, loc in zip(run.slots, chk, bad, local):
+                    if loc:
+                        assert nb == 0, (method, pack, src, dst)
+                        assert ck == O.chk64(O.fingerprint(1, src, seed, it, d)), (method, pack, src, dst)
+                    else:     # never received (poison, or unpacked from staging nobody filled)
+                        assert nb > d // 2, (method, pack, src, dst, nb)
+            finally:
+                run.close()
+    finally:
+        ctx.close()
