@@ -171,24 +171,29 @@ def test_cross_gpu_step_forms(xg, form, rccl, G):
             cx.close()
 
 
+@pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("rccl", [False, True])
 @pytest.mark.parametrize("G", (2, 8))
-def test_wave_copy_on_every_cross_gpu_launch(xg, rccl, G):
+def test_wave_copy_on_every_cross_gpu_launch(xg, rccl, G, graph):
     """XG_COPY_WAVE_MIN=0: every plain, 16-B aligned copy launch of a cross-GPU step (packs,
     unpacks, fused unpack + pack, the local part) runs copy_kernel_w over 8 KiB pieces --
     every method, direct and both packed forms, a power-of-two -d and a ragged one (pieces of
     every length below 8 KiB), every slot against the oracle."""
     import os
     import xg_oracle as O
-    old = os.environ.get("XG_COPY_WAVE_MIN")
-    os.environ["XG_COPY_WAVE_MIN"] = "0"
+    env = {"XG_COPY_WAVE_MIN": "0"}
+    if graph:
+        env["XG_GRAPH"] = "1"           # the whole job captured once and replayed (twice below)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         ctxs = [xg.Context.virtual(g, G, device=0) for g in range(G)]
     finally:
-        if old is None:
-            del os.environ["XG_COPY_WAVE_MIN"]
-        else:
-            os.environ["XG_COPY_WAVE_MIN"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     try:
         P, A, c, k, it = 20, 6, 7, 2, 3
         rl = xg.aggregator_list(P, A)
@@ -197,7 +202,7 @@ def test_wave_copy_on_every_cross_gpu_launch(xg, rccl, G):
                 s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, proc_node=3, barrier_type=2, iteration=it)
                 exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
                 for pack, pform in PACKINGS:
-                    res = _run_job(xg, ctxs, s, it, 1, pack, rccl=rccl, form=pform)
+                    res = _run_job(xg, ctxs, s, it, 1, pack, rccl=rccl, form=pform, reps=2 if graph else 1)
                     for (src, seed, dst, off), ck, nb, _fb in res:
                         assert nb == 0, (d, method, G, pack, pform, src, dst)
                         local = off - s.recv_offset(G, dst)
