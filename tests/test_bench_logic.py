@@ -47,6 +47,10 @@ def test_bench_multi_gpu_rank0_line(world, tmp_path):
     assert out["xgmi"]["peak"] > 0 and out["xgmi"]["cross_gpu_bytes_per_step"] > 0
     assert out["roofline"] and out["roofline"]["bound"] == "hbm"
     assert set(out["pack_autotune_ms_per_run"]) == {"1", "2", "3", "4"}
+    forms = ("direct", "packed_one_sided", "packed_two_sided")
+    for m, tune in out["pack_autotune_ms_per_run"].items():      # every form timed, the fastest kept
+        assert set(tune) == {f + "_ms" for f in forms} | {"chosen"}, tune
+        assert tune["chosen"] in forms and tune[tune["chosen"] + "_ms"] == min(tune[f + "_ms"] for f in forms)
     calls = json.loads([l for l in p.stdout.splitlines() if l.startswith("CALLS ")][0][6:])
     sweep = out["xgmi"]["sweep"]          # the pt2pt_test analogue: 1 -> 0 latency + all pairs, 4 sizes
     assert calls["p2p"] == 1 + len(sweep) == 9
