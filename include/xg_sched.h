@@ -314,6 +314,10 @@ int64_t xg_piece_size(const int64_t *lens, int n, int64_t chunk, int cus, int64_
  * reads or writes bytes that step s-1's unpacks write -- then the two may not share one copy
  * launch; 0 if they may; -1 for a bad step (pieces.c). */
 int xg_step_local_meets_unpacks(const xg_devplan *dp, int s);
+/* 1 if a pre copy of step s after its stage copies (local gather/scatter, packs) reads or writes
+ * bytes a stage copy writes, or writes bytes one reads -- then the stage copies keep a launch of
+ * their own; 0 if all may share one launch; -1 for a bad step (pieces.c). */
+int xg_step_stage_meets_rest(const xg_devplan *dp, int s);
 
 /* fill: `nsegs` consecutive d-byte segments at `off` in the SEND region,
  * segment i = fingerprint(rank, seed0 + i, iter) (prepare_*_data loops). */

@@ -130,6 +130,7 @@ struct xg_ctx {
     int64_t split_min;         // ... when it moves >= this many bytes (smaller: in the pack / fused launch)
     int64_t self_max;          // a cross-GPU step's local part of <= this many bytes goes in its RCCL group
     int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
+    int fuse_stage;            // 1: a step's stage copies launch with its local copies when hazard-free
     int graph;                 // hipGraph replay of multi-launch runs: 1 always, 0 never, -1 latency-bound one-GPU runs
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
@@ -167,6 +168,8 @@ struct StepR {
     bool split, fused, deferred;
     bool self_local;                 // the local copies travel in the RCCL group as self send/recv (XG_SELF_MAX)
     bool fused_local;                // fused, and the local copies join that launch (small, hazard-free)
+    bool stage_fused;                // the stage copies join the step's local (+ pack) launch: none of the
+                                     // other pre copies meets their bytes (xg_step_stage_meets_rest)
 };
 
 // A run of >= 2 consecutive GPU-local steps (no RCCL op, no in-loop barrier, no
@@ -508,6 +511,8 @@ static int init_ctx(xg_ctx *c, const void *uid)
     c->self_max = env ? atoll(env) : (int64_t)256 << 10;
     env = getenv("XG_FUSE_UNPACK");          // "0": unpacks and the next step's packs apart
     c->fuse_unpack = !(env && !strcmp(env, "0"));
+    env = getenv("XG_FUSE_STAGE");           // "0": stage copies always in a launch of their own
+    c->fuse_stage = !(env && !strcmp(env, "0"));
     // hipGraph replay: "1" every multi-launch run (and virtual job), "0" never; default (-1):
     // one-GPU latency-bound runs only (xg_plan.graph_auto)
     env = getenv("XG_GRAPH");
@@ -785,8 +790,8 @@ extern "C" int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_
 // per-launch boundary dominates (profiles/r01_engine_sweep.txt: crossover ~16 MiB).
 static bool engine_step(const xg_ctx *c, const StepR &st)
 {
-    return !st.p2p_n && !st.sync_after && !st.stage_n && !st.post_n && !st.pack_n && !st.fused && !st.deferred &&
-           st.local_bytes <= c->engine_max_step;
+    return !st.p2p_n && !st.sync_after && !st.stage_n && !st.stage_fused && !st.post_n && !st.pack_n && !st.fused &&
+           !st.deferred && st.local_bytes <= c->engine_max_step;
 }
 
 // Build the engine segments of a loaded plan from its host piece table: every
@@ -1327,6 +1332,10 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
                              !p->steps[s - 1].sync_after && dp->steps[s - 1].post_count > 0;
         st.fused = prev_ok && (st.split || nloc == 0 || !xg_step_local_meets_unpacks(dp, s));
         st.fused_local = st.fused && !st.split && nloc > 0;
+        // TAM: a step's stage copies share the local (+ pack) launch when none of those meets
+        // their bytes -- README m15 / m16 step 3: 6 -> 5 launches per run
+        st.stage_fused = c->fuse_stage && sp.stage_count > 0 && (nloc > 0 || npack > 0) && !st.split &&
+                         !st.fused && !st.self_local && xg_step_stage_meets_rest(dp, s) == 0;
         if (st.fused) p->steps[s - 1].deferred = true;
     }
     p->call_begin.push_back((int32_t)p->calls.size());
@@ -1384,27 +1393,38 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             r_pack{sp.pre_begin + first_pack, sp.pre_count - first_pack},
             r_prev{st.fused ? dp->steps[s - 1].post_begin : 0, st.fused ? dp->steps[s - 1].post_count : 0},
             r_post{sp.post_begin, sp.post_count};
-        launch_chunk({r_stage});
-        st.stage_b = (int)pieces.size();
-        for (int i = 0; i < sp.stage_count; ++i)
-            if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
-        st.stage_n = (int)pieces.size() - st.stage_b;
-        st.stage_bytes = span(st.stage_b);
+        int64_t b_local = 0;
+        for (int i = 0; i < r_local.second; ++i) b_local += std::max<int64_t>(0, dp->copies[r_local.first + i].len);
+        if (st.stage_fused) {
+            // stage | local | packs as ONE launch (the stage pieces count as local ones)
+            launch_chunk({r_stage, r_local, r_pack}, st.p2p_n > 0 || r_pack.second > 0 || c->engine_max_step <= 0 ||
+                                                         b_local > c->engine_max_step, true);
+            st.stage_b = (int)pieces.size();
+            for (int i = 0; i < sp.stage_count; ++i)
+                if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
+            st.stage_n = 0;
+            st.stage_bytes = 0;
+        } else {
+            launch_chunk({r_stage});
+            st.stage_b = (int)pieces.size();
+            for (int i = 0; i < sp.stage_count; ++i)
+                if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
+            st.stage_n = (int)pieces.size() - st.stage_b;
+            st.stage_bytes = span(st.stage_b);
+        }
         // piece order: stage | local | [previous unpacks] | packs (split or not fused), or
         // stage | previous unpacks | local | packs (fused_local: one launch over all three)
         if (st.fused_local) {
             launch_chunk({r_prev, r_local, r_pack}, true, true);
             if (!add_post(s - 1)) goto bad;
-        } else {
+        } else if (!st.stage_fused) {
             // a GPU-local step's launch too, when it cannot be an engine step (larger than
             // engine_max_step, or the engine off): one large one-off launch
-            int64_t b_local = 0;
-            for (int i = 0; i < r_local.second; ++i) b_local += std::max<int64_t>(0, dp->copies[r_local.first + i].len);
             const bool big_local = c->engine_max_step <= 0 || b_local > c->engine_max_step;
             if (st.split) launch_chunk({r_local}, true);
             else launch_chunk({r_local, r_pack}, st.p2p_n > 0 || r_pack.second > 0 || big_local, r_pack.second > 0);
         }
-        st.local_b = (int)pieces.size();
+        st.local_b = st.stage_fused ? st.stage_b : (int)pieces.size();
         for (int i = sp.stage_count; i < first_pack && !st.self_local; ++i)
             if (!add(dp->copies[sp.pre_begin + i], -1)) goto bad;
         st.local_n = (int)pieces.size() - st.local_b;
@@ -1508,7 +1528,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             };
             return p->seg_of[s] < 0 && !st.split && !st.fused && !st.deferred && !st.p2p_n && !st.pack_n &&
                    !st.post_n && !st.sync_after && (st.local_n > 0 || st.stage_n > 0) &&
-                   (!st.local_n || stamps(st.local_bytes, false)) && (!st.stage_n || stamps(st.stage_bytes, true));
+                   (!st.local_n || stamps(st.local_bytes, st.stage_fused)) && (!st.stage_n || stamps(st.stage_bytes, true));
         };
         bool any = false;
         for (int s = 0; s < p->nsteps;) {
@@ -1722,7 +1742,8 @@ static int enqueue_pre(xg_plan *p, int s, hipStream_t stream, hipStream_t side)
         HIPCHK(hipEventRecord(p->join[s], side));
         if (!st.fused && st.pack_n && (rc = timed_copy(p, st.pack_b, st.pack_n, st.pack_bytes, stream, true))) return rc;
     } else if (!st.fused && st.pre_n &&
-               (rc = timed_copy(p, st.local_b, st.pre_n, st.local_bytes + st.pack_bytes, stream, st.pack_n > 0))) {
+               (rc = timed_copy(p, st.local_b, st.pre_n, st.local_bytes + st.pack_bytes, stream,
+                                st.pack_n > 0 || st.stage_fused))) {
         return rc;
     }
     return XG_OK;
@@ -1937,7 +1958,8 @@ static int enqueue_run(xg_plan *p, double *step_post)
                     rc = launch_copy(p, st.stage_b, st.stage_n, st.stage_bytes, c->stream, start, true);
                     start = nullptr;
                 }
-                if (!rc && st.local_n) rc = launch_copy(p, st.local_b, st.local_n, st.local_bytes, c->stream, start);
+                if (!rc && st.local_n)
+                    rc = launch_copy(p, st.local_b, st.local_n, st.local_bytes, c->stream, start, st.stage_fused);
                 if (rc) {
                     p->rec_ev = false;
                     return rc;

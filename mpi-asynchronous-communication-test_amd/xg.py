@@ -162,6 +162,7 @@ def host():
         h.xg_devplans_match.argtypes = [C.POINTER(C.POINTER(DevPlan)), C.c_int, C.c_int64, C.POINTER(CallPair),
                                         C.c_int64, C.c_char_p, C.c_size_t]
         h.xg_step_local_meets_unpacks.argtypes = [C.POINTER(DevPlan), C.c_int]
+        h.xg_step_stage_meets_rest.argtypes = [C.POINTER(DevPlan), C.c_int]
         h.xg_piece_size.restype = C.c_int64
         h.xg_piece_size.argtypes = [C.POINTER(C.c_int64), C.c_int, C.c_int64, C.c_int, C.c_int64]
         h.xg_fill_runs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(SegRun)]
@@ -442,6 +443,10 @@ class DevicePlanView:
     def local_meets_unpacks(self, step):
         """xg_step_local_meets_unpacks: may step's local copies share a launch with step-1's unpacks?"""
         return host().xg_step_local_meets_unpacks(self._p, step)
+
+    def stage_meets_rest(self, step):
+        """xg_step_stage_meets_rest: must step's stage copies keep a launch of their own?"""
+        return host().xg_step_stage_meets_rest(self._p, step)
 
     def calls(self, step, self_max=0):
         """xg_devplan_step_calls: [(kind, peer, buf, off, len)] this GPU posts in `step`"""

@@ -117,6 +117,53 @@ def test_tam_aggregation_buffers_match_oracle(xg, ctx, method):
         run.close()
 
 
+@pytest.mark.parametrize("d", [2048, 1000])
+@pytest.mark.parametrize("method", [15, 16])
+def test_tam_stage_copies_share_a_launch(xg, method, d):
+    """XG_FUSE_STAGE: a TAM step whose stage copies nothing else of the step touches
+    (xg_step_stage_meets_rest) runs them in the same launch as its local copies -- one launch
+    fewer per run at the README configuration -- and every receive slot and aggregation buffer
+    is the same as with the stage copies in a launch of their own."""
+    import os
+    import xg_oracle as O
+    P, A, c, k, it = 32, 14, 3, 2, 1
+    rl = xg.aggregator_list(P, A)
+    s = xg.Schedule(method, P, A, d, c, rl, ntimes=k, iteration=it)
+    exp = O.expected_recv(method, P, A, d, rl, it, mode=1)
+    runs = {}
+    ctxs = []
+    try:
+        for fuse in ("1", "0"):
+            old = os.environ.get("XG_FUSE_STAGE")
+            os.environ["XG_FUSE_STAGE"] = fuse
+            try:
+                cx = xg.Context(rank=0, nranks=1, device=0)
+            finally:
+                if old is None:
+                    del os.environ["XG_FUSE_STAGE"]
+                else:
+                    os.environ["XG_FUSE_STAGE"] = old
+            ctxs.append(cx)
+            run = xg.MethodRun(cx, s, it=it, mode=1)
+            runs[fuse] = run
+            for _ in range(2):
+                done, _post, wall = run.run_timed()
+                assert all(0 <= a <= b for a, b in zip(done, done[1:])) and done[-1] <= wall + 1e-4
+            chk, bad, _first = run.verify()
+            assert not any(bad), (method, d, fuse)
+            for (src, seed, dst, off), ck in zip(run.slots, chk):
+                local = off - s.recv_offset(1, dst)
+                assert ck == O.chk64(exp[dst][local: local + d]), (method, d, fuse, src, dst)
+        assert runs["1"].launches < runs["0"].launches, (runs["1"].launches, runs["0"].launches)
+        scr = s.region_bytes(1, 0, xg.BUF_SCRATCH)
+        assert runs["1"].read(xg.BUF_SCRATCH, 0, scr) == runs["0"].read(xg.BUF_SCRATCH, 0, scr)
+    finally:
+        for r in runs.values():
+            r.close()
+        for cx in ctxs:
+            cx.close()
+
+
 @pytest.mark.parametrize("d", [1000, 2048])
 @pytest.mark.parametrize("method", [1, 6, 9, 10, 11, 12, 13, 18])
 def test_step_engine_matches_per_step_launches(xg, ctx, method, d):

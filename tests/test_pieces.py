@@ -88,3 +88,70 @@ def test_real_plans_never_meet_their_unpacks(xg):
                     v = s.devplan(G, g, 1 << 30)
                     for st in range(1, v.nsteps):
                         assert v.local_meets_unpacks(st) == 0, (cfg, m, G, g, st)
+
+
+def test_stage_meets_rest(xg):
+    """xg_step_stage_meets_rest: a stage copy's written bytes read or written by another pre copy
+    of the step, or its read bytes written by one, keep the stage copies in a launch of their own"""
+    import ctypes as C
+    S, R, SC, SS = xg.BUF_SEND, xg.BUF_RECV, xg.BUF_SCRATCH, xg.BUF_STAGE_SEND
+    stage = [(S, 0, SC, 1000, 100), (SC, 4000, SC, 6000, 50)]     # writes SCRATCH [1000,1100), [6000,6050); reads S [0,100), SC [4000,4050)
+    cases = [
+        ([(S, 200, R, 0, 64)], [], 0),                # disjoint
+        ([(SC, 1099, R, 0, 1)], [], 1),               # reads the last byte a stage copy writes
+        ([(SC, 900, R, 0, 100)], [], 0),              # ends where a stage write starts
+        ([(S, 200, SC, 6049, 1)], [], 1),             # writes a byte a stage copy writes
+        ([(S, 200, SC, 4010, 8)], [], 1),             # writes a byte a stage copy reads
+        ([(S, 0, R, 0, 100)], [], 0),                 # reads what a stage copy reads: fine
+        ([], [(SC, 1050, SS, 0, 10)], 1),             # a pack reads a stage copy's output
+        ([(S, 200, R, 0, 8)], [(S, 300, SS, 0, 8)], 0),
+    ]
+    for local, packs, want in cases:
+        dp = _plan(xg, [(stage, local, packs, [])])
+        assert xg.host().xg_step_stage_meets_rest(C.byref(dp), 0) == want, (local, packs, want)
+    dp = _plan(xg, [([], [(S, 0, R, 0, 8)], [], [])])
+    assert xg.host().xg_step_stage_meets_rest(C.byref(dp), 0) == 0           # no stage copies
+    assert xg.host().xg_step_stage_meets_rest(C.byref(dp), 1) == -1
+
+
+def _brute_stage_meets_rest(v, st):
+    pb, pc, _qb, _qc, _ob, _oc = v.steps[st]
+    sc = v.stage_count[st]
+    stage, rest = v.copies[pb:pb + sc], v.copies[pb + sc:pb + pc]
+    def ov(b1, o1, n1, b2, o2, n2):
+        return n1 > 0 and n2 > 0 and b1 == b2 and o1 < o2 + n2 and o2 < o1 + n1
+    for sb, so, db, do, n in stage:
+        for rsb, rso, rdb, rdo, rn in rest:
+            if ov(rsb, rso, rn, db, do, n) or ov(rdb, rdo, rn, db, do, n) or ov(rdb, rdo, rn, sb, so, n):
+                return 1
+    return 0
+
+
+def test_stage_meets_rest_on_real_plans(xg):
+    """every golden-shape TAM plan (m15 / m16) on 1, 2 and 8 GPUs: the C test equals a brute-force
+    overlap check step by step, and the README configuration's step 3 may share one launch"""
+    from conftest import golden_configs, load_golden
+    fusable = 0
+    for cfg in golden_configs():
+        meta, _, _ = load_golden(cfg)
+        for m in (15, 16):
+            if m not in meta["method_list"]:
+                continue
+            s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], meta["aggregators"], ntimes=meta["ntimes"],
+                            proc_node=meta["proc_node"], barrier_type=meta["barrier"])
+            for G in (1, 2, 8):
+                if G > meta["P"]:
+                    continue
+                for g in range(G):
+                    v = s.devplan(G, g, 1 << 30)
+                    for st in range(v.nsteps):
+                        if not v.stage_count[st]:
+                            continue
+                        got = v.stage_meets_rest(st)
+                        assert got == _brute_stage_meets_rest(v, st), (cfg, m, G, g, st)
+                        fusable += got == 0 and v.steps[st][1] > v.stage_count[st]
+    assert fusable > 0
+    rl = xg.aggregator_list(32, 14)
+    for m in (15, 16):
+        v = xg.Schedule(m, 32, 14, 2048, 3, rl, ntimes=1).devplan(1, 0)
+        assert v.stage_count[3] and v.steps[3][1] > v.stage_count[3] and v.stage_meets_rest(3) == 0
