@@ -131,6 +131,7 @@ struct xg_ctx {
     int64_t self_max;          // a cross-GPU step's local part of <= this many bytes goes in its RCCL group
     int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
     int fuse_stage;            // 1: a step's stage copies launch with its local copies when hazard-free
+    int split_after_pack;      // 1: a split step's local part forks after its pack launch
     int graph;                 // hipGraph replay of multi-launch runs: 1 always, 0 never, -1 latency-bound one-GPU runs
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
@@ -513,6 +514,8 @@ static int init_ctx(xg_ctx *c, const void *uid)
     c->fuse_unpack = !(env && !strcmp(env, "0"));
     env = getenv("XG_FUSE_STAGE");           // "0": stage copies always in a launch of their own
     c->fuse_stage = !(env && !strcmp(env, "0"));
+    env = getenv("XG_SPLIT_AFTER_PACK");     // "0": a split step's local part and its packs start together
+    c->split_after_pack = !(env && !strcmp(env, "0"));
     // hipGraph replay: "1" every multi-launch run (and virtual job), "0" never; default (-1):
     // one-GPU latency-bound runs only (xg_plan.graph_auto)
     env = getenv("XG_GRAPH");
@@ -1736,11 +1739,20 @@ static int enqueue_pre(xg_plan *p, int s, hipStream_t stream, hipStream_t side)
         if (p->rec_ev && (rc = mark(p, s - 1, stream))) return rc;
     }
     if (st.split) {
+        // the packs feed the RCCL group (the critical path), the local part does not: by default
+        // the local part forks after the pack launch, so it overlaps the transfer instead of
+        // sharing HBM with the packs (XG_SPLIT_AFTER_PACK=0: both at once, as in round 2)
+        const bool pack_here = !st.fused && st.pack_n;
+        if (pack_here && p->ctx->split_after_pack &&
+            (rc = timed_copy(p, st.pack_b, st.pack_n, st.pack_bytes, stream, true)))
+            return rc;
         HIPCHK(hipEventRecord(p->fork[s], stream));
         HIPCHK(hipStreamWaitEvent(side, p->fork[s], 0));
         if ((rc = timed_copy(p, st.local_b, st.local_n, st.local_bytes, side))) return rc;
         HIPCHK(hipEventRecord(p->join[s], side));
-        if (!st.fused && st.pack_n && (rc = timed_copy(p, st.pack_b, st.pack_n, st.pack_bytes, stream, true))) return rc;
+        if (pack_here && !p->ctx->split_after_pack &&
+            (rc = timed_copy(p, st.pack_b, st.pack_n, st.pack_bytes, stream, true)))
+            return rc;
     } else if (!st.fused && st.pre_n &&
                (rc = timed_copy(p, st.local_b, st.pre_n, st.local_bytes + st.pack_bytes, stream,
                                 st.pack_n > 0 || st.stage_fused))) {

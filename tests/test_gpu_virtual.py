@@ -126,7 +126,8 @@ def test_config2_full_size_through_rccl(xg, worlds, G, method):
 
 
 STEP_FORMS = {
-    "split": {"XG_SELF_MAX": "0", "XG_SPLIT_MIN": "0"},       # local part on the side stream (round 2)
+    "split": {"XG_SELF_MAX": "0", "XG_SPLIT_MIN": "0"},       # local part on the side stream, after the packs
+    "split_with_packs": {"XG_SELF_MAX": "0", "XG_SPLIT_MIN": "0", "XG_SPLIT_AFTER_PACK": "0"},   # round 2: together
     "self_in_group": {"XG_SELF_MAX": str(1 << 30)},          # local part as self send/recv in the RCCL group
     "local_in_fused": {"XG_SELF_MAX": "0", "XG_SPLIT_MIN": str(1 << 40)},   # in the (fused) pack launch
     "graph": {"XG_GRAPH": "1", "XG_SELF_MAX": "0"},           # the whole job captured once, replayed
