@@ -181,20 +181,28 @@ def cpu_baseline_port(a, methods, note=""):
 SWEEP_SIZES = (4096, 65536, 1 << 20, 16 << 20)
 
 
-def p2p_sweep(ctx, world):
+def p2p_sweep(ctx, world, error=RuntimeError):
     """The pt2pt_test analogue (mpi_sendrecv_test.c:15-74) as RCCL p2p over xGMI, a few
     seconds at most: per message size, one direction 1 -> 0 (xg_p2p_bench mode 2: latency
     of one send/recv pair, what a latency-bound step pays per cross-GPU message) and all
     pairs at once (mode 0: every GPU sends `bytes` to each of its N-1 peers).  Every rank
     runs every case (the calls are collective); the figures are MAX time / MIN rate over
-    the GPUs taking part."""
+    the GPUs taking part.  -> (rows, None) or, when a case fails on some GPU (`error`
+    raised), (the rows before it, the error): every rank stops at the same case."""
     out = []
     for nbytes in SWEEP_SIZES:
         reps = 50 if nbytes <= 65536 else (20 if nbytes <= 1 << 20 else 5)
         for mode, name in ((2, "one_way_1_to_0"), (0, "all_pairs")):
-            gbps, sec = ctx.p2p_bench(nbytes, mode=mode, reps=reps)
+            msg = None
+            try:
+                gbps, sec = ctx.p2p_bench(nbytes, mode=mode, reps=reps)
+            except error as e:
+                gbps, sec, msg = 0.0, 0.0, str(e)
             part = mode == 0 or ctx.rank < 2          # mode 2 moves bytes between GPUs 1 and 0 only
-            t_max, neg_rate = ctx.allreduce_max([sec if part else 0.0, -gbps if part else -1e30])
+            t_max, neg_rate, err = ctx.allreduce_max([sec if part else 0.0, -gbps if part else -1e30,
+                                                      1.0 if msg else 0.0])
+            if err:
+                return out, "%s %d B: %s" % (name, nbytes, msg or "failed on another GPU")
             row = {"mode": name, "bytes": nbytes, "reps": reps, "us_per_rep": round(t_max * 1e6, 2)}
             if mode == 2:
                 row["GBps"] = round(-neg_rate, 2)
@@ -202,7 +210,7 @@ def p2p_sweep(ctx, world):
                 row["GBps_per_gpu_egress_min"] = round(-neg_rate, 2)
                 row["GBps_aggregate"] = round(-neg_rate * world, 2)
             out.append(row)
-    return out
+    return out, None
 
 
 # ---------------------------------------------------------------- N-GPU job without a launcher
@@ -396,12 +404,26 @@ def main():
     names = {(0, -1): "direct", (4 << 20, xg.PACK_ONE_SIDED): "packed_one_sided",
              (4 << 20, xg.PACK_TWO_SIDED): "packed_two_sided"}
     cands = list(names) if tune_on else [(a.pack_max_seg, -1)]
+    failed = {}         # method -> why each of its plan forms was refused (every form failed)
     for m in methods:
         phase("method %d: verify + plan choice" % m)
         s = xg.Schedule(m, a.procs, a.aggs, a.size, a.comm_size, rl, ntimes=1)
-        best = None
+        best, why = None, {}
         for pk, form in cands:
-            r = xg.MethodRun(ctx, s, it=0, mode=0, pack_max_seg=pk, pack_form=form)
+            fname = names.get((pk, form), "plan")
+            # a form that cannot be planned, loaded or verified on SOME GPU is left out on every
+            # GPU alike (MAX over the GPUs) and recorded; the line is printed from the forms that
+            # passed.  Nothing collective is posted with a plan before every GPU has loaded it.
+            r, err = None, ""
+            try:
+                r = xg.MethodRun(ctx, s, it=0, mode=0, pack_max_seg=pk, pack_form=form)
+            except xg.XGError as e:
+                err = "plan failed: %s" % e
+            if ctx.allreduce_max([1.0 if err else 0.0])[0]:
+                why[fname] = err or "plan failed on another GPU"
+                if r is not None:
+                    r.close()
+                continue
             # parity gate + the reference's own timing report for this method
             ctx.barrier()
             done, post, _wall = r.run_timed()
@@ -411,7 +433,9 @@ def main():
             nbad = float(sum(1 for b in bad if b))
             tmax, nbad = ctx.allreduce_max([tmax, nbad])
             if nbad:
-                raise SystemExit("bench: method %d delivered wrong bytes on some GPU; refusing to time it" % m)
+                why[fname] = "verify failed: %d slots (most on one GPU)" % nbad
+                r.close()
+                continue
             # the reference's report for a warm method: median of 3 more timed runs
             tw = []
             for _ in range(3):
@@ -421,7 +445,7 @@ def main():
             tmax = ctx.allreduce_max([sorted(tw)[1]])[0]
             t = timed_reps(r, 5) if len(cands) > 1 else 0.0
             if len(cands) > 1:
-                tune.setdefault(str(m), {})[names[(pk, form)] + "_ms"] = round(t * 1e3, 4)
+                tune.setdefault(str(m), {})[fname + "_ms"] = round(t * 1e3, 4)
             if best is None or t < best[0]:
                 if best is not None:
                     best[1].close()
@@ -429,9 +453,27 @@ def main():
             else:
                 r.close()
         if len(cands) > 1:
+            tune.setdefault(str(m), {}).update(why)
+        if best is None:
+            failed[str(m)] = why
+            continue
+        if len(cands) > 1:
             tune[str(m)]["chosen"] = names[best[3]]
         max_total[str(m)] = best[2]
         runs.append(best[1])
+    if failed:
+        # a method none of whose forms delivered: no throughput can be quoted for the
+        # workload -- say which and why in the line, then fail
+        for r in runs:
+            r.close()
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": a.steps,
+                              "warmup": a.warmup, "higher_is_better": True, "dtype": "u8",
+                              "error": "every plan form of method(s) %s failed" % ",".join(sorted(failed)),
+                              "failed_methods": failed, "pack_autotune_ms_per_run": tune or None,
+                              "cpu_baseline": cpu}))
+        ctx.close()
+        return 1
 
     def step():
         for r in runs:
@@ -504,15 +546,30 @@ def main():
             for g in range(world):
                 cross_step += r.sched.devplan(world, g, r.pack_max_seg).remote_send_bytes
         per_pair = max(65536, (cross_step // max(1, len(methods) * world * (world - 1)) + 4095) & ~4095)
-        ceil_gbps, _ = ctx.p2p_bench(per_pair, mode=0, reps=20)
-        ceil_min = -ctx.allreduce_max([-ceil_gbps])[0]          # slowest GPU's egress
         achieved = cross_step * a.steps / elapsed / 1e9
-        xgmi = {"achieved": round(achieved, 1), "peak": round(ceil_min * world, 1), "unit": "GB/s",
-                "frac": round(achieved / (ceil_min * world), 4) if ceil_min > 0 else None,
+        # the ceiling and the sweep are measurements beside the exchange, not the exchange: an
+        # RCCL error in them leaves null + the error in the line (as long as the ranks can still
+        # agree on it -- every rank reduces the error flag with the figures)
+        ceil_min, ceil_err = None, None
+        try:
+            ceil_gbps, _ = ctx.p2p_bench(per_pair, mode=0, reps=20)
+            err = 0.0
+        except xg.XGError as e:
+            ceil_gbps, err, ceil_err = 0.0, 1.0, str(e)
+        neg, err = ctx.allreduce_max([-ceil_gbps, err])
+        if err:
+            ceil_err = ceil_err or "failed on another GPU"
+        else:
+            ceil_min = -neg                                       # slowest GPU's egress
+        peak = round(ceil_min * world, 1) if ceil_min else None
+        xgmi = {"achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
+                "frac": round(achieved / (ceil_min * world), 4) if ceil_min else None,
                 "cross_gpu_bytes_per_step": int(cross_step),
                 "peak_source": "measured: RCCL all-pairs send/recv, %d B per GPU pair, slowest GPU egress x %d "
                                "(xg_p2p_bench mode 0)" % (per_pair, world),
-                "sweep": p2p_sweep(ctx, world)}
+                "ceiling_error": ceil_err}
+        phase("xGMI p2p sweep")
+        xgmi["sweep"], xgmi["sweep_error"] = p2p_sweep(ctx, world, xg.XGError)
     if rank != 0:
         ctx.close()
         return 0

@@ -69,3 +69,37 @@ def load_golden(name):
                 m, it, rank, _k, src, cnt, chk = r.split(",")
                 data["tam"].setdefault((int(m), int(it), int(rank)), []).append((int(src), int(cnt), int(chk, 16)))
     return meta, traces, data
+
+
+BASELINE = os.path.join(GOLDEN, "baseline")
+
+
+def baseline_configs(prefix=""):
+    """the reference captured at the BASELINE.json configuration shapes
+    (tests/golden/make_baseline.py): cfg1 / cfg2 at full size, cfg3 / cfg4 at reduced -d"""
+    if not os.path.isdir(BASELINE):
+        return []
+    return sorted(n for n in os.listdir(BASELINE)
+                  if n.startswith(prefix) and os.path.exists(os.path.join(BASELINE, n, "meta.json")))
+
+
+def load_baseline(name):
+    """-> meta (+ barrier, method_list), sampled full traces {(m, r): tokens}, data {direction: {(it, src, dst):
+    (len, chk)}}; meta["trace_sha1"][str(m)][r] is the sha1 of rank r's whole token string"""
+    p = os.path.join(BASELINE, name)
+    meta = json.load(open(os.path.join(p, "meta.json")))
+    meta["barrier"] = 0
+    meta["method_list"] = sorted(int(m) for m, v in meta["methods"].items() if v.get("status") == "ok")
+    traces = {}
+    for line in gzip.open(os.path.join(p, "trace_sample.txt.gz"), "rt"):
+        if line.strip():
+            head, _, toks = line.rstrip("\n").partition(": ")
+            m, r = head.split()
+            traces[(int(m[1:]), int(r[1:]))] = toks
+    data = {}
+    src_dir = os.path.join(BASELINE, meta["data_from"])
+    for direction in ("a2m", "m2a"):
+        rows = gzip.open(os.path.join(src_dir, "data_%s.csv.gz" % direction), "rt").read().split("\n")[1:]
+        data[direction] = {tuple(map(int, r.split(",")[:3])): (int(r.split(",")[3]), int(r.split(",")[4], 16))
+                           for r in rows if r}
+    return meta, traces, data

@@ -9,7 +9,16 @@ import time
 import types
 
 
+def _faults(var):
+    """XG_FAKE_VERIFY_FAIL / XG_FAKE_P2P_FAIL: comma-separated colon tuples of ints"""
+    return {tuple(int(x) for x in f.split(":")) for f in os.environ.get(var, "").split(",") if f.strip()}
+
+
 def make(real_xg):
+    """fault injection (bench.py's partial-failure paths), on the rank XG_FAKE_FAIL_RANK names
+    (default: every rank): XG_FAKE_VERIFY_FAIL=<method>:<pack_max_seg>:<pack_form>,... makes that
+    plan's verify report a wrong slot; XG_FAKE_P2P_FAIL=<n>,... makes the n-th p2p_bench call
+    (0-based: 0 = bench.py's xGMI ceiling, 1.. = its sweep) raise XGError"""
     fake = types.ModuleType("xg")
     for name in ("aggregator_list", "Schedule", "XGError", "NBUF", "BUF_SEND", "BUF_RECV",
                  "BUF_STAGE_SEND", "BUF_STAGE_RECV", "BUF_SCRATCH", "PACK_TWO_SIDED", "PACK_ONE_SIDED",
@@ -21,6 +30,10 @@ def make(real_xg):
     # would see): compared across ranks by tests/test_rccl_calls.py
     trace = []
     fake.trace = trace
+
+    def _on_fail_rank(rank):
+        v = os.environ.get("XG_FAKE_FAIL_RANK")
+        return v is None or int(v) == rank
 
     def _wait_all(d, name, nranks):
         t0 = time.time()
@@ -96,6 +109,8 @@ def make(real_xg):
         def p2p_bench(self, nbytes, mode=0, reps=20):
             calls["p2p_bench"] += 1
             trace.append(["p2p_bench", int(nbytes), int(mode), int(reps)])
+            if _on_fail_rank(self.rank) and (calls["p2p_bench"] - 1,) in _faults("XG_FAKE_P2P_FAIL"):
+                raise real_xg.XGError("xg_p2p_bench failed with code 5 (injected)")
             return 50.0, nbytes / 50e9
 
         def close(self):
@@ -103,7 +118,7 @@ def make(real_xg):
 
     class MethodRun:
         def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None, pack_min=0, pack_form=-1):
-            self.ctx, self.sched, self.pack_max_seg = ctx, sched, pack_max_seg
+            self.ctx, self.sched, self.pack_max_seg, self.pack_form = ctx, sched, pack_max_seg, pack_form
             G, g = ctx.nranks, ctx.rank
             if G > 1:     # as the real MethodRun: refuse calls RCCL would not pair
                 sched.check_pairing(G, pack_max_seg, pack_min, pack_form)
@@ -131,7 +146,11 @@ def make(real_xg):
 
         def verify(self):
             n = len(self.slots)
-            return [0] * n, [0] * n, [-1] * n
+            bad = [0] * n
+            if n and _on_fail_rank(self.ctx.rank) and \
+                    (self.sched.method, self.pack_max_seg, self.pack_form) in _faults("XG_FAKE_VERIFY_FAIL"):
+                bad[0] = 7
+            return [0] * n, bad, [-1] * n
 
         def enqueue(self):
             trace.append(["enqueue"] + self.key)

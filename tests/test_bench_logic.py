@@ -116,3 +116,60 @@ def test_bench_under_torchrun_launch_form(tmp_path):
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["xgmi"]["cross_gpu_bytes_per_step"] > 0
+
+
+def _run_job(world, argv, tmp_path, extra_env):
+    """all `world` ranks as processes whose barriers and MAX reductions really span the job
+    (XG_FAKE_BARRIER_DIR), so a failure on one rank reaches every rank's decisions"""
+    procs = []
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                   XG_RDZV_KEY="fault_%s_%d" % (tmp_path.name, world), XG_FAKE_BARRIER_DIR=str(tmp_path),
+                   **extra_env)
+        procs.append(subprocess.Popen([sys.executable, "-c", DRIVER.format(repo=REPO, argv=argv)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    return [p.returncode for p in procs], outs
+
+
+ARGV2 = ["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--methods", "1,2"]
+
+
+def test_bench_excludes_a_form_that_fails_verification_on_one_gpu(tmp_path):
+    """packed one-sided m1 delivers a wrong slot on GPU 1 only: both ranks drop that form (MAX
+    over the GPUs), the line names why, and is printed from the forms that passed"""
+    rcs, outs = _run_job(2, ARGV2, tmp_path, {"XG_FAKE_VERIFY_FAIL": "1:%d:1" % (4 << 20), "XG_FAKE_FAIL_RANK": "1"})
+    assert rcs == [0, 0], [o[1][-1500:] for o in outs]
+    out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+    t1 = out["pack_autotune_ms_per_run"]["1"]
+    assert t1["packed_one_sided"].startswith("verify failed: 1 slots")
+    assert t1["chosen"] in ("direct", "packed_two_sided") and "packed_one_sided_ms" not in t1
+    assert set(out["pack_autotune_ms_per_run"]["2"]) >= {"direct_ms", "packed_one_sided_ms", "packed_two_sided_ms"}
+    assert out["value"] > 0 and out["xgmi"]["sweep"] and out["xgmi"]["sweep_error"] is None
+
+
+def test_bench_fails_with_a_line_when_every_form_of_a_method_fails(tmp_path):
+    bad = ",".join("2:%d:%d" % f for f in ((0, -1), (4 << 20, 1), (4 << 20, 0)))
+    rcs, outs = _run_job(2, ARGV2, tmp_path, {"XG_FAKE_VERIFY_FAIL": bad, "XG_FAKE_FAIL_RANK": "0"})
+    assert rcs == [1, 1], [o[1][-1500:] for o in outs]
+    lines = [l for l in outs[0][0].splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and not [l for l in outs[1][0].splitlines() if l.startswith("{")]
+    out = json.loads(lines[0])
+    assert out["value"] is None and "method(s) 2" in out["error"]
+    assert set(out["failed_methods"]["2"]) == {"direct", "packed_one_sided", "packed_two_sided"}
+
+
+def test_bench_survives_a_failing_ceiling_and_sweep(tmp_path):
+    """an RCCL error on GPU 1 in the xGMI ceiling (p2p_bench call 0) and in the sweep's 1 MiB
+    all-pairs case (call 6): the line still comes, with null + the error for each, and the
+    sweep rows before the failing case"""
+    rcs, outs = _run_job(2, ARGV2, tmp_path, {"XG_FAKE_P2P_FAIL": "0,6", "XG_FAKE_FAIL_RANK": "1"})
+    assert rcs == [0, 0], [o[1][-1500:] for o in outs]
+    out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+    x = out["xgmi"]
+    assert x["peak"] is None and x["frac"] is None and x["ceiling_error"] == "failed on another GPU"
+    assert x["achieved"] > 0 and out["value"] > 0
+    assert x["sweep_error"] == "all_pairs 1048576 B: failed on another GPU"
+    assert [(r["mode"], r["bytes"]) for r in x["sweep"]] == [("one_way_1_to_0", 4096), ("all_pairs", 4096),
+                                                             ("one_way_1_to_0", 65536), ("all_pairs", 65536),
+                                                             ("one_way_1_to_0", 1 << 20)]

@@ -39,6 +39,29 @@ def test_plans_deliver_every_byte(xg, case, G):
                 assert sum(views[0].sync_after) >= 1 or m == 13
 
 
+P256_CASES = [  # (A, d, c, methods): configs[3] and configs[4]'s shapes at reduced -d
+    (32, 48, 200000000, (1, 2, 9, 10)),
+    (64, 16, 1, (7, 11, 12)),
+    (64, 16, 3, (7, 11, 12)),
+    (64, 16, 8, (7, 11, 12)),
+]
+
+
+@pytest.mark.parametrize("case", P256_CASES, ids=lambda c: "A%d_d%d_c%d" % c[:3])
+def test_p256_plans_deliver_every_byte(xg, case):
+    """The plans the 8-GPU run of configs[3] / configs[4] executes (P = 256, 32 or 64 ranks per
+    GPU, 32 / 64 aggregators), at a reduced -d, through the race-checked executor: direct,
+    two-sided and one-sided, every received byte against the closed form"""
+    A, d, c, methods = case
+    P, G = 256, 8
+    rl = xg.aggregator_list(P, A)
+    for m in methods:
+        s = xg.Schedule(m, P, A, d, c, rl, ntimes=2, iteration=1)
+        for pack, form in FORMS:
+            _views, regs = simulate(s, G, it=1, mode=1, pack=pack, form=form)
+            check_recv(s, G, regs, it=1, mode=1)
+
+
 def test_pack_decision_and_volume(xg):
     """Two-sided packing: >= 2 segments to a peer with mean < pack_max_seg -> one RCCL op per
     peer and direction."""
