@@ -62,6 +62,10 @@ int xg_init_virtual(xg_ctx **out, int rank, int nranks, int device);
 int xg_finalize(xg_ctx *ctx);
 int xg_rank(const xg_ctx *ctx);
 int xg_nranks(const xg_ctx *ctx);
+/* The self_max this context posts with (XG_SELF_MAX at xg_init, default 256 KiB): a cross-GPU
+ * step whose local part moves <= this many bytes lists it as self send/recv pairs in its RCCL
+ * group (xg_devplan_step_calls).  The pairing proof of a job must use the same value. */
+int64_t xg_self_max(const xg_ctx *ctx);
 int xg_barrier(xg_ctx *ctx);
 int xg_allreduce_max(xg_ctx *ctx, double *vals, int n);       /* in place, MAX over all GPUs (any n) */
 int xg_sync(xg_ctx *ctx);                                      /* this context's stream */

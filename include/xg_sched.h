@@ -213,6 +213,9 @@ enum { XG_PACK_TWO_SIDED = 0, XG_PACK_ONE_SIDED = 1 };
 #define XG_RUN_CALL_BYTES (1 << 20)
 xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
                                   int form);
+/* All three return NULL (nothing leaked) when the host runs out of memory while building: every
+ * rank of a job builds plans, and xg_run_method turns a NULL on any rank into an error all ranks
+ * agree on before any of them posts a call.  xg_devplan_free(NULL) is a no-op. */
 void xg_devplan_free(xg_devplan *p);
 
 /* ---------------------------------------------------------------- RCCL calls (calls.c)

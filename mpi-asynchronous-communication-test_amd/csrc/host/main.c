@@ -225,7 +225,7 @@ int main(int argc, char **argv)
          * started with different ones would post calls nobody pairs and hang -- compare a
          * digest (FNV-1a of argv and the planning settings, in 16-bit parts) first */
         static const char *keys[] = {"XG_PROCS", "XG_VERIFY", "XG_FINGERPRINT", "XG_EAGER_LIMIT", "XG_PACK_MAX_SEG",
-                                     "XG_PACK_MIN", "XG_PACK_FORM", NULL};
+                                     "XG_PACK_MIN", "XG_PACK_FORM", "XG_SELF_MAX", NULL};
         uint64_t h = 0xcbf29ce484222325ull;
         double red[8];
         int k;

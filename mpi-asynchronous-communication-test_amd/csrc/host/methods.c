@@ -29,20 +29,48 @@ void xg_run_opts_default(xg_run_opts *o)
 #define TRY(x) do { rc = (x); if (rc) goto out; } while (0)
 
 /* A G-GPU job's RCCL calls pair step by step as RCCL pairs them (xg_devplans_match over
- * every GPU's plan, calls.c); otherwise err says which call would not. */
-static int pairing_ok(const xg_sched *s, int G, int64_t pack_max_seg, int64_t pack_min, int form, char *err,
-                      size_t errlen)
+ * every GPU's plan, calls.c), the calls listed with the self_max this process posts with
+ * (xg_self_max: the exact lists enqueue_step hands RCCL).  -> XG_OK, XG_EARG (err says which
+ * call would not pair) or XG_ENOMEM. */
+static int pairing_ok(const xg_sched *s, int G, int64_t pack_max_seg, int64_t pack_min, int form, int64_t self_max,
+                      char *err, size_t errlen)
 {
     xg_devplan **plans = (xg_devplan **)calloc(G, sizeof *plans);
-    int g, ok = 0;
+    int g, rc = XG_OK;
     char why[400];
-    if (!plans) return 0;
-    for (g = 0; g < G; ++g) plans[g] = xg_devplan_build_form(s, G, g, pack_max_seg, pack_min, form);
-    if (xg_devplans_match((const xg_devplan *const *)plans, G, 0, NULL, 0, why, sizeof why) >= 0) ok = 1;
-    else snprintf(err, errlen, "the GPUs' RCCL calls do not pair: %s", why);
+    if (!plans) {
+        snprintf(err, errlen, "pairing check: out of host memory");
+        return XG_ENOMEM;
+    }
+    for (g = 0; g < G && rc == XG_OK; ++g)
+        if (!(plans[g] = xg_devplan_build_form(s, G, g, pack_max_seg, pack_min, form))) {
+            snprintf(err, errlen, "pairing check: out of host memory building GPU %d's plan", g);
+            rc = XG_ENOMEM;
+        }
+    if (rc == XG_OK && xg_devplans_match((const xg_devplan *const *)plans, G, self_max, NULL, 0, why, sizeof why) < 0) {
+        snprintf(err, errlen, "the GPUs' RCCL calls do not pair: %s", why);
+        rc = XG_EARG;
+    }
     for (g = 0; g < G; ++g) xg_devplan_free(plans[g]);
     free(plans);
-    return ok;
+    return rc;
+}
+
+/* One MAX reduction over the job: whether any GPU failed (and the highest code).  Each GPU plans,
+ * allocates, fills and loads its part alone; one that failed must not return while its peers go
+ * on to post RCCL calls it will never pair (they would wait forever), so every GPU learns the
+ * outcome here and all return an error alike.  local_rc: this GPU's result so far. */
+static int peers_agree(xg_ctx *ctx, int local_rc, char *err, size_t errlen)
+{
+    double red[2];
+    int rc;
+    red[0] = local_rc ? 1.0 : 0.0;
+    red[1] = (double)local_rc;
+    if ((rc = xg_allreduce_max(ctx, red, 2))) return local_rc ? local_rc : rc;
+    if (red[0] == 0.0) return XG_OK;
+    if (local_rc) return local_rc;
+    snprintf(err, errlen, "another GPU of the job failed (code %d) setting up or running this method", (int)red[1]);
+    return (int)red[1];
 }
 
 /* Every GPU of a job must plan from the same inputs: each derives every GPU's RCCL calls from
@@ -61,13 +89,13 @@ static uint64_t fnv(uint64_t h, const void *p, size_t n)
 static int inputs_agree(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list,
                         int comm_size, int iter, int ntimes, const xg_run_opts *o, char *err, size_t errlen)
 {
-    int64_t v[13];
+    int64_t v[14];
     double red[8];
     uint64_t h = 0xcbf29ce484222325ull;
     int i, rc;
     v[0] = method; v[1] = procs; v[2] = cb_nodes; v[3] = data_size; v[4] = comm_size; v[5] = iter;
     v[6] = ntimes; v[7] = o->eager_limit; v[8] = o->pack_max_seg; v[9] = o->pack_min_bytes;
-    v[10] = o->proc_node; v[11] = o->barrier_type; v[12] = o->pack_form;
+    v[10] = o->proc_node; v[11] = o->barrier_type; v[12] = o->pack_form; v[13] = xg_self_max(ctx);
     h = fnv(h, v, sizeof v);
     h = fnv(h, rank_list, sizeof(int) * (size_t)cb_nodes);
     for (i = 0; i < 4; ++i) {
@@ -84,6 +112,50 @@ static int inputs_agree(xg_ctx *ctx, int method, int procs, int cb_nodes, int da
     return XG_OK;
 }
 
+/* Set-up of one GPU's part (untimed, no collective call): schedule, pairing proof, device plan,
+ * regions, fingerprint fill, plan upload and the host arrays.  -> XG_OK or the first error. */
+static int setup(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list, int comm_size,
+                 int iter, int ntimes, const xg_run_opts *o, xg_sched **s, xg_devplan **dp, xg_regions **reg,
+                 xg_plan **plan, double **done, double **post, char *err, size_t errlen)
+{
+    const int g = xg_rank(ctx), G = xg_nranks(ctx);
+    xg_segrun *runs;
+    int rc, nruns;
+    *s = xg_sched_build_iter(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, o->proc_node,
+                             o->barrier_type, o->eager_limit, iter, err, errlen);
+    if (!*s) return XG_ESCHED;
+    /* every GPU derives every GPU's calls from the same schedule, so every GPU refuses a job
+     * that would not pair alike -- before any of them posts a call that could wait forever */
+    if (G > 1 && (rc = pairing_ok(*s, G, o->pack_max_seg, o->pack_min_bytes, o->pack_form, xg_self_max(ctx), err,
+                                  errlen)))
+        return rc;
+    if (!(*dp = xg_devplan_build_form(*s, G, g, o->pack_max_seg, o->pack_min_bytes, o->pack_form))) {
+        snprintf(err, errlen, "device plan: out of host memory");
+        return XG_ENOMEM;
+    }
+    if ((rc = xg_regions_alloc(ctx, (*dp)->region_bytes, reg))) {
+        snprintf(err, errlen, "HBM regions of %lld + %lld + %lld + %lld + %lld bytes: allocation failed (%d)",
+                 (long long)(*dp)->region_bytes[0], (long long)(*dp)->region_bytes[1],
+                 (long long)(*dp)->region_bytes[2], (long long)(*dp)->region_bytes[3],
+                 (long long)(*dp)->region_bytes[4], rc);
+        return rc;
+    }
+    nruns = xg_fill_runs(*s, G, g, NULL);
+    runs = (xg_segrun *)malloc(sizeof(xg_segrun) * (nruns + 1));
+    *done = (double *)calloc(xg_sched_nsteps(*s) + 1, sizeof(double));
+    *post = (double *)calloc(xg_sched_nsteps(*s) + 1, sizeof(double));
+    if (!runs || !*done || !*post) {
+        free(runs);
+        snprintf(err, errlen, "out of host memory");
+        return XG_ENOMEM;
+    }
+    xg_fill_runs(*s, G, g, runs);
+    rc = xg_fill(*reg, runs, nruns, data_size, iter, o->fingerprint);
+    free(runs);
+    if (rc) return rc;
+    return xg_plan_load(ctx, *reg, *dp, plan);
+}
+
 int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list,
                   int comm_size, xg_timer *timers, int iter, int ntimes, const xg_run_opts *opts,
                   int64_t *bad_slots, char *err, size_t errlen)
@@ -91,40 +163,26 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
     xg_run_opts dflt;
     const int g = xg_rank(ctx), G = xg_nranks(ctx);
     char ebuf[512];
-    xg_sched *s;
+    xg_sched *s = NULL;
     xg_devplan *dp = NULL;
     xg_regions *reg = NULL;
     xg_plan *plan = NULL;
-    xg_segrun *runs = NULL;
     xg_slot *slots = NULL;
-    int64_t *bad = NULL;
+    int64_t *bad = NULL, nbad = 0;
     double *done = NULL, *post = NULL, wall = 0;
-    int rc = 0, nruns, nsteps, lo, hi, r, i;
+    int rc = 0, agreed = 0, lo, hi, r, i;
     if (!opts) { xg_run_opts_default(&dflt); opts = &dflt; }
     if (!err) { err = ebuf; errlen = sizeof ebuf; }
+    err[0] = 0;
     if (bad_slots) *bad_slots = 0;
     if (G > 1 && (rc = inputs_agree(ctx, method, procs, cb_nodes, data_size, rank_list, comm_size, iter, ntimes, opts,
                                     err, errlen)))
         return rc;
-    s = xg_sched_build_iter(method, procs, cb_nodes, data_size, comm_size, rank_list, ntimes, opts->proc_node,
-                            opts->barrier_type, opts->eager_limit, iter, err, errlen);
-    if (!s) return XG_ESCHED;
-    if (G > 1 && !pairing_ok(s, G, opts->pack_max_seg, opts->pack_min_bytes, opts->pack_form, err, errlen)) {
-        /* every GPU derives every GPU's calls from the same schedule, so every GPU refuses
-         * alike -- before any of them posts a call that could wait forever */
-        xg_sched_free(s);
-        return XG_EARG;
-    }
-    dp = xg_devplan_build_form(s, G, g, opts->pack_max_seg, opts->pack_min_bytes, opts->pack_form);
-    TRY(xg_regions_alloc(ctx, dp->region_bytes, &reg));
-    nruns = xg_fill_runs(s, G, g, NULL);
-    runs = (xg_segrun *)malloc(sizeof(xg_segrun) * (nruns + 1));
-    xg_fill_runs(s, G, g, runs);
-    TRY(xg_fill(reg, runs, nruns, data_size, iter, opts->fingerprint));
-    TRY(xg_plan_load(ctx, reg, dp, &plan));
-    nsteps = xg_sched_nsteps(s);
-    done = (double *)calloc(nsteps + 1, sizeof(double));
-    post = (double *)calloc(nsteps + 1, sizeof(double));
+    rc = setup(ctx, method, procs, cb_nodes, data_size, rank_list, comm_size, iter, ntimes, opts, &s, &dp, &reg, &plan,
+               &done, &post, err, errlen);
+    if (G > 1) rc = peers_agree(ctx, rc, err, errlen);      /* before the first call of the exchange */
+    if (rc) goto out;
+    agreed = 1;
     TRY(xg_barrier(ctx));                                   /* MPI_Barrier before total_start */
     TRY(xg_plan_run(plan, done, post, &wall));
     xg_block_range(procs, G, g, &lo, &hi);
@@ -137,18 +195,27 @@ int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_siz
         int ns = xg_verify_slots(s, G, g, NULL);
         slots = (xg_slot *)malloc(sizeof(xg_slot) * (ns + 1));
         bad = (int64_t *)calloc(ns + 1, sizeof(int64_t));
+        if (!slots || !bad) {
+            snprintf(err, errlen, "verify: out of host memory");
+            rc = XG_ENOMEM;
+            goto out;
+        }
         xg_verify_slots(s, G, g, slots);
         TRY(xg_verify(reg, slots, ns, data_size, iter, opts->fingerprint, NULL, bad, NULL));
         for (i = 0; i < ns; ++i)
             if (bad[i]) {
-                if (bad_slots && *bad_slots == 0)
-                    fprintf(stderr, "rank %d, message is wrong from rank %d\n", slots[i].dst, slots[i].src);
-                if (bad_slots) ++*bad_slots;
+                if (nbad == 0) fprintf(stderr, "rank %d, message is wrong from rank %d\n", slots[i].dst, slots[i].src);
+                ++nbad;
             }
+        if (bad_slots) *bad_slots = nbad;
     }
 out:
+    /* a GPU that failed after the set-up (the run, the verify) tells its peers too: the caller's
+     * next collective (the timer reduction) must not wait for it.  A run that failed inside RCCL
+     * may leave the communicator unusable -- then this reports that error as well. */
+    if (G > 1 && agreed) rc = peers_agree(ctx, rc, err, errlen);
     if (rc && err[0] == 0) snprintf(err, errlen, "device error %d (see stderr)", rc);
-    free(runs); free(slots); free(bad); free(done); free(post);
+    free(slots); free(bad); free(done); free(post);
     if (plan) xg_plan_free(plan);
     if (reg) xg_regions_free(reg);
     xg_devplan_free(dp);

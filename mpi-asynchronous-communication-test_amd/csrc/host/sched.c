@@ -1738,17 +1738,31 @@ int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf)
 }
 
 /* ------------------------------------------------------------------ device plan */
-typedef struct { xg_copy *v; int n, cap; } cvec;
-typedef struct { xg_p2p *v; int n, cap; } pvec;
+/* Growable arrays of the device-plan builder.  The builder runs on every rank of a job and
+ * must not stop one rank alone: when the host runs out of memory, a push lands in `sink` and
+ * `fail` is set; xg_devplan_build_form then frees what it built and returns NULL, which the
+ * caller turns into an error every rank agrees on (methods.c peers_agree). */
+typedef struct { xg_copy *v; int n, cap, fail; xg_copy sink; } cvec;
+typedef struct { xg_p2p *v; int n, cap, fail; xg_p2p sink; } pvec;
 static xg_copy *cpush(cvec *c)
 {
-    if (c->n == c->cap) { c->cap = c->cap ? 2 * c->cap : 256; c->v = (xg_copy *)realloc(c->v, sizeof(xg_copy) * c->cap); if (!c->v) abort(); }
+    if (c->n == c->cap) {
+        const int cap = c->cap ? 2 * c->cap : 256;
+        xg_copy *v = c->fail ? NULL : (xg_copy *)realloc(c->v, sizeof(xg_copy) * cap);
+        if (!v) { c->fail = 1; memset(&c->sink, 0, sizeof c->sink); return &c->sink; }
+        c->v = v; c->cap = cap;
+    }
     memset(&c->v[c->n], 0, sizeof(xg_copy));
     return &c->v[c->n++];
 }
 static xg_p2p *ppush(pvec *c)
 {
-    if (c->n == c->cap) { c->cap = c->cap ? 2 * c->cap : 256; c->v = (xg_p2p *)realloc(c->v, sizeof(xg_p2p) * c->cap); if (!c->v) abort(); }
+    if (c->n == c->cap) {
+        const int cap = c->cap ? 2 * c->cap : 256;
+        xg_p2p *v = c->fail ? NULL : (xg_p2p *)realloc(c->v, sizeof(xg_p2p) * cap);
+        if (!v) { c->fail = 1; memset(&c->sink, 0, sizeof c->sink); return &c->sink; }
+        c->v = v; c->cap = cap;
+    }
     memset(&c->v[c->n], 0, sizeof(xg_p2p));
     return &c->v[c->n++];
 }
@@ -1770,12 +1784,14 @@ static int use_pack(int n, int64_t total, int64_t pack_max_seg, int64_t pack_min
 /* region base of every rank hosted by the GPU the plan is for */
 typedef struct { int64_t *base[XG_NBUF]; } plan_bases;
 
-static void plan_bases_init(plan_bases *pb, const xg_sched *s, int G, int g)
+/* -> 0, or -1 when the host is out of memory (pb is then freeable) */
+static int plan_bases_init(plan_bases *pb, const xg_sched *s, int G, int g)
 {
-    int lo, hi, r, k;
+    int lo, hi, r, k, fail = 0;
     int64_t scr = 0;
     (void)g;
-    for (k = 0; k < XG_NBUF; ++k) pb->base[k] = (int64_t *)calloc(s->P, sizeof(int64_t));
+    for (k = 0; k < XG_NBUF; ++k) fail |= !(pb->base[k] = (int64_t *)calloc(s->P + 1, sizeof(int64_t)));
+    if (fail) return -1;
     for (r = 0; r < s->P; ++r) {
         pb->base[XG_BUF_SEND][r] = xg_send_offset(s, G, r);
         pb->base[XG_BUF_RECV][r] = xg_recv_offset(s, G, r);
@@ -1784,6 +1800,7 @@ static void plan_bases_init(plan_bases *pb, const xg_sched *s, int G, int g)
         xg_block_range(s->P, G, k, &lo, &hi);
         for (scr = 0, r = lo; r < hi; ++r) { pb->base[XG_BUF_SCRATCH][r] = scr; scr += s->scr_size[r]; }
     }
+    return 0;
 }
 
 static void plan_bases_free(plan_bases *pb)
@@ -1834,7 +1851,7 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
  * fewer copied bytes + XG_RUN_CALL_BYTES per call wins (ties: destination order).  Both GPUs
  * of the pair derive it from the same message list, so their calls pair one to one. */
 typedef struct {
-    int n, nrun, by_src;
+    int n, nrun, by_src, fail;   /* fail: out of host memory (the plan is discarded) */
     int *idx;                 /* message indices, run order */
     int *run_b;               /* run r = idx[run_b[r] .. run_b[r + 1]) */
     unsigned char *staged;    /* run r goes through staging */
@@ -1856,8 +1873,13 @@ static int64_t os_layout(const xg_sched *s, const plan_bases *pb, oneside *o, in
 {
     int i, r;
     int64_t cost = 0;
-    os_key *key = (os_key *)xmalloc(sizeof(os_key) * ((size_t)o->n + 1));
+    os_key *key = (os_key *)malloc(sizeof(os_key) * ((size_t)o->n + 1));
     o->by_src = by_src;
+    if (!key) {
+        o->fail = 1;
+        o->nrun = 0;
+        return 0;
+    }
     for (i = 0; i < o->n; ++i) {
         const xg_msg *m = os_msg(s, o, i);
         key[i].buf = by_src ? m->sbuf : m->dbuf;
@@ -1908,9 +1930,17 @@ static void os_build(const xg_sched *s, const plan_bases *pb, const int *order, 
         const xg_msg *m = &s->msgs[order[k]];
         if (moves(m) && xg_gpu_of(s->P, G, m->src) == gs && xg_gpu_of(s->P, G, m->dst) == gd) o->n++;
     }
-    o->idx = (int *)xmalloc(sizeof(int) * ((size_t)o->n + 1));
-    o->run_b = (int *)xmalloc(sizeof(int) * ((size_t)o->n + 2));
-    o->staged = (unsigned char *)xmalloc((size_t)o->n + 1);
+    o->idx = (int *)malloc(sizeof(int) * ((size_t)o->n + 1));
+    o->run_b = (int *)malloc(sizeof(int) * ((size_t)o->n + 2));
+    o->staged = (unsigned char *)malloc((size_t)o->n + 1);
+    if (!o->idx || !o->run_b || !o->staged) {
+        free(o->idx); free(o->run_b); free(o->staged);
+        o->idx = o->run_b = NULL;
+        o->staged = NULL;
+        o->n = o->nrun = 0;
+        o->fail = 1;
+        return;
+    }
     o->n = 0;
     for (k = b; k < e; ++k) {
         const xg_msg *m = &s->msgs[order[k]];
@@ -1921,41 +1951,46 @@ static void os_build(const xg_sched *s, const plan_bases *pb, const int *order, 
     if (cost_s < cost_d) os_layout(s, pb, o, 1);
 }
 
+/* frees the arrays; keeps `fail` for the caller to see */
 static void os_free(oneside *o)
 {
+    const int fail = o->fail;
     free(o->idx); free(o->run_b); free(o->staged);
     memset(o, 0, sizeof *o);
+    o->fail = fail;
 }
 
 xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
                                   int form)
 {
     xg_devplan *dp = (xg_devplan *)calloc(1, sizeof *dp);
-    int nst = s->nsteps, i, st, G = ngpus;
-    int *cnt = (int *)calloc(nst + 1, sizeof(int)), *order = (int *)xmalloc(sizeof(int) * (s->nmsg + 1));
-    cvec pre = {0}, post = {0};
-    pvec pp = {0};
+    int nst = s->nsteps, i, st, G = ngpus, oom = 0;
+    int *cnt = (int *)calloc(nst + 1, sizeof(int)), *order = (int *)malloc(sizeof(int) * (s->nmsg + 1));
+    int *pos = (int *)malloc(sizeof(int) * (nst + 1));
+    cvec pre, post;
+    pvec pp;
     int64_t stage_s_max = 0, stage_r_max = 0;
     int *bucket_n = (int *)calloc((size_t)G * 2, sizeof(int));
     int64_t *bucket_b = (int64_t *)calloc((size_t)G * 2, sizeof(int64_t));
     oneside *os_out = (oneside *)calloc((size_t)G, sizeof(oneside)), *os_in = (oneside *)calloc((size_t)G, sizeof(oneside));
     plan_bases pb;
+    memset(&pre, 0, sizeof pre); memset(&post, 0, sizeof post); memset(&pp, 0, sizeof pp);
+    memset(&pb, 0, sizeof pb);
     if (form != XG_PACK_TWO_SIDED && form != XG_PACK_ONE_SIDED) form = XG_PACK_FORM_DEFAULT;
-    plan_bases_init(&pb, s, G, g);
+    if (!dp || !cnt || !order || !pos || !bucket_n || !bucket_b || !os_out || !os_in || plan_bases_init(&pb, s, G, g) ||
+        !(dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan)))) {
+        oom = 1;
+        goto done;
+    }
     dp->gpu = g; dp->ngpus = G; dp->nsteps = nst;
-    dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan));
     /* in-loop MPI_Barrier -> device-side barrier after the step it completes at (G > 1) */
     for (i = 0; i < s->nbarrier; ++i)
         if (G > 1 && s->barrier_epoch[i] >= 0 && s->barrier_epoch[i] < nst) dp->steps[s->barrier_epoch[i]].sync_after = 1;
     /* counting sort of messages by step, stable in message order */
     for (i = 0; i < s->nmsg; ++i) cnt[s->msgs[i].step + 1]++;
     for (st = 0; st < nst; ++st) cnt[st + 1] += cnt[st];
-    {
-        int *pos = (int *)xmalloc(sizeof(int) * (nst + 1));
-        memcpy(pos, cnt, sizeof(int) * (nst + 1));
-        for (i = 0; i < s->nmsg; ++i) order[pos[s->msgs[i].step]++] = i;
-        free(pos);
-    }
+    memcpy(pos, cnt, sizeof(int) * (nst + 1));
+    for (i = 0; i < s->nmsg; ++i) order[pos[s->msgs[i].step]++] = i;
     dp->region_bytes[XG_BUF_SEND] = xg_region_bytes(s, G, g, XG_BUF_SEND);
     dp->region_bytes[XG_BUF_RECV] = xg_region_bytes(s, G, g, XG_BUF_RECV);
     dp->region_bytes[XG_BUF_SCRATCH] = xg_region_bytes(s, G, g, XG_BUF_SCRATCH);
@@ -1997,6 +2032,7 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
                     os_build(s, &pb, order, b, e, G, g, p, &os_out[p]);
                 if (bucket_n[G + p] && use_pack(bucket_n[G + p], bucket_b[G + p], pack_max_seg, pack_min))
                     os_build(s, &pb, order, b, e, G, p, g, &os_in[p]);
+                oom |= os_out[p].fail | os_in[p].fail;
             }
         /* packs (into staging) join the pre-exchange copy launch */
         for (p = 0; p < G; ++p) {
@@ -2133,7 +2169,7 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
                     dp->remote_recv_bytes += bucket_b[G + p];
                 }
             }
-            if (soff != sbase) { fprintf(stderr, "xg_devplan_build: staging mismatch\n"); abort(); }
+            if (soff != sbase && !oom) { fprintf(stderr, "xg_devplan_build: staging mismatch\n"); abort(); }
         }
         sp->p2p_count = pp.n - sp->p2p_begin;
         sp->post_count = post.n - sp->post_begin;
@@ -2143,20 +2179,30 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
             os_free(&os_out[p]);
             os_free(&os_in[p]);
         }
+        if (oom) goto done;
     }
-    free(os_out); free(os_in);
     /* post copies are stored after the pre copies in one array */
+    oom |= pre.fail | post.fail | pp.fail;
     dp->ncopy = pre.n + post.n;
-    dp->copies = (xg_copy *)xmalloc(sizeof(xg_copy) * (dp->ncopy + 1));
-    if (pre.n) memcpy(dp->copies, pre.v, sizeof(xg_copy) * pre.n);
-    if (post.n) memcpy(dp->copies + pre.n, post.v, sizeof(xg_copy) * post.n);
-    for (st = 0; st < nst; ++st) dp->steps[st].post_begin += pre.n;
-    dp->np2p = pp.n;
-    dp->p2p = pp.v ? pp.v : (xg_p2p *)xmalloc(sizeof(xg_p2p));
-    dp->region_bytes[XG_BUF_STAGE_SEND] = stage_s_max;
-    dp->region_bytes[XG_BUF_STAGE_RECV] = stage_r_max;
-    free(pre.v); free(post.v); free(cnt); free(order); free(bucket_n); free(bucket_b);
+    if (!oom && (dp->copies = (xg_copy *)malloc(sizeof(xg_copy) * (dp->ncopy + 1)))) {
+        if (pre.n) memcpy(dp->copies, pre.v, sizeof(xg_copy) * pre.n);
+        if (post.n) memcpy(dp->copies + pre.n, post.v, sizeof(xg_copy) * post.n);
+        for (st = 0; st < nst; ++st) dp->steps[st].post_begin += pre.n;
+        dp->np2p = pp.n;
+        dp->p2p = pp.v ? pp.v : (xg_p2p *)malloc(sizeof(xg_p2p));
+        if (dp->p2p == pp.v) pp.v = NULL;           /* owned by the plan now */
+        dp->region_bytes[XG_BUF_STAGE_SEND] = stage_s_max;
+        dp->region_bytes[XG_BUF_STAGE_RECV] = stage_r_max;
+    }
+    oom |= !dp->copies || !dp->p2p;
+done:
+    free(pre.v); free(post.v); free(pp.v); free(cnt); free(order); free(pos); free(bucket_n); free(bucket_b);
+    free(os_out); free(os_in);
     plan_bases_free(&pb);
+    if (oom) {
+        xg_devplan_free(dp);
+        return NULL;
+    }
     return dp;
 }
 

@@ -597,6 +597,7 @@ extern "C" int xg_finalize(xg_ctx *c)
 
 extern "C" int xg_rank(const xg_ctx *c) { return c->rank; }
 extern "C" int xg_nranks(const xg_ctx *c) { return c->nranks; }
+extern "C" int64_t xg_self_max(const xg_ctx *c) { return c ? c->self_max : 0; }
 
 extern "C" int xg_sync(xg_ctx *c)
 {

@@ -385,23 +385,28 @@ class Schedule:
     def devplan(self, ngpus, g, pack_max_seg=4 << 20, pack_min=0, pack_form=-1):
         return DevicePlanView(self, ngpus, g, pack_max_seg, pack_min, pack_form)
 
-    def check_pairing(self, ngpus, pack_max_seg=4 << 20, pack_min=0, pack_form=-1):
+    def check_pairing(self, ngpus, pack_max_seg=4 << 20, pack_min=0, pack_form=-1, self_max=0):
         """Refuse (XGError) a job whose GPUs' RCCL calls RCCL would not pair step by step
-        (xg_devplans_match over every GPU's plan, built in C); returns the number of pairs."""
+        (xg_devplans_match over every GPU's plan, built in C, the calls listed with the
+        self_max the runtime posts with); returns the number of pairs."""
         h = host()
         plans = [h.xg_devplan_build_form(self._h, ngpus, g, pack_max_seg, pack_min, pack_form)
                  for g in range(ngpus)]
         try:
+            if not all(plans):
+                raise XGError("method %d on %d GPUs: out of host memory building the device plans"
+                              % (self.method, ngpus))
             arr = (C.POINTER(DevPlan) * ngpus)(*plans)
             err = C.create_string_buffer(512)
-            n = h.xg_devplans_match(arr, ngpus, 0, None, 0, err, 512)
+            n = h.xg_devplans_match(arr, ngpus, self_max, None, 0, err, 512)
             if n < 0:
                 raise XGError("method %d on %d GPUs: RCCL calls do not pair: %s"
                               % (self.method, ngpus, err.value.decode()))
             return n
         finally:
             for q in plans:
-                h.xg_devplan_free(q)
+                if q:
+                    h.xg_devplan_free(q)
 
     def fill_runs(self, ngpus, g):
         n = host().xg_fill_runs(self._h, ngpus, g, None)
@@ -423,6 +428,9 @@ class DevicePlanView:
         self.sched = sched
         # pack_form: PACK_TWO_SIDED, PACK_ONE_SIDED, or -1 = the library's default (xg_sched.h)
         self._p = host().xg_devplan_build_form(sched.handle, ngpus, g, pack_max_seg, pack_min, pack_form)
+        if not self._p:
+            self._p = None
+            raise XGError("xg_devplan_build_form: out of host memory")
         p = self._p.contents
         self.gpu, self.ngpus, self.nsteps = p.gpu, p.ngpus, p.nsteps
         self.region_bytes = list(p.region_bytes)
@@ -476,6 +484,8 @@ def device():
         d.xg_vplans_run.argtypes = [C.POINTER(vp), ip, C.POINTER(C.c_double)]
         d.xg_vplans_run_rccl.argtypes = [C.POINTER(vp), ip, C.POINTER(C.c_double)]
         d.xg_plan_set_local_only.argtypes = [vp, ip]
+        d.xg_self_max.restype = i64
+        d.xg_self_max.argtypes = [vp]
         d.xg_barrier.argtypes = [vp]
         d.xg_sync.argtypes = [vp]
         d.xg_device_sync.argtypes = [vp]
@@ -653,7 +663,7 @@ class MethodRun:
         if G > 1 and not getattr(ctx, "is_virtual", False):
             # a real multi-GPU job: refuse, on every rank alike, calls RCCL would not pair
             # step by step, before any rank posts one (xg_devplans_match)
-            sched.check_pairing(G, pack_max_seg, pack_min, pack_form)
+            sched.check_pairing(G, pack_max_seg, pack_min, pack_form, d.xg_self_max(ctx.handle))
         self.view = sched.devplan(G, g, pack_max_seg, pack_min, pack_form)
         self._shared = regions is not None
         if regions is not None:

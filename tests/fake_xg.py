@@ -121,7 +121,8 @@ def make(real_xg):
             self.ctx, self.sched, self.pack_max_seg, self.pack_form = ctx, sched, pack_max_seg, pack_form
             G, g = ctx.nranks, ctx.rank
             if G > 1:     # as the real MethodRun: refuse calls RCCL would not pair
-                sched.check_pairing(G, pack_max_seg, pack_min, pack_form)
+                sched.check_pairing(G, pack_max_seg, pack_min, pack_form,
+                                    int(os.environ.get("XG_SELF_MAX", 256 << 10)))
             self.view = sched.devplan(G, g, pack_max_seg, pack_min, pack_form)
             # the RCCL calls this GPU's plan posts per run: per step its send/recv group and
             # its barrier (xg_devplan_step_calls), as a signature the ranks must agree on in

@@ -19,6 +19,8 @@
  * XG_HOST_DEV_DIR (required for nranks > 1): parent of the job's message directory,
  * named by the unique id rank 0 hands over.  XG_HOST_DEV_CORRUPT=<g>: GPU g flips
  * one byte of every message it receives (the verify path must see it).
+ * XG_HOST_DEV_FAIL_ALLOC=<g>: GPU g's region allocations fail (XG_ENOMEM), as hipMalloc
+ * does when HBM is exhausted -- every rank must then stop alike.
  */
 #include <errno.h>
 #include <stdint.h>
@@ -33,7 +35,8 @@
 #include "xg_sched.h"
 
 struct xg_ctx {
-    int rank, nranks, corrupt;
+    int rank, nranks, corrupt, fail_alloc;
+    int64_t self_max;          /* XG_SELF_MAX, as the runtime reads it at xg_init */
     char dir[3072];
     int64_t *sent, *recvd;     /* per peer: messages posted / taken */
     int64_t coll;              /* collectives so far */
@@ -93,6 +96,10 @@ int xg_init(xg_ctx **out, int rank, int nranks, int device, const void *uid)
     c->recvd = (int64_t *)calloc(nranks, sizeof(int64_t));
     env = getenv("XG_HOST_DEV_CORRUPT");
     c->corrupt = env ? atoi(env) : -1;
+    env = getenv("XG_HOST_DEV_FAIL_ALLOC");
+    c->fail_alloc = env ? atoi(env) == rank : 0;
+    env = getenv("XG_SELF_MAX");
+    c->self_max = env ? atoll(env) : (int64_t)256 << 10;
     env = getenv("XG_HOST_DEV_TIMEOUT");
     c->timeout = env ? atof(env) : 60.0;
     env = getenv("XG_HOST_DEV_DIR");
@@ -118,6 +125,7 @@ int xg_finalize(xg_ctx *c)
 }
 
 int xg_rank(const xg_ctx *c) { return c->rank; }
+int64_t xg_self_max(const xg_ctx *c) { return c->self_max; }
 int xg_nranks(const xg_ctx *c) { return c->nranks; }
 
 static int put_file(const char *dir, const char *name, const void *p, size_t n)
@@ -200,6 +208,11 @@ int xg_regions_alloc(xg_ctx *c, const int64_t region_bytes[XG_NBUF], xg_regions 
     int b;
     *out = NULL;
     if (!r) return XG_ENOMEM;
+    if (c->fail_alloc) {
+        free(r);
+        fprintf(stderr, "host_dev: GPU %d: region allocation fails (XG_HOST_DEV_FAIL_ALLOC)\n", c->rank);
+        return XG_ENOMEM;
+    }
     r->ctx = c;
     for (b = 0; b < XG_NBUF; ++b) {
         r->n[b] = region_bytes[b];
@@ -291,7 +304,6 @@ int xg_verify(xg_regions *r, const xg_slot *slots, int nslots, int64_t d, int it
 int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_plan **out)
 {
     xg_plan *p;
-    const char *env = getenv("XG_SELF_MAX");
     int i;
     *out = NULL;
     if (!dp || dp->gpu != c->rank || dp->ngpus != c->nranks) return XG_EARG;
@@ -308,7 +320,7 @@ int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_plan **out)
     p->ctx = c;
     p->r = r;
     p->dp = dp;
-    p->self_max = c->nranks > 1 ? (env ? atoll(env) : (int64_t)256 << 10) : 0;
+    p->self_max = c->nranks > 1 ? c->self_max : 0;
     *out = p;
     return XG_OK;
 }

@@ -107,16 +107,19 @@ def test_corrupted_message_is_reported(exes, tmp_path):
     assert "verify = FAILED" in p.stdout and "message is wrong" in p.stderr
 
 
-@pytest.mark.parametrize("differ", ["argv", "env"])
+@pytest.mark.parametrize("differ", ["argv", "env", "self_max"])
 def test_processes_started_differently_refuse(exes, tmp_path, differ):
-    """ranks launched by hand (RANK / WORLD_SIZE) with another -d or XG_PACK_MIN: both stop
-    before any exchange instead of posting calls nobody pairs"""
+    """ranks launched by hand (RANK / WORLD_SIZE) with another -d, XG_PACK_MIN or XG_SELF_MAX (which
+    changes the calls a rank posts): both stop before any exchange instead of posting calls nobody
+    pairs"""
     procs = []
     for r in range(2):
-        d = 3000 if differ == "env" or r == 0 else 4000
+        d = 4000 if differ == "argv" and r == 1 else 3000
         env = _env(tmp_path, RANK=r, WORLD_SIZE=2, LOCAL_RANK=r, XG_RDZV_KEY="differ")
         if differ == "env" and r == 1:
             env["XG_PACK_MIN"] = "0"
+        if differ == "self_max" and r == 1:
+            env["XG_SELF_MAX"] = "0"
         (tmp_path / "cwd").mkdir(exist_ok=True)
         procs.append(subprocess.Popen([exes["test"], "-m", "1", "-a", "3", "-d", str(d), "--procs", "7"],
                                       cwd=tmp_path / "cwd", env=env, stdout=subprocess.PIPE,
@@ -125,6 +128,22 @@ def test_processes_started_differently_refuse(exes, tmp_path, differ):
         out, err = p.communicate(timeout=60)
         assert p.returncode == 1 and "different arguments" in err, (out, err)
         assert "max total time" not in out
+
+
+@pytest.mark.parametrize("self_max", [0, 1 << 30])
+@pytest.mark.parametrize("G", [2, 4])
+def test_allocation_failure_on_one_rank_stops_every_rank(exes, tmp_path, G, self_max):
+    """GPU 1's HBM regions cannot be allocated (XG_HOST_DEV_FAIL_ALLOC, as hipMalloc fails when
+    HBM is exhausted): every rank learns it in one MAX reduction before the exchange's first call
+    (methods.c peers_agree) and every rank exits 1 naming the failure -- none waits for a peer that
+    stopped, none posts a call nobody pairs.  With XG_SELF_MAX at 0 and 1 GiB (the pairing proof
+    checks the lists posted with that value, xg_self_max)."""
+    p = _run(exes["test"], ["-m", 1, "-a", 3, "-d", 3000, "--procs", 7, "--gpus", G], tmp_path, timeout=90,
+             XG_HOST_DEV_FAIL_ALLOC=1, XG_SELF_MAX=self_max)
+    assert p.returncode == 1, (p.returncode, p.stderr[-3000:])
+    assert p.stderr.count("allocation failed") == 1, p.stderr[-3000:]
+    assert p.stderr.count("another GPU of the job failed (code 4)") == G - 1, p.stderr[-3000:]
+    assert "max total time" not in p.stdout
 
 
 def test_pt2pt_two_processes(exes, tmp_path):
