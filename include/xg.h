@@ -118,7 +118,7 @@ int xg_plan_enqueue(xg_plan *p);
 int xg_plan_check(xg_plan *p);
 /* Step engine: every maximal run of >= 2 GPU-local steps (no RCCL op, no in-loop
  * barrier, no unpack, each <= XG_ENGINE_MAX_STEP bytes; 0 = off) is ONE persistent
- * launch of up to one workgroup per CU (XG_ENGINE_WG lowers it), grid barrier +
+ * launch of up to one workgroup per CU (fewer if the device admits fewer), grid barrier +
  * wall-clock stamp per step; the other steps are their own launches.
  * Small hazard-free segments run on the solo engine instead: each step's pieces
  * dealt over up to XG_SOLO_RAILS independent rails (default 512 rails of one wave;
@@ -167,12 +167,11 @@ int xg_ktime_launch(xg_ctx *ctx, int k, double *ms, int64_t *bytes);
  * second (mode 2: bytes moved 1 -> 0), *sec = seconds per repetition. */
 int xg_p2p_bench(xg_ctx *ctx, int64_t bytes, int mode, int reps, double *gbps, double *sec);
 
-/* Tuning: bytes per copy workgroup (default 32768) and copy kernel variant: 0 (default)
- * = copy_kernel_g<4> with non-temporal loads/stores for launches moving >= XG_COPY_NT_MIN
- * bytes (default 128 MiB: source + destination past the 256 MiB Infinity Cache) and plain
- * ones below; 1 = always plain, 6 = always non-temporal (XG_EARG for any other).  variant < 0
- * keeps the current one; XG_COPY_VARIANT / XG_COPY_CHUNK at xg_init.  Applies to plans loaded
- * afterwards. */
+/* Tuning: bytes per copy workgroup (default 32768; chunk_bytes 0 keeps it) and copy kernel
+ * variant: 0 (default) = copy_kernel_g<4> with non-temporal loads/stores for launches moving
+ * >= 128 MiB (source + destination past the 256 MiB Infinity Cache) and plain ones below;
+ * 1 = always plain, 6 = always non-temporal (XG_EARG for any other).  variant < 0 keeps the
+ * current one; XG_COPY_VARIANT at xg_init.  Applies to plans loaded afterwards. */
 int xg_set_copy_params(xg_ctx *ctx, int64_t chunk_bytes, int variant);
 
 /* ------------------------------------------------------------------ method operators

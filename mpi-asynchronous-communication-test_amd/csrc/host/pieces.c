@@ -83,8 +83,9 @@ int xg_step_local_meets_unpacks(const xg_devplan *dp, int s)
         for (side = 0; side < 2 && !hit; ++side) {
             const int buf = side ? c->dst_buf : c->src_buf;
             const int64_t a = side ? c->dst_off : c->src_off, b = a + c->len;
-            int lo = 0, hi = nw[buf];                        /* intervals starting before b: [0, lo) */
+            int lo = 0, hi;
             if (buf < 0 || buf >= XG_NBUF) continue;
+            hi = nw[buf];                                    /* intervals starting before b: [0, lo) */
             while (lo < hi) {
                 const int mid = (lo + hi) / 2;
                 if (w[buf][mid].lo < b) lo = mid + 1;

@@ -784,7 +784,7 @@ __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned lon
                                                                    uint8_t *dst_base, const int *__restrict__ meta,
                                                                    int nsteps, EngineState *st,
                                                                    unsigned long long *stamps, int stride,
-                                                                   Doorbell *db, unsigned epoch, int relay)
+                                                                   Doorbell *db, unsigned epoch)
 {
     const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
     const int rail = (int)blockIdx.x, R = (int)gridDim.x;
@@ -807,8 +807,8 @@ __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned lon
         ts[i] = 0;
     }
     // armed: every rail resident, then rail 0 announces `ready`; the ring reaches the
-    // rails either each through its own poll of host memory, or (relay) through rail 0,
-    // which alone polls the host and passes the epoch on in device memory
+    // rails through rail 0, which alone polls the host and relays the epoch in device memory
+    // (hundreds of rails polling host memory take ~45 us to all see it)
     __shared__ int relay_now;
     if (threadIdx.x == 0) {
         bool ok = true, relay_go = false;
@@ -825,10 +825,9 @@ __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned lon
                 }
                 ok = ok && wait_ring(db, epoch);
                 if (!ok) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else if (relay) relay_go = true;
+                else relay_go = true;
             } else {
-                ok = relay ? poll_word<false>((g_u32 *)&st->go[rail % kGoLines][0], epoch, tmo)
-                           : poll_word<true>((g_u32 *)&db->ring, epoch, tmo);
+                ok = poll_word<false>((g_u32 *)&st->go[rail % kGoLines][0], epoch, tmo);
                 if (!ok) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }

@@ -111,32 +111,23 @@ struct xg_ctx {
     int engine_drain;          // 1: always drain before each barrier arrival (XG_ENGINE_DRAIN=1)
     int solo;                  // 0: never use the solo engine
     int64_t solo_max;          // solo segments move <= this many bytes per run
-    int64_t grid_cache_max;    // grid_pays: runs of <= this many bytes stay cache-resident (the 256 MiB MALL)
     int solo_rails;            // solo segments deal their pieces over up to this many rails
     int solo_waves;            // waves per rail: 16 (a workgroup) or 1
-    int solo_min_steps;        // a whole plan of fewer steps stays a copy launch
     int64_t launch_max;        // copy launches above this many bytes go as back-to-back launches of ~this size
-    int balance;               // 1: per launch, the piece size that least loads the busiest CU (launch_chunk)
-    int wave;                  // 1: cross-GPU steps' plain copy launches run copy_kernel_w (launch_chunk)
-    int64_t wave_min, wave_max;   // ... when they move between this many bytes and that many
+    int64_t wave_min;          // cross-GPU steps' plain copy launches of >= this many bytes (and <= kWaveMax)
+                               // run copy_kernel_w (launch_chunk)
     int wave_grid;             // copy_kernel_w workgroups resident at once (occupancy x CUs)
-    int64_t wg_cost;           // ... a workgroup's fixed start, in bytes-equivalent
     int cus;                   // compute units
-    int solo_relay;            // armed solo: rail 0 alone polls the doorbell and relays the ring
     int step_chain;            // 1: time runs of one-launch local steps by in-kernel stamps (xg_plan_run)
-    int piece_order;           // local pieces of a launch: 0 message order, 1 by destination, 2 by source
     int engine_arm;            // 1: xg_plan_run arms single-segment plans (doorbell)
-    int split_local;           // 1: a cross-GPU step's local gather runs on the side stream
-    int64_t split_min;         // ... when it moves >= this many bytes (smaller: in the pack / fused launch)
+    int64_t split_min;         // a cross-GPU step's local gather of >= this many bytes runs on the side stream
+                               // (smaller: in the pack / fused launch)
     int64_t self_max;          // a cross-GPU step's local part of <= this many bytes goes in its RCCL group
-    int fuse_unpack;           // 1: a step's packs launch with the previous step's unpacks
     int fuse_stage;            // 1: a step's stage copies launch with its local copies when hazard-free
     int split_after_pack;      // 1: a split step's local part forks after its pack launch
     int graph;                 // hipGraph replay of multi-launch runs: 1 always, 0 never, -1 latency-bound one-GPU runs
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
-    int64_t nt_min;         // variant 0: launches moving >= this many bytes use non-temporal loads/stores
-    int64_t nt_stream;      // ... and in a plan streaming past the Infinity Cache, launches >= this many
     int engine_occ;            // co-resident step-engine workgroups the device admits (plan load caps W)
     // kernel timing session (xg_ktime_begin/end): 1 = an event pair around every
     // copy launch, 2 = one pair around the whole session on the main stream
@@ -314,18 +305,25 @@ static int capture(hipStream_t stream, hipGraphExec_t *out, F body)
     return XG_OK;
 }
 
+// Settled tuning, fixed since round 4 (DESIGN.md "Knobs" lists what each was measured against).
+constexpr int64_t kNtMin = 128 << 20;      // launches of >= this many bytes stream past the MALL:
+                                           // non-temporal (profiles/r02/copy_nt_sizes.txt, copy_ab_nt/)
+constexpr int64_t kNtStream = 4 << 20;     // ... and, in a streaming plan, launches of >= this many
+constexpr int64_t kGridCacheMax = 256 << 20;   // grid_pays: a run of <= this many bytes stays in the MALL
+constexpr int64_t kWgCost = 2048;          // a copy workgroup's fixed start, bytes-equivalent (xg_piece_size)
+constexpr int64_t kWaveMax = 32 << 20;     // copy_kernel_w up to this launch size (profiles/r03/wave_local/)
+
 // The copy kernel variant of a launch moving `bytes` (launch_copy).  Variant 0 picks
 // non-temporal loads/stores (6) when the bytes cannot come back from the 256 MiB
 // Infinity Cache: a launch whose own source + destination exceed it, or a launch of
-// >= nt_stream bytes in a plan whose run copies more than it (every step then finds
+// >= kNtStream bytes in a plan whose run copies more than it (every step then finds
 // its bytes evicted by the steps before) -- unless what it writes is read again at
 // once (`reread`: packs feeding RCCL, TAM stage copies), which then may still find
 // it in the cache; plain (1) otherwise.
 static int copy_variant(const xg_plan *p, int64_t bytes, bool reread = false)
 {
     if (p->variant) return p->variant;
-    const xg_ctx *c = p->ctx;
-    return bytes >= c->nt_min || (!reread && p->streaming && c->nt_stream > 0 && bytes >= c->nt_stream) ? 6 : 1;
+    return bytes >= kNtMin || (!reread && p->streaming && bytes >= kNtStream) ? 6 : 1;
 }
 
 extern "C" double xg_now(void)
@@ -413,31 +411,21 @@ static int init_ctx(xg_ctx *c, const void *uid)
     const int device = c->device, rank = c->rank, nranks = c->nranks;
     (void)rank;
     c->chunk = 32768; c->variant = 0; c->kt_mode = 0; c->nk = 0; c->kt_bytes = 0;   // profiles/r01_copy_ab.txt
-    const char *env = getenv("XG_COPY_CHUNK");
-    if (env && atol(env) >= 4096) c->chunk = atol(env) & ~(int64_t)15;
-    env = getenv("XG_COPY_VARIANT");          // 0 by size (default), 1 plain, 6 non-temporal
+    const char *env = getenv("XG_COPY_VARIANT");          // 0 by size (default), 1 plain, 6 non-temporal
     if (env && (atoi(env) == 1 || atoi(env) == 6)) c->variant = atoi(env);
     else if (env && atoi(env) != 0) fprintf(stderr, "xg: XG_COPY_VARIANT=%s ignored (0, 1 or 6)\n", env);
-    c->nt_min = 128 << 20;
-    env = getenv("XG_COPY_NT_MIN");
-    if (env) c->nt_min = atol(env);
-    c->nt_stream = 4 << 20;           // below it nt and plain tie (profiles/r02/copy_nt_sizes.txt); 0: off
-    env = getenv("XG_COPY_NT_STREAM");
-    if (env) c->nt_stream = atol(env);
     c->engine_max_step = 16 << 20;    // crossover vs one launch per step: profiles/r01_engine_sweep.txt
     env = getenv("XG_ENGINE_MAX_STEP");      // 0: never use the step engine
     if (env) c->engine_max_step = atol(env);
     {
         // the engine's grid barrier needs every workgroup resident at once: at most one
-        // per CU by design (XG_ENGINE_WG lowers it), never more than the device admits
-        // (a partitioned device has fewer CUs; several ranks per GPU share them)
+        // per CU by design, never more than the device admits (a partitioned device has
+        // fewer CUs; several ranks per GPU share them)
         int cus = 0, per_cu = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, xgk::step_engine_kernel<16>, xgk::kThreads, 0));
         c->engine_occ = cus * (per_cu < 1 ? 1 : per_cu);
-        env = getenv("XG_ENGINE_WG");
-        c->engine_wmax = env && atoi(env) > 0 ? atoi(env) : cus;
-        if (c->engine_wmax > cus) c->engine_wmax = cus;
+        c->engine_wmax = cus;
         if (c->engine_wmax > c->engine_occ) c->engine_wmax = c->engine_occ;
         if (c->engine_wmax < 1) c->engine_wmax = 1;
     }
@@ -451,9 +439,6 @@ static int init_ctx(xg_ctx *c, const void *uid)
     c->solo_max = (int64_t)1 << 30;
     env = getenv("XG_ENGINE_SOLO_MAX");
     if (env) c->solo_max = atol(env);
-    c->grid_cache_max = (int64_t)256 << 20;   // the Infinity Cache, not solo_max (1 GiB since a9cb48e)
-    env = getenv("XG_GRID_CACHE_MAX");
-    if (env) c->grid_cache_max = atol(env);
     env = getenv("XG_SOLO_WAVES");           // waves per rail: 1 (default) or 16
     c->solo_waves = env && atoi(env) == xgk::kSoloWaves ? xgk::kSoloWaves : 1;
     // see DESIGN.md (solo engine): profiles/r02/rails/solo_probe.txt
@@ -466,41 +451,25 @@ static int init_ctx(xg_ctx *c, const void *uid)
         int cus = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         c->cus = cus > 0 ? cus : 256;
-        env = getenv("XG_COPY_BALANCE");
-        c->balance = !(env && !strcmp(env, "0"));
-        env = getenv("XG_COPY_WG_COST");
-        c->wg_cost = env ? atoll(env) : 2048;
         // the wave-persistent copy for the launches of cross-GPU steps (packs, unpacks, the
         // local part): profiles/r03/wave_copy/ -- one GPU's configs[2] pack launch 5.8 ->
-        // 6.25 TB/s; the 448 MiB non-temporal launches stay copy_kernel_g (6.0 vs 5.5-5.8)
-        env = getenv("XG_COPY_WAVE");
-        c->wave = !(env && !strcmp(env, "0"));
-        env = getenv("XG_COPY_WAVE_MIN");
-        c->wave_min = env ? atoll(env) : (int64_t)1 << 20;
-        // above ~32 MiB the one-piece-per-workgroup launch is as fast or faster
+        // 6.25 TB/s; the 448 MiB non-temporal launches stay copy_kernel_g (6.0 vs 5.5-5.8);
+        // above kWaveMax the one-piece-per-workgroup launch is as fast or faster
         // (profiles/r03/wave_local/: 28 MiB 9.3 vs 9.9 us, 56 MiB 18.7 vs 18.2, 112 MiB equal)
-        env = getenv("XG_COPY_WAVE_MAX");
-        c->wave_max = env ? atoll(env) : (int64_t)32 << 20;
+        env = getenv("XG_COPY_WAVE_MIN");     // test hook: 0 puts every cross-GPU launch on the wave copy
+        c->wave_min = env ? atoll(env) : (int64_t)1 << 20;
         int per_cu = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, xgk::copy_kernel_w<xgk::kWaveKiB>, xgk::kThreads,
                                                             0));
         c->wave_grid = c->cus * (per_cu < 1 ? 1 : per_cu);
     }
-    env = getenv("XG_SOLO_MIN_STEPS");       // plans of fewer steps never run as an armed solo launch
-    c->solo_min_steps = env ? atoi(env) : 1;  // profiles/r02/one_step/: armed beats the event-timed launch
-    env = getenv("XG_PIECE_ORDER");          // profiles/r02/piece_order/: by destination is fastest
-    c->piece_order = env ? atoi(env) : 1;
     env = getenv("XG_STEP_CHAIN");           // "0": an event after every step launch
     c->step_chain = !(env && !strcmp(env, "0"));
-    env = getenv("XG_SOLO_RELAY");           // "0": every rail polls the doorbell itself
-    c->solo_relay = !(env && !strcmp(env, "0"));
     // "1": arm single-segment plans (launched before the timed region, started by the host's
     // doorbell ring).  Off by default: the reference's total_time brackets its request posts
     // (mpi_test.c:1444, :1763), so the like-for-like time includes the kernel launch
     env = getenv("XG_ENGINE_ARM");
     c->engine_arm = env && !strcmp(env, "1");
-    env = getenv("XG_SPLIT_LOCAL");          // "0": local gather + packs in one launch
-    c->split_local = !(env && !strcmp(env, "0"));
     // a cross-GPU step's local part: <= self_max bytes travels in the step's RCCL group as self
     // send/recv (one RCCL launch carries a latency-bound step), < split_min bytes joins the
     // step's pack / fused launch, larger runs on the side stream beside the exchange (split).
@@ -510,8 +479,6 @@ static int init_ctx(xg_ctx *c, const void *uid)
     c->split_min = env ? atoll(env) : (int64_t)1 << 20;
     env = getenv("XG_SELF_MAX");             // bytes: local part posted as self send/recv (0: never)
     c->self_max = env ? atoll(env) : (int64_t)256 << 10;
-    env = getenv("XG_FUSE_UNPACK");          // "0": unpacks and the next step's packs apart
-    c->fuse_unpack = !(env && !strcmp(env, "0"));
     env = getenv("XG_FUSE_STAGE");           // "0": stage copies always in a launch of their own
     c->fuse_stage = !(env && !strcmp(env, "0"));
     env = getenv("XG_SPLIT_AFTER_PACK");     // "0": a split step's local part and its packs start together
@@ -938,7 +905,7 @@ static std::vector<std::pair<int, int>> solo_split(const xg_plan *p, const SegCa
 }
 
 // Grid engine vs the same steps as chained copy launches, for a run larger than the
-// Infinity Cache (bytes > grid_cache_max = 256 MiB, the MALL, XG_GRID_CACHE_MAX: every
+// Infinity Cache (bytes > kGridCacheMax = 256 MiB, the MALL: every
 // round of units pays HBM latency and address translation of fresh pages).  Per step, the grid's workgroups take ceil(units / W)
 // dependent load -> store rounds of ~2 us each behind a ~0.9 us barrier; a chained
 // launch costs a ~2.3 us boundary and moves the step at the copy kernel's rate.  Measured
@@ -947,7 +914,7 @@ static std::vector<std::pair<int, int>> solo_split(const xg_plan *p, const SegCa
 static bool grid_pays(const xg_plan *p, const SegCand &k)
 {
     const xg_ctx *c = p->ctx;
-    if (k.bytes <= c->grid_cache_max) return true;
+    if (k.bytes <= kGridCacheMax) return true;
     const int b = k.maxstep <= (1 << 20) ? 1 : (k.maxstep <= (4 << 20) ? 4 : 16);
     const int64_t unit = (int64_t)b * xgk::kThreads * 16;
     std::vector<int64_t> units(k.n, 0);
@@ -1037,8 +1004,8 @@ static int build_segments(xg_plan *p, const std::vector<xgk::DCopy> &pieces)
         for (int t = s; t < e; ++t) busy += p->steps[t].pre_n > 0;
         // one busy step is worth an engine launch only as the whole plan: a small one-step
         // plan on rails takes 5 us armed against 6 us (10-24 us cold) as an event-timed copy
-        // launch (profiles/r02/one_step/; XG_SOLO_MIN_STEPS=2 restores the copy launch)
-        const bool whole = s_run == 0 && run_end == p->nsteps && p->nsteps >= c->solo_min_steps && !c->virt;
+        // launch (profiles/r02/one_step/)
+        const bool whole = s_run == 0 && run_end == p->nsteps && !c->virt;
         if (busy < (whole ? 1 : 2)) {
             s = run_end > s ? run_end : s + 1;
             continue;
@@ -1215,10 +1182,10 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     // a halving keeps dividing the power-of-two segment sizes: no ragged tail piece per segment,
     // profiles/r01_min_pieces_ab.txt), whichever gives the least work to the busiest CU: a
     // launch of w pieces of c bytes puts ceil(w / CUs) pieces on some CU, each costing c bytes
-    // plus a fixed per-workgroup start (XG_COPY_WG_COST bytes-equivalent, default 2 KiB); ties
+    // plus a fixed per-workgroup start (kWgCost = 2 KiB bytes-equivalent); ties
     // keep the larger piece.  A 28 MiB pack of 256 KiB segments: 896 pieces of 32 KiB = 3.5
     // per CU (the busiest 4 x 32 KiB) -> 1792 of 16 KiB = exactly 7 (7 x 16 KiB).  The bench's
-    // 448 MiB launches stay 32 KiB (56 per CU).  XG_COPY_BALANCE=0: always c->chunk.  (A rule
+    // 448 MiB launches stay 32 KiB (56 per CU).  (A rule
     // forcing >= 2 x CUs pieces on small launches was measured 3-7 % slower and dropped:
     // profiles/r03/min_wg/summary.txt.)
     // A launch of a cross-GPU step (packs, unpacks, its local part), or of a GPU-local step too
@@ -1244,17 +1211,16 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
                 bits |= (uint64_t)cp.src_off | (uint64_t)cp.dst_off | (uint64_t)cp.len;
             }
         if (bytes <= 0) return;
-        if (cross && c->wave && bytes >= c->wave_min && bytes <= c->wave_max && (bits & 15) == 0 &&
+        if (cross && bytes >= c->wave_min && bytes <= kWaveMax && (bits & 15) == 0 &&
             copy_variant(p, bytes, reread) == 1) {
             chunk = (int64_t)xgk::kWaveKiB << 10;
             wave_at[first] = 1;
             return;
         }
-        if (!c->balance) return;
         std::vector<int64_t> lens;
         for (const auto &rg : ranges)
             for (int i = 0; i < rg.second; ++i) lens.push_back(dp->copies[rg.first + i].len);
-        chunk = xg_piece_size(lens.data(), (int)lens.size(), c->chunk, c->cus, c->wg_cost);
+        chunk = xg_piece_size(lens.data(), (int)lens.size(), c->chunk, c->cus, kWgCost);
     };
     DisplScan ds;
     int rc;
@@ -1330,9 +1296,9 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         // group (split) when it is large enough to pay for the fork / join; a smaller one joins
         // the step's first launch -- the fused one too, if it touches none of the bytes the
         // previous step's unpacks write (then the step is ONE copy launch + its RCCL group)
-        st.split = c->split_local && st.p2p_n > 0 && nloc > 0 && b_loc >= c->split_min;
+        st.split = st.p2p_n > 0 && nloc > 0 && b_loc >= c->split_min;
         st.deferred = false;
-        const bool prev_ok = c->fuse_unpack && s > 0 && npack > 0 && sp.stage_count == 0 &&
+        const bool prev_ok = s > 0 && npack > 0 && sp.stage_count == 0 &&
                              !p->steps[s - 1].sync_after && dp->steps[s - 1].post_count > 0;
         st.fused = prev_ok && (st.split || nloc == 0 || !xg_step_local_meets_unpacks(dp, s));
         st.fused_local = st.fused && !st.split && nloc > 0;
@@ -1450,36 +1416,32 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         launch_chunk({r_post}, true);
         if (!st.deferred && !add_post(s)) goto bad;
     }
-    // order of a launch's local pieces (workgroup i copies piece i): by destination address
-    // (default), by source (XG_PIECE_ORDER=2) or in message order (0).  The workgroups in
-    // flight at any moment then write a few consecutive segments instead of one piece in
-    // each of dozens of scattered slots -- 7-10 % shorter all-to-many launches (DRAM row
-    // locality of the write stream).  Local pieces carry no displacement fix-ups and a
-    // launch's pieces are independent, so any order is valid.
+    // order of a launch's local pieces (workgroup i copies piece i): by destination address.
+    // The workgroups in flight at any moment then write a few consecutive segments instead of
+    // one piece in each of dozens of scattered slots -- 7-10 % shorter all-to-many launches
+    // (DRAM row locality of the write stream; message or source order measured slower,
+    // profiles/r02/piece_order/).  Local pieces carry no displacement fix-ups and a launch's
+    // pieces are independent, so any order is valid.
     // Unpack pieces (source in staging, patched by the device scan) are ordered by their
     // destination too, with their fix-ups renumbered.
-    if (c->piece_order) {
-        auto key_less = [&](const xgk::DCopy &x, const xgk::DCopy &y) {
-            return c->piece_order == 1 ? x.dst < y.dst : x.src < y.src;
-        };
+    {
+        auto key_less = [](const xgk::DCopy &x, const xgk::DCopy &y) { return x.dst < y.dst; };
         for (const StepR &st : p->steps)
             std::stable_sort(pieces.begin() + st.local_b, pieces.begin() + st.local_b + st.local_n, key_less);
-        if (c->piece_order == 1) {
-            std::vector<int> where(pieces.size(), -1);      // old index -> its fix-up
-            for (size_t f = 0; f < ds.fix.size(); ++f) where[ds.fix[f].piece] = (int)f;
-            for (const StepR &st : p->steps) {
-                if (st.post_n < 2) continue;
-                std::vector<int> idx(st.post_n);
-                for (int i = 0; i < st.post_n; ++i) idx[i] = st.post_b + i;
-                std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return pieces[x].dst < pieces[y].dst; });
-                std::vector<xgk::DCopy> sorted(st.post_n);
-                for (int i = 0; i < st.post_n; ++i) sorted[i] = pieces[idx[i]];
-                for (int i = 0; i < st.post_n; ++i) {
-                    const int f = where[idx[i]];
-                    if (f >= 0) ds.fix[f].piece = st.post_b + i;
-                }
-                std::copy(sorted.begin(), sorted.end(), pieces.begin() + st.post_b);
+        std::vector<int> where(pieces.size(), -1);      // old index -> its fix-up
+        for (size_t f = 0; f < ds.fix.size(); ++f) where[ds.fix[f].piece] = (int)f;
+        for (const StepR &st : p->steps) {
+            if (st.post_n < 2) continue;
+            std::vector<int> idx(st.post_n);
+            for (int i = 0; i < st.post_n; ++i) idx[i] = st.post_b + i;
+            std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return pieces[x].dst < pieces[y].dst; });
+            std::vector<xgk::DCopy> sorted(st.post_n);
+            for (int i = 0; i < st.post_n; ++i) sorted[i] = pieces[idx[i]];
+            for (int i = 0; i < st.post_n; ++i) {
+                const int f = where[idx[i]];
+                if (f >= 0) ds.fix[f].piece = st.post_b + i;
             }
+            std::copy(sorted.begin(), sorted.end(), pieces.begin() + st.post_b);
         }
     }
     p->npieces = (int)pieces.size();
@@ -1826,19 +1788,19 @@ static int launch_seg(xg_plan *p, const EngSeg &g, hipStream_t stream, bool arme
     if (g.solo && g.wv == 1 && g.gran == 16)
         hipLaunchKernelGGL((xgk::solo_engine_kernel<xgk::kSoloK, 1>), dim3(g.w), dim3(64), 0, stream,
                            p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
-                           db, epoch, c->solo_relay);
+                           db, epoch);
     else if (g.solo && g.wv == 1 && g.gran == 4)
         hipLaunchKernelGGL((xgk::solo_engine_kernel<xgk::kSoloK, 1, 4>), dim3(g.w), dim3(64), 0, stream,
                            p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
-                           db, epoch, c->solo_relay);
+                           db, epoch);
     else if (g.solo && g.wv == 1)      // granule 1: 16 registers per piece and lane, half the rows per chunk
         hipLaunchKernelGGL((xgk::solo_engine_kernel<xgk::kSoloK / 2, 1, 1>), dim3(g.w), dim3(64), 0, stream,
                            p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
-                           db, epoch, c->solo_relay);
+                           db, epoch);
     else if (g.solo)
         hipLaunchKernelGGL((xgk::solo_engine_kernel<xgk::kSoloK, xgk::kSoloWaves>), dim3(g.w), dim3(xgk::kSoloThreads), 0,
                            stream, p->d_solo + g.u0, g.npieces, g.sbase, g.dbase, sb, n, p->d_engine, stamps, p->nsteps,
-                           db, epoch, c->solo_relay);
+                           db, epoch);
     else if (g.b == 1)
         hipLaunchKernelGGL(xgk::step_engine_kernel<1>, dim3(g.w), dim3(xgk::kThreads), 0, stream, p->d_epieces, sb, n,
                            p->d_engine, stamps, base, db, epoch);
@@ -2039,9 +2001,16 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     const double t0 = xg_now();
     if (graph) {
         HIPCHK(hipGraphLaunch(p->g_run, c->stream));
-        if (step_post) {
-            step_post[0] = xg_now() - t0;          // the whole run is posted by one graph launch
-            for (int s = 1; s < p->nsteps; ++s) step_post[s] = 0;
+        // a replay restarts the device ticket counter from zero (the memset captured in the
+        // graph) and leaves it at the captured run's count, which the host base does not track:
+        // the next eager launch must zero the state again
+        p->engine_reset = true;
+        if (step_post && p->nsteps > 0) {
+            // the whole run is posted by one graph launch: its host time is shared evenly over the
+            // steps, so each step (and each rank posting in it, xg_sched_rank_timer) keeps a share
+            // as under per-step enqueueing, and the shares sum to the launch time
+            const double tp = (xg_now() - t0) / p->nsteps;
+            for (int s = 0; s < p->nsteps; ++s) step_post[s] = tp;
         }
     } else if ((rc = enqueue_run(p, step_post))) {
         return rc;
@@ -2121,6 +2090,7 @@ extern "C" int xg_plan_enqueue(xg_plan *p)
         }
     }
     HIPCHK(hipGraphLaunch(p->g_enq, p->ctx->stream));
+    p->engine_reset = true;          // the replay moved the device counter, not the host base
     return XG_OK;
 }
 
@@ -2252,6 +2222,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
             vg.rccl = rccl;
         }
         HIPCHK(hipGraphLaunch(vg.exec, st));
+        for (int g = 0; g < n; ++g) plans[g]->engine_reset = true;   // device counters moved by the replay
     } else if ((rc = pair_calls()) || (rc = body())) {
         return rc;
     }

@@ -133,6 +133,41 @@ def test_engine_orders_hazards(xg, ctx, unit_kib, n_units):
         sy.close()
 
 
+def test_graph_replays_alternate_with_eager_runs(xg):
+    """XG_GRAPH=1 on a plan of a grid-engine segment (flag-2 hazard steps, which the solo engine
+    never takes) and one step too large for the engine: runs replayed from the captured graph
+    alternate with runs under a kernel-timing session (launched eagerly).  A replay restarts the
+    device ticket counter inside the graph, so every replay leaves the host's ticket base stale;
+    the next eager launch must zero the engine state again -- otherwise its grid
+    barrier waits for tickets that never come and the run fails.  Every run's bytes checked."""
+    unit, n_units, big = 4 << 10, 64, 32 << 20
+    L = unit * n_units
+    steps = _hazard_steps(unit, n_units, 1) + [[(0, 0, 1, 5 * L, big)]]
+    cx = _ctx_env(xg, XG_GRAPH=1, XG_ENGINE_SOLO=0)
+    try:
+        sy = Synth(xg, cx, big, 5 * L + big, steps)
+        try:
+            d = xg.device()
+            assert d.xg_plan_engine(sy.p) > 0 and d.xg_plan_engine_rails(sy.p) == 0
+            assert d.xg_plan_launches(sy.p) == 2
+            want = None
+            for i in range(8):
+                want = sy.expected(want)
+                timed = i % 2 == 1               # odd runs: eager, inside a kernel-timing session
+                if timed:
+                    cx.ktime_begin(per_launch=True)
+                got = sy.run()
+                if timed:
+                    _ms, n, _b = cx.ktime_end()
+                    assert n == 2
+                assert (got == want).all(), "run %d (%s): %d bytes differ" % (
+                    i, "eager" if timed else "graph", int((got != want).sum()))
+        finally:
+            sy.close()
+    finally:
+        cx.close()
+
+
 def _random_steps(rng, send_bytes, recv_bytes, nsteps, align):
     steps = []
     for _ in range(nsteps):

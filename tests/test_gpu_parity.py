@@ -210,7 +210,7 @@ ENGINE_MODES = {
     "solo_armed": {"XG_ENGINE_ARM": "1"},                       # 512 one-wave rails, doorbell-armed
     "solo64_armed": {"XG_SOLO_RAILS": "64", "XG_ENGINE_ARM": "1"},
     "solo37_launch": {"XG_SOLO_RAILS": "37", "XG_ENGINE_ARM": "0"},
-    "solo_norelay": {"XG_SOLO_RELAY": "0", "XG_SOLO_RAILS": "16", "XG_ENGINE_ARM": "1"},   # every rail polls
+    "solo16_armed": {"XG_SOLO_RAILS": "16", "XG_ENGINE_ARM": "1"},
     "wg_armed": {"XG_SOLO_WAVES": "16", "XG_ENGINE_ARM": "1"},  # 16 workgroup rails of 16 waves
     "wg1_launch": {"XG_SOLO_WAVES": "16", "XG_SOLO_RAILS": "1", "XG_ENGINE_ARM": "0"},
     "grid_armed": {"XG_ENGINE_SOLO": "0", "XG_ENGINE_ARM": "1"},
@@ -249,7 +249,7 @@ def test_step_engine_modes(xg, method, k):
             run = xg.MethodRun(cx, s, it=it, mode=1)
             try:
                 assert run.engine_workgroups > 0
-                rails = {"solo_armed": 512, "solo64_armed": 64, "solo37_launch": 37, "solo_norelay": 16, "wg_armed": 16,
+                rails = {"solo_armed": 512, "solo64_armed": 64, "solo37_launch": 37, "solo16_armed": 16, "wg_armed": 16,
                          "wg1_launch": 1, "solo_launch": 512}.get(name, 0)
                 assert run.engine_rails == rails, (name, run.engine_rails)
                 for _rep in range(3):
