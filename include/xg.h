@@ -73,6 +73,9 @@ int xg_device_sync(xg_ctx *ctx);                               /* whole device (
 /* device name, CU count, HBM bytes (any pointer may be NULL) */
 int xg_device_info(xg_ctx *ctx, char *name, size_t namelen, int *cus, size_t *hbm_bytes);
 double xg_now(void);                                           /* host seconds (monotonic) */
+/* Diagnostics: where this process's host thread last was in the library -- entry point, step,
+ * posting or waiting for the device -- for a watchdog to print when a run does not return. */
+const char *xg_debug_where(void);
 
 /* ------------------------------------------------------------------ HBM regions */
 /* region_bytes: XG_BUF_SEND, XG_BUF_RECV, XG_BUF_STAGE_SEND, XG_BUF_STAGE_RECV,

@@ -71,6 +71,25 @@ struct EventPair {
     }
 };
 
+// Where the host thread is (diagnostics for a run that does not return: xg_debug_where): the
+// entry point, the step it is posting and whether it is waiting for the device.  Plain stores,
+// read only by a watchdog after the fact.
+static struct {
+    const char *fn = "idle";
+    int step = -1, nsteps = 0;
+    const char *phase = "";
+} g_where;
+static inline void where(const char *fn, int step, int nsteps, const char *phase)
+{
+    g_where.fn = fn; g_where.step = step; g_where.nsteps = nsteps; g_where.phase = phase;
+}
+extern "C" const char *xg_debug_where(void)
+{
+    static char buf[160];
+    snprintf(buf, sizeof buf, "%s: step %d of %d: %s", g_where.fn, g_where.step, g_where.nsteps, g_where.phase);
+    return buf;
+}
+
 // One RCCL group whose calls come from `post`, a callable returning ncclResult_t for
 // call i (i = 0..n-1): the group is closed (ncclGroupEnd) on every path, so an error
 // never leaves this rank inside an open group.  Returns XG_OK or XG_ERCCL.
@@ -1999,6 +2018,7 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     }
     const bool graph = p->g_run && use_graph(p);
     const double t0 = xg_now();
+    where("xg_plan_run", 0, p->nsteps, "posting the steps");
     if (graph) {
         HIPCHK(hipGraphLaunch(p->g_run, c->stream));
         // a replay restarts the device ticket counter from zero (the memset captured in the
@@ -2015,7 +2035,9 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
     } else if ((rc = enqueue_run(p, step_post))) {
         return rc;
     }
+    where("xg_plan_run", p->nsteps, p->nsteps, "waiting for the device (hipStreamSynchronize)");
     HIPCHK(hipStreamSynchronize(c->stream));
+    where("idle", -1, 0, "");
     if (wall) *wall = xg_now() - t0;
     if ((rc = xg_plan_check(p))) return rc;
     if (!step_done) return XG_OK;
@@ -2156,6 +2178,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
         if ((rc = mark(plans[0], -1, st))) return rc;
         size_t q0 = 0;
         for (int s = 0; s < nst; ++s) {
+            where(rccl ? "xg_vplans_run_rccl" : "xg_vplans_run", s, nst, "posting the pre copies");
             for (int g = 0; g < n; ++g) {
                 xg_plan *pg = plans[g];
                 const int gi = pg->seg_of[s];
@@ -2177,6 +2200,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
                     if (pairs[q].len) HIPCHK(hipMemcpyAsync(dst, src, (size_t)pairs[q].len, hipMemcpyDeviceToDevice, st));
                 }
             } else if (q1 > q0) {
+                where("xg_vplans_run_rccl", s, nst, "posting the RCCL group (ncclGroupEnd)");
                 // every pair of the step as a self send + receive in ONE group (issue order = pair order)
                 if ((rc = rccl_group(
                          (int)(2 * (q1 - q0)),
@@ -2226,7 +2250,9 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
     } else if ((rc = pair_calls()) || (rc = body())) {
         return rc;
     }
+    where(rccl ? "xg_vplans_run_rccl" : "xg_vplans_run", nst, nst, "waiting for the device (hipStreamSynchronize)");
     HIPCHK(hipStreamSynchronize(st));
+    where("idle", -1, 0, "");
     for (int g = 0; g < n; ++g)
         if ((rc = xg_plan_check(plans[g]))) return rc;
     if (step_done) {

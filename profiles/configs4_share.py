@@ -6,7 +6,7 @@ m12 at every -c in 1..8 (script_theta_all_to_many_256.sh:33-106 sweeps -c).  Per
 regions it holds, its steps and launches, the bytes it keeps on the GPU and the bytes it would
 send over xGMI, the device time of its local share (min of REPS), and the delivery check: every
 slot whose source lives on GPU 0 bit-exact (and two sampled against the oracle's closed form),
-every other slot still unwritten.  usage: python3 profiles/configs4_share.py"""
+every other slot still unwritten.  usage: python3 profiles/configs4_share.py   (CELLS=11:1,12:8 runs only those (method, -c) cells)"""
 import os
 import sys
 
@@ -31,9 +31,12 @@ print("GPU 0 of %d, P%d A%d -d %d: regions %s = %.1f GiB of %.1f GiB HBM" % (
     GPUS, P, A, d, need, sum(need) / 2 ** 30, hbm / 2 ** 30), flush=True)
 R = xg.Regions(ctx, need)
 lo, hi = 0, 0
+CELLS = [tuple(map(int, x.split(":"))) for x in os.environ.get("CELLS", "").split(",") if x.strip()]
 try:
     for m in (7, 11, 12):
         for c in range(1, 9):
+            if CELLS and (m, c) not in CELLS:
+                continue
             s = xg.Schedule(m, P, A, d, c, rl, ntimes=1, iteration=1)
             lo, hi = s.block_range(GPUS, 0)
             run = xg.MethodRun(ctx, s, it=1, mode=1, regions=R)

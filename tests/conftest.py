@@ -2,6 +2,7 @@ import gzip
 import json
 import os
 import sys
+import threading
 
 import pytest
 
@@ -13,6 +14,42 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))      # the checker (xg_oracle)
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
+
+
+@pytest.fixture(autouse=True)
+def _gpu_test_watchdog(request):
+    """A -m gpu test still running after XG_TEST_WATCHDOG seconds (default 150; the slowest test
+    takes ~20 s) names itself and where the device library's host thread is (xg_debug_where: the
+    entry point, the step, posting or waiting for the device), dumps every Python thread's stack
+    and ends the run (exit 3) -- a hang then leaves a diagnosis instead of a silent timeout."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    secs = float(os.environ.get("XG_TEST_WATCHDOG", "150"))
+
+    def fire():
+        import faulthandler
+        where = "?"
+        try:
+            mod = sys.modules.get("xgamd")
+            dev = getattr(getattr(mod, "xg", None), "_dev", None)
+            if dev is not None:
+                dev.xg_debug_where.restype = __import__("ctypes").c_char_p
+                where = dev.xg_debug_where().decode()
+        except Exception as e:            # a diagnostic must not mask the hang
+            where = "unavailable (%s)" % e
+        sys.stderr.write("\nwatchdog: %s still running after %.0f s; libxg host thread: %s\n"
+                         % (request.node.nodeid, secs, where))
+        sys.stderr.flush()
+        faulthandler.dump_traceback(all_threads=True)
+        sys.stderr.flush()
+        os._exit(3)
+
+    t = threading.Timer(secs, fire)
+    t.daemon = True
+    t.start()
+    yield
+    t.cancel()
 
 
 @pytest.fixture(scope="session")
