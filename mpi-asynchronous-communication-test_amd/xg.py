@@ -470,11 +470,42 @@ class DevicePlanView:
 
 
 # --------------------------------------------------------------------------- device (libxg.so)
+ROCM_RUNTIME_LIBS = ("libamdhip64.so", "librccl.so", "libhsa-runtime64.so")
+
+
+def foreign_rocm_runtime():
+    """ROCm runtime libraries mapped into this process from outside the ROCm install libxg.so is
+    built against (/opt/rocm, or $ROCM_PATH).  torch's wheel bundles its own libamdhip64.so.7,
+    librccl.so.1 and libhsa-runtime64.so.1 under the same sonames: once `import torch` has
+    loaded them, libxg.so binds to those instead -- another runtime and RCCL than it was built
+    and tested with (the full GPU suite hung in RCCL that way, profiles/r04/torch_runtime/)."""
+    roots = {os.path.realpath(r) for r in ("/opt/rocm", os.environ.get("ROCM_PATH") or "/opt/rocm")}
+    try:
+        roots |= {os.path.realpath(os.path.join("/opt", n)) for n in os.listdir("/opt") if n.startswith("rocm")}
+        maps = open("/proc/self/maps").read().splitlines()
+    except OSError:
+        return []
+    bad = set()
+    for line in maps:
+        path = line.split(None, 5)[5].strip() if len(line.split(None, 5)) == 6 else ""
+        if os.path.basename(path).startswith(ROCM_RUNTIME_LIBS):
+            rp = os.path.realpath(path)
+            if not any(rp.startswith(r + os.sep) for r in roots):
+                bad.add(rp)
+    return sorted(bad)
+
+
 def device():
-    """libxg.so -- the HIP/RCCL half.  Loading it does not touch the GPU."""
+    """libxg.so -- the HIP/RCCL half.  Loading it does not touch the GPU.  Refused (XGError) in a
+    process that already holds another ROCm runtime (foreign_rocm_runtime: e.g. torch's)."""
     global _dev
     if _dev is None:
         host()
+        bad = foreign_rocm_runtime()
+        if bad:
+            raise XGError("libxg.so would bind to the ROCm runtime already loaded in this process from %s "
+                          "(e.g. by `import torch`), not the one it is built against: load the framework "
+                          "before torch, or in a process without it" % ", ".join(bad))
         d = _load("libxg.so")
         vp, ip, i64 = C.c_void_p, C.c_int, C.c_int64
         d.xg_get_unique_id.argtypes = [vp]

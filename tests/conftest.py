@@ -38,8 +38,19 @@ def _gpu_test_watchdog(request):
                 where = dev.xg_debug_where().decode()
         except Exception as e:            # a diagnostic must not mask the hang
             where = "unavailable (%s)" % e
-        sys.stderr.write("\nwatchdog: %s still running after %.0f s; libxg host thread: %s\n"
-                         % (request.node.nodeid, secs, where))
+        msg = "\nwatchdog: %s still running after %.0f s; libxg host thread: %s\n" % (request.node.nodeid, secs, where)
+        # pytest captures fd 2 during the test: write the diagnosis to a file as well
+        # (XG_WATCHDOG_LOG, default gpurun_out/watchdog.txt under the repository)
+        path = os.environ.get("XG_WATCHDOG_LOG") or os.path.join(REPO, "gpurun_out", "watchdog.txt")
+        try:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            with open(path, "a") as f:
+                f.write(msg)
+                f.flush()
+                faulthandler.dump_traceback(file=f, all_threads=True)
+        except OSError:
+            pass
+        sys.stderr.write(msg)
         sys.stderr.flush()
         faulthandler.dump_traceback(all_threads=True)
         sys.stderr.flush()

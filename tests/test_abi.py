@@ -38,3 +38,18 @@ def test_product_does_not_reference_oracle():
             if f.endswith((".py", ".c", ".h", ".hip", "Makefile")):
                 txt = open(os.path.join(root, f), errors="ignore").read()
                 assert "xg_oracle" not in txt and "oracle/" not in txt, f
+
+
+def test_device_library_refuses_a_foreign_rocm_runtime():
+    """A process that imported torch first holds torch's bundled libamdhip64.so.7 / librccl.so.1
+    (the same sonames as /opt/rocm's): xg.device() refuses to load libxg.so there rather than
+    bind it to another runtime (the full GPU suite hung in RCCL that way, profiles/r04/torch_runtime/).
+    In a fresh process nothing foreign is mapped and it loads."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); %s import __graft_entry__ as G; xg = G.load_package().xg\n"
+            "try:\n    xg.device(); print('loaded', xg.foreign_rocm_runtime())\n"
+            "except xg.XGError as e:\n    print('refused', e)\n")
+    for pre, want in (("", "loaded []"), ("import torch;", "refused")):
+        out = subprocess.run([sys.executable, "-c", code % (REPO, pre)], capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0 and out.stdout.startswith(want), (pre, out.stdout, out.stderr[-1000:])

@@ -3,15 +3,18 @@ GPU's device plan on numpy regions and posts exactly the calls the runtime posts
 (xg_devplan_step_calls: cross-GPU sends/receives with torch.distributed (gloo) in the
 per-peer issue order RCCL matches on, self send/recv pairs as local copies, the in-loop
 barrier as dist.barrier), with and without the local part in the group (self_max).
-Same bytes as the oracle."""
+Same bytes as the oracle.
+
+torch is imported only in the two worker processes, never in the pytest process: collecting or
+running this module in the same process as the -m gpu tests must not load torch's bundled ROCm
+runtime (its
+libamdhip64.so.7 / librccl.so.1 carry the same sonames as /opt/rocm's, so libxg.so would bind
+to them -- the full GPU suite hung in RCCL that way, profiles/r04/torch_runtime/)."""
 import os
 import socket
 
 import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -26,6 +29,8 @@ def _free_port():
 
 def _worker(rank, world, port, results):
     import sys
+    import torch
+    import torch.distributed as dist
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -96,7 +101,16 @@ def _worker(rank, world, port, results):
 
 
 def test_two_process_exchange():
-    mgr = mp.Manager()
+    # two spawned processes (stdlib multiprocessing: this pytest process never imports torch)
+    import multiprocessing
+    ctx = multiprocessing.get_context("spawn")
+    mgr = ctx.Manager()
     results = mgr.dict()
-    mp.spawn(_worker, args=(2, _free_port(), results), nprocs=2, join=True)
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, results)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert results[0] and results[1]
