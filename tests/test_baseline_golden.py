@@ -113,3 +113,27 @@ def test_steps_match_oracle_at_p256(xg, cfg):
         ref = sorted((a, b, c, d, n, st) for (a, b, c, d, n, _sp, _rp), st in zip(om, ost))
         assert mine == ref, (cfg, m)
         assert s.nsteps >= ons
+
+
+def _counts_as_d(trace, d):
+    """a trace with every message count equal to the segment size written as 'D'"""
+    import re
+    return re.sub(r":%d(?=[@# ]|$)" % d, ":D", trace)
+
+
+@pytest.mark.parametrize("cfg,d_full", [("cfg3_p256_a32_d64k", 4 << 20)] +
+                         [("cfg4_p256_a64_d4k_c%d" % c, 64 << 20) for c in range(1, 9)])
+def test_stated_size_schedules_are_the_captured_ones(xg, cfg, d_full):
+    """configs[3] (-d 4 MiB) and configs[4] (-d 64 MiB) were captured at a reduced -d (host RAM).
+    The MPI program of every rank at the stated size is the captured one with every segment
+    count scaled: the product's schedule at the stated -d, counts written as 'D', equals its
+    schedule at the captured -d (whose every rank equals the reference's by digest, above)."""
+    meta, _, _ = load_baseline(cfg)
+    rl, d = meta["aggregators"], meta["d"]
+    for m in meta["method_list"]:
+        small = xg.Schedule(m, meta["P"], meta["A"], d, meta["c"], rl, ntimes=meta["ntimes"])
+        full = xg.Schedule(m, meta["P"], meta["A"], d_full, meta["c"], rl, ntimes=meta["ntimes"])
+        for r in range(meta["P"]):
+            ts = small.trace(r)
+            assert _sha1(ts) == meta["trace_sha1"][str(m)][r], (cfg, m, r)
+            assert _counts_as_d(full.trace(r), d_full) == _counts_as_d(ts, d), (cfg, m, r)
