@@ -144,8 +144,6 @@ struct xg_ctx {
     int64_t self_max;          // a cross-GPU step's local part of <= this many bytes goes in its RCCL group
     int fuse_stage;            // 1: a step's stage copies launch with its local copies when hazard-free
     int split_after_pack;      // 1: a split step's local part forks after its pack launch
-    int xcd_order;             // A/B (XG_XCD_ORDER=1): a launch's local pieces dealt so that workgroup b
-                               // (XCD b % 8) copies the (b / 8)-th piece of the launch's (b % 8)-th eighth
     int graph;                 // hipGraph replay of multi-launch runs: 1 always, 0 never, -1 latency-bound one-GPU runs
     double wall_hz;            // wall_clock64() rate
     int variant;            // copy kernel variant (launch_copy)
@@ -502,8 +500,6 @@ static int init_ctx(xg_ctx *c, const void *uid)
     c->self_max = env ? atoll(env) : (int64_t)256 << 10;
     env = getenv("XG_FUSE_STAGE");           // "0": stage copies always in a launch of their own
     c->fuse_stage = !(env && !strcmp(env, "0"));
-    env = getenv("XG_XCD_ORDER");
-    c->xcd_order = env && !strcmp(env, "1");
     env = getenv("XG_SPLIT_AFTER_PACK");     // "0": a split step's local part and its packs start together
     c->split_after_pack = !(env && !strcmp(env, "0"));
     // hipGraph replay: "1" every multi-launch run (and virtual job), "0" never; default (-1):
@@ -1443,7 +1439,8 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     // The workgroups in flight at any moment then write a few consecutive segments instead of
     // one piece in each of dozens of scattered slots -- 7-10 % shorter all-to-many launches
     // (DRAM row locality of the write stream; message or source order measured slower,
-    // profiles/r02/piece_order/).  Local pieces carry no displacement fix-ups and a launch's
+    // profiles/r02/piece_order/; so did dealing each XCD its own eighth, 3-8 %,
+    // profiles/r04/xcd_order/).  Local pieces carry no displacement fix-ups and a launch's
     // pieces are independent, so any order is valid.
     // Unpack pieces (source in staging, patched by the device scan) are ordered by their
     // destination too, with their fix-ups renumbered.
@@ -1451,19 +1448,6 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         auto key_less = [](const xgk::DCopy &x, const xgk::DCopy &y) { return x.dst < y.dst; };
         for (const StepR &st : p->steps)
             std::stable_sort(pieces.begin() + st.local_b, pieces.begin() + st.local_b + st.local_n, key_less);
-        if (c->xcd_order)
-            for (const StepR &st : p->steps) {
-                // workgroups are dispatched round-robin over the 8 XCDs: give XCD x the x-th eighth
-                // of the destination-ordered pieces, walked in order (its own contiguous stream)
-                const int n = st.local_n, X = 8, per = (n + X - 1) / X;
-                if (n < 2 * X) continue;
-                std::vector<xgk::DCopy> dealt;
-                dealt.reserve(n);
-                for (int k = 0; k < per; ++k)
-                    for (int x = 0; x < X; ++x)
-                        if (x * per + k < n) dealt.push_back(pieces[st.local_b + x * per + k]);
-                std::copy(dealt.begin(), dealt.end(), pieces.begin() + st.local_b);
-            }
         std::vector<int> where(pieces.size(), -1);      // old index -> its fix-up
         for (size_t f = 0; f < ds.fix.size(); ++f) where[ds.fix[f].piece] = (int)f;
         for (const StepR &st : p->steps) {
