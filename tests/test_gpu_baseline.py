@@ -99,6 +99,25 @@ def test_baseline_virtual8_rccl(xg, world8, cfg):
             _check_golden(cfg, meta, data, method, it, res, "G8 rccl pack%d/%d" % (pack, form))
 
 
+@pytest.mark.parametrize("G", [2, 4])
+@pytest.mark.parametrize("cfg", ["cfg1_p32_a14_d1m", "cfg2_p64_a16_d256k"])
+def test_baseline_scaling_jobs_rccl(xg, cfg, G):
+    """the bench's N = 2 and 4 workloads (configs[1], and configs[2]'s shape) as G-GPU jobs over
+    RCCL, direct / one-sided / two-sided, every slot against the reference's checksums"""
+    meta, _, data = load_baseline(cfg)
+    it = meta["iters"] - 1
+    ctxs = [xg.Context.virtual(g, G, device=0) for g in range(G)]
+    try:
+        for method in meta["method_list"]:
+            s = _sched(xg, meta, method, it)
+            for pack, form in PACKINGS:
+                res = _run_job(xg, ctxs, s, it, 0, pack, form, rccl=True)
+                _check_golden(cfg, meta, data, method, it, res, "G%d rccl pack%d/%d" % (G, pack, form))
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 def _shared_regions(xg, ctxs, scheds, packings):
     """one Regions per virtual GPU, sized for every (schedule, packing) it will run"""
     G = len(ctxs)
