@@ -1694,14 +1694,6 @@ static int nrecv_slots(const xg_sched *s, int r)
     return s->dir == XG_A2M ? (s->isagg[r] ? s->P : 0) : s->A;
 }
 
-/* A/B (XG_REGION_SKEW, bytes, multiple of 16): a gap after every rank's buffer, so rank buffers
- * of a power-of-two size do not start at power-of-two strides */
-static int64_t region_skew(void)
-{
-    const char *e = getenv("XG_REGION_SKEW");
-    return e ? (atoll(e) & ~(int64_t)15) : 0;
-}
-
 static int64_t rank_offset(const xg_sched *s, int ngpus, int rank, int recv)
 {
     int lo, hi, g = xg_gpu_of(s->P, ngpus, rank);
@@ -1709,11 +1701,9 @@ static int64_t rank_offset(const xg_sched *s, int ngpus, int rank, int recv)
     xg_block_range(s->P, ngpus, g, &lo, &hi);
     if (!per_rank) return -1;
     /* ranks with a buffer of this kind on the GPU are laid out rank-major */
-    if ((s->dir == XG_A2M) == (recv != 0)) {
-        const int64_t i = s->agg_prefix[rank] - s->agg_prefix[lo];
-        return i * ((int64_t)s->P * s->d + region_skew());                           /* aggregator buffers */
-    }
-    return (int64_t)(rank - lo) * ((int64_t)s->A * s->d + region_skew());           /* every-rank buffers */
+    if ((s->dir == XG_A2M) == (recv != 0))
+        return (int64_t)(s->agg_prefix[rank] - s->agg_prefix[lo]) * s->P * s->d;   /* aggregator buffers */
+    return (int64_t)(rank - lo) * s->A * s->d;                                      /* every-rank buffers */
 }
 
 int64_t xg_send_offset(const xg_sched *s, int ngpus, int rank) { return rank_offset(s, ngpus, rank, 0); }
@@ -1735,11 +1725,9 @@ int64_t xg_region_bytes(const xg_sched *s, int ngpus, int g, int buf)
     xg_block_range(s->P, ngpus, g, &lo, &hi);
     naggs = s->agg_prefix[hi] - s->agg_prefix[lo];
     if (buf == XG_BUF_SEND)
-        return s->dir == XG_A2M ? (int64_t)(hi - lo) * ((int64_t)s->A * s->d + region_skew())
-                                : (int64_t)naggs * ((int64_t)s->P * s->d + region_skew());
+        return s->dir == XG_A2M ? (int64_t)(hi - lo) * s->A * s->d : (int64_t)naggs * s->P * s->d;
     if (buf == XG_BUF_RECV)
-        return s->dir == XG_A2M ? (int64_t)naggs * ((int64_t)s->P * s->d + region_skew())
-                                : (int64_t)(hi - lo) * ((int64_t)s->A * s->d + region_skew());
+        return s->dir == XG_A2M ? (int64_t)naggs * s->P * s->d : (int64_t)(hi - lo) * s->A * s->d;
     if (buf == XG_BUF_SCRATCH) {
         int64_t t = 0;
         int r;
