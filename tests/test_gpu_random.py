@@ -134,3 +134,42 @@ def test_random_config_virtual_gpus(xg, worlds, cfg):
         finally:
             for r in runs:
                 r.close()
+
+
+NL = int(os.environ.get("XG_RANDOM_NL", 24))
+
+
+def _large_configs(seed, n):
+    """P from 48 to 256 (the BASELINE jobs' 32-64 ranks per GPU on 8 GPUs), -d kept so that
+    P * A * d <= 32 MiB (the oracle builds every expected slot on the CPU)"""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        P = rng.choice([48, 64, 96, 128, 160, 200, 256])
+        A = rng.choice([1, max(1, P // 8), max(1, P // 4), min(P, 64)])
+        d = rng.choice([d for d in (16, 100, 1000, 4096) if P * A * d <= 32 << 20])
+        out.append((rng.randint(1, 20), P, A, d, rng.choice([1, 2, 3, 8, 200000000]), rng.randint(1, 2),
+                    rng.randint(0, 3), rng.choice([1, 2, 4, 8]), rng.randint(0, 2), rng.randint(0, 2)))
+    return out
+
+
+@pytest.mark.parametrize("cfg", _large_configs(11, NL), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
+def test_random_large_p_virtual_gpus(xg, worlds, cfg):
+    """P = 48..256 as 4- and 8-GPU virtual jobs (the BASELINE jobs' rank counts), every method,
+    direct and packed, copies or RCCL, every slot against the oracle's closed form"""
+    rng = random.Random(hash(cfg) & 0xffff)
+    G = rng.choice([4, 8])
+    s, rl = _schedule(xg, cfg)
+    for pack, form in ((0, -1), (1 << 30, rng.choice([0, 1]))):
+        runs = [xg.MethodRun(c, s, it=cfg[-1], mode=1, pack_max_seg=pack, pack_form=form) for c in worlds[G]]
+        try:
+            done = xg.run_virtual(runs, rccl=rng.random() < 0.5)
+            assert all(y >= x for x, y in zip(done, done[1:]))
+            res = []
+            for r in runs:
+                chk, bad, first = r.verify()
+                res += list(zip(r.slots, chk, bad, first))
+            _check(xg, s, rl, cfg, res, G)
+        finally:
+            for r in runs:
+                r.close()
