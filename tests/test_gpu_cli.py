@@ -51,3 +51,25 @@ def test_cli_refuses_reference_deadlock(pkg, tmp_path):
     out = subprocess.run([exe, "--procs", "32", "-a", "14", "-d", "65536", "-c", "3", "-m", "6"],
                          capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
     assert out.returncode == 0 and "deadlocks" in out.stderr
+
+
+@pytest.mark.parametrize("cfg", ["cfg1_p32_a14_d1m", "cfg2_p64_a16_d256k", "cfg3_p256_a32_d64k", "cfg4_p256_a64_d4k_c3"])
+def test_cli_report_matches_reference_at_baseline_shapes(pkg, cfg, tmp_path):
+    """bin/test at the BASELINE.json shapes (one GPU hosts every rank): the report of every
+    captured method equals the reference's with numbers masked, with --verify confirming every
+    byte; a method the reference hung on (configs[1] m6) is refused and named on stderr."""
+    from conftest import BASELINE, load_baseline
+    meta, _, _ = load_baseline(cfg)
+    exe = os.path.join(os.path.dirname(pkg.__file__), "bin", "test")
+    for m in sorted(int(x) for x in meta["methods"]):
+        args = [exe, "--procs", str(meta["P"])] + meta["args"].split() + ["-m", str(m)]
+        out = subprocess.run(args + ["--verify"], capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+        assert out.returncode == 0, (cfg, m, out.stderr[-2000:])
+        if meta["methods"][str(m)]["status"] == "timeout":
+            assert "deadlocks" in out.stderr and "max total time" not in out.stdout, (cfg, m)
+            continue
+        golden = open(os.path.join(BASELINE, cfg, "report_m%d.txt" % m)).read()
+        verified = [ln for ln in out.stdout.splitlines() if "verify = " in ln]
+        body = "\n".join(ln for ln in out.stdout.splitlines() if "verify = " not in ln) + "\n"
+        assert _mask(body) == golden, (cfg, m, out.stdout[:500])
+        assert len(verified) == meta["iters"] and all("verify = OK" in ln for ln in verified), (cfg, m, verified)
