@@ -6,6 +6,11 @@ the closed-form fingerprint (xg_verify: zero mismatching bytes, strong mode so a
 misroute cannot hide), the CPU oracle confirms the schedule (every rank's MPI
 call trace equals the oracle's restatement), and the sum of the per-slot
 checksums equals the oracle's closed-form value for a sample of slots.
+
+The oracle's traces at these P = 256 shapes are themselves pinned to the reference: every rank's
+whole MPI program at configs[3]'s and configs[4]'s shapes equals the reference's by digest
+(tests/test_baseline_golden.py, captured at a reduced -d for every -c), and the programs at the
+stated -d are those with every count scaled (test_stated_size_schedules_are_the_captured_ones).
 """
 import pytest
 
