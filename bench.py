@@ -68,6 +68,13 @@ def parse():
     ap.add_argument("--child-timeout", type=float, default=0,
                     help="parent mode: seconds before the children are stopped (0: none)")
     ap.add_argument("--cpu-reps", type=int, default=10, help="-k of the reference CPU run")
+    ap.add_argument("--baseline-configs", choices=("auto", "on", "off"), default="auto",
+                    help="after the line's own measurements, run BASELINE.json's 8-GPU configurations "
+                         "(configs[2], [3], [4] at their stated sizes) on this job and add them to the line "
+                         "(auto: only when the job has 8 GPUs)")
+    ap.add_argument("--baseline-budget", type=float, default=150.0,
+                    help="seconds the BASELINE-configs phase may take; cells past it are skipped (all ranks "
+                         "alike), and a phase still running 60 s later prints the line without the rest")
     ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 900)),
                     help="rank process: seconds before a rank that is still running reports the phase it is "
                          "stuck in and exits 124 (0: off) -- a lost peer leaves RCCL waiting forever")
@@ -211,6 +218,81 @@ def p2p_sweep(ctx, world, error=RuntimeError):
                 row["GBps_aggregate"] = round(-neg_rate * world, 2)
             out.append(row)
     return out, None
+
+
+# ---------------------------------------------------------------- BASELINE.json's 8-GPU configurations
+# (name, P, A, d, -c, methods): configs[2], configs[3], configs[4] at their stated sizes
+BASELINE_CELLS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
+                   ("configs[3]", 256, 32, 4 << 20, 200000000, (1, 2, 9, 10))] +
+                  [("configs[4] -c %d" % c, 256, 64, 64 << 20, c, (7, 11, 12)) for c in range(1, 9)])
+
+
+def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_CELLS):
+    """Every method of BASELINE.json's 8-GPU configurations on this job: per (config, method) one
+    verified run (every slot checked on its GPU, bad slots MAX-reduced), one timed run (device
+    time, MAX over GPUs), delivered and cross-GPU (xGMI) GB/s and the reference's max total time.
+    Collective throughout: every rank takes the same cells in the same order, and every decision
+    (budget spent, a plan or allocation that failed on some GPU) is MAX-reduced first, so all ranks
+    skip alike.  Fills result["cells"] as it goes (a watchdog may print it half done)."""
+    t0 = time.time()
+    result["cells"] = cells_out = {}
+    regions = {}                      # (P, A, d) -> Regions shared by that configuration's cells
+    try:
+        for name, P, A, d, c, methods in cells:
+            rl = xg.aggregator_list(P, A)
+            for m in methods:
+                key = "%s m%d" % (name, m)
+                phase("BASELINE configs: %s" % key)
+                if ctx.allreduce_max([time.time() - t0])[0] > budget:
+                    cells_out[key] = "skipped: phase budget of %.0f s spent" % budget
+                    continue
+                run, err = None, ""
+                try:
+                    s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
+                    need = [0] * xg.NBUF
+                    for mm in methods:          # one allocation per configuration, sized for all its methods
+                        v = xg.Schedule(mm, P, A, d, c, rl, ntimes=1).devplan(world, rank)
+                        need = [max(x, y) for x, y in zip(need, v.region_bytes)]
+                    rk = (P, A, d)
+                    if rk not in regions:
+                        for old in regions.values():
+                            old.close()
+                        regions.clear()
+                        regions[rk] = xg.Regions(ctx, need)
+                    run = xg.MethodRun(ctx, s, it=0, mode=0, regions=regions[rk])
+                except xg.XGError as e:
+                    err = str(e)
+                if ctx.allreduce_max([1.0 if err else 0.0])[0]:
+                    cells_out[key] = "failed: %s" % (err or "on another GPU")
+                    if run is not None:
+                        run.close()
+                    continue
+                try:
+                    ctx.barrier()
+                    done, post, _wall = run.run_timed()
+                    lo, hi = s.block_range(world, rank)
+                    tmax = max(s.rank_timer(q, done, post, world).total_time for q in range(lo, hi)) if hi > lo else 0.0
+                    _chk, bad, _first = run.verify()
+                    tmax, nbad = ctx.allreduce_max([tmax, float(sum(1 for b in bad if b))])
+                    ctx.barrier()
+                    ctx.device_sync()
+                    t1 = time.perf_counter()
+                    run.enqueue()
+                    ctx.device_sync()
+                    run.check()
+                    t_run = ctx.allreduce_max([time.perf_counter() - t1])[0]
+                    cross = sum(s.devplan(world, g).remote_send_bytes for g in range(world))
+                    cells_out[key] = {"P": P, "A": A, "d": d, "c": c, "ms_per_run": round(t_run * 1e3, 4),
+                                      "GBps_delivered": round(P * A * d / t_run / 1e9, 2),
+                                      "GBps_cross_gpu": round(cross / t_run / 1e9, 2),
+                                      "cross_gpu_bytes": int(cross), "max_total_time_s": tmax,
+                                      "verified": nbad == 0, "bad_slots_max_gpu": int(nbad)}
+                finally:
+                    run.close()
+    finally:
+        for r in regions.values():
+            r.close()
+    result["spent_s"] = round(time.time() - t0, 1)
 
 
 # ---------------------------------------------------------------- N-GPU job without a launcher
@@ -570,11 +652,8 @@ def main():
                 "ceiling_error": ceil_err}
         phase("xGMI p2p sweep")
         xgmi["sweep"], xgmi["sweep_error"] = p2p_sweep(ctx, world, xg.XGError)
-    if rank != 0:
-        ctx.close()
-        return 0
     roof = None
-    if nlaunch:
+    if nlaunch and rank == 0:
         avg_s = kms / nlaunch / 1e3
         per_launch = kbytes / nlaunch
         achieved = per_launch / avg_s / 1e9
@@ -619,7 +698,33 @@ def main():
         "pack_autotune_ms_per_run": tune or None,
         "cpu_baseline": cpu,
     }
-    print(json.dumps(out))
+    if a.baseline_configs == "on" or (a.baseline_configs == "auto" and world == 8):
+        # BASELINE.json's 8-GPU configurations on this job, after everything above is measured.
+        # The line must come out whatever happens in there: a rank still in the phase 60 s past its
+        # budget (a peer lost inside RCCL waits forever) prints the line with what was done (rank 0)
+        # and ends its process.
+        for r in runs:
+            r.close()
+        runs = []
+        extra = out["baseline_configs_8gpu"] = {"budget_s": a.baseline_budget}
+
+        def overdue():
+            extra["error"] = "still in phase '%s' %.0f s after the budget; line printed from what was done" % (
+                PHASE[0], 60.0)
+            if rank == 0:
+                print(json.dumps(out), flush=True)
+            os._exit(0)
+
+        guard = threading.Timer(a.baseline_budget + 60.0, overdue)
+        guard.daemon = True
+        guard.start()
+        try:
+            baseline_configs_phase(xg, ctx, world, rank, a.baseline_budget, extra)
+        except xg.XGError as e:
+            extra["error"] = str(e)
+        guard.cancel()
+    if rank == 0:
+        print(json.dumps(out))
     ctx.close()
     return 0
 

@@ -119,6 +119,8 @@ def make(real_xg):
     class MethodRun:
         def __init__(self, ctx, sched, it=0, mode=0, pack_max_seg=4 << 20, regions=None, pack_min=0, pack_form=-1):
             self.ctx, self.sched, self.pack_max_seg, self.pack_form = ctx, sched, pack_max_seg, pack_form
+            if os.environ.get("XG_FAKE_PLAN_FAIL") == "%d:%d" % (sched.method, ctx.rank):
+                raise real_xg.XGError("xg_regions_alloc failed with code 4 (injected)")
             G, g = ctx.nranks, ctx.rank
             if G > 1:     # as the real MethodRun: refuse calls RCCL would not pair
                 sched.check_pairing(G, pack_max_seg, pack_min, pack_form,
@@ -162,9 +164,21 @@ def make(real_xg):
         def close(self):
             pass
 
+    class Regions:
+        def __init__(self, ctx, region_bytes):
+            self.bytes = list(region_bytes)
+            trace.append(["regions", [int(b) for b in region_bytes]])
+
+        def fits(self, region_bytes):
+            return all(a <= b for a, b in zip(region_bytes, self.bytes))
+
+        def close(self):
+            pass
+
     fake.unique_id = unique_id
     fake.Context = Context
     fake.MethodRun = MethodRun
+    fake.Regions = Regions
     return fake
 
 

@@ -173,3 +173,35 @@ def test_bench_survives_a_failing_ceiling_and_sweep(tmp_path):
     assert [(r["mode"], r["bytes"]) for r in x["sweep"]] == [("one_way_1_to_0", 4096), ("all_pairs", 4096),
                                                              ("one_way_1_to_0", 65536), ("all_pairs", 65536),
                                                              ("one_way_1_to_0", 1 << 20)]
+
+
+def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
+    """--baseline-configs on (the default at 8 GPUs): after the line's own measurements every method
+    of configs[2], [3] and [4] (stated sizes) runs on the job, one verified and one timed run each,
+    and lands in the line; a plan that fails on one GPU (injected: m9 on GPU 1) is recorded for that
+    cell on every rank and the rest go on"""
+    argv = ARGV2 + ["--baseline-configs", "on", "--no-ktime"]
+    rcs, outs = _run_job(2, argv, tmp_path, {"XG_FAKE_PLAN_FAIL": "9:1"})
+    assert rcs == [0, 0], [o[1][-1500:] for o in outs]
+    out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+    assert out["value"] > 0 and out["xgmi"]["peak"] > 0
+    ex = out["baseline_configs_8gpu"]
+    cells = ex["cells"]
+    want = ["configs[2] m5", "configs[2] m8"] + ["configs[3] m%d" % m for m in (1, 2, 9, 10)] + \
+           ["configs[4] -c %d m%d" % (c, m) for c in range(1, 9) for m in (7, 11, 12)]
+    assert list(cells) == want
+    assert cells["configs[3] m9"].startswith("failed")
+    for k, v in cells.items():
+        if k != "configs[3] m9":
+            assert v["verified"] and v["ms_per_run"] > 0 and v["GBps_cross_gpu"] > 0, (k, v)
+    assert cells["configs[4] -c 1 m7"]["cross_gpu_bytes"] == 256 * 64 * (64 << 20) // 2   # half the pairs cross
+    assert "error" not in ex and ex["spent_s"] >= 0
+
+
+def test_bench_baseline_configs_phase_keeps_to_its_budget(tmp_path):
+    argv = ARGV2 + ["--baseline-configs", "on", "--baseline-budget", "0", "--no-ktime"]
+    rcs, outs = _run_job(2, argv, tmp_path, {})
+    assert rcs == [0, 0], [o[1][-1500:] for o in outs]
+    out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+    cells = out["baseline_configs_8gpu"]["cells"]
+    assert len(cells) == 2 + 4 + 24 and all(str(v).startswith("skipped: phase budget") for v in cells.values())
