@@ -72,9 +72,9 @@ def parse():
                     help="after the line's own measurements, run BASELINE.json's 8-GPU configurations "
                          "(configs[2], [3], [4] at their stated sizes) on this job and add them to the line "
                          "(auto: only when the job has 8 GPUs)")
-    ap.add_argument("--baseline-budget", type=float, default=150.0,
+    ap.add_argument("--baseline-budget", type=float, default=90.0,
                     help="seconds the BASELINE-configs phase may take; cells past it are skipped (all ranks "
-                         "alike), and a phase still running 60 s later prints the line without the rest")
+                         "alike), and a phase still running 45 s later prints the line without the rest")
     ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 900)),
                     help="rank process: seconds before a rank that is still running reports the phase it is "
                          "stuck in and exits 124 (0: off) -- a lost peer leaves RCCL waiting forever")
@@ -700,7 +700,7 @@ def main():
     }
     if a.baseline_configs == "on" or (a.baseline_configs == "auto" and world == 8):
         # BASELINE.json's 8-GPU configurations on this job, after everything above is measured.
-        # The line must come out whatever happens in there: a rank still in the phase 60 s past its
+        # The line must come out whatever happens in there: a rank still in the phase 45 s past its
         # budget (a peer lost inside RCCL waits forever) prints the line with what was done (rank 0)
         # and ends its process.
         for r in runs:
@@ -710,12 +710,12 @@ def main():
 
         def overdue():
             extra["error"] = "still in phase '%s' %.0f s after the budget; line printed from what was done" % (
-                PHASE[0], 60.0)
+                PHASE[0], 45.0)
             if rank == 0:
                 print(json.dumps(out), flush=True)
             os._exit(0)
 
-        guard = threading.Timer(a.baseline_budget + 60.0, overdue)
+        guard = threading.Timer(a.baseline_budget + 45.0, overdue)
         guard.daemon = True
         guard.start()
         try:
