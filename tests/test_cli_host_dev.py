@@ -156,3 +156,18 @@ def test_pt2pt_two_processes(exes, tmp_path):
     assert p.stdout.count("status = 1, statuses = 1") == 2
     rows = open(tmp_path / "cwd" / "sendrecv_results.csv").read().split()
     assert len(rows) == 4 and all(float(x) > 0 for x in rows)
+
+
+@pytest.mark.parametrize("args", [["-m", 7, "-a", 64, "-c", 3], ["-m", 11, "-a", 64, "-c", 8], ["-m", 9, "-a", 32]],
+                         ids=["m7_c3", "m11_c8", "m9"])
+def test_p256_on_8_processes(exes, tmp_path, args):
+    """the BASELINE 8-GPU jobs' rank counts through the CLI's multi-process path: P = 256 logical
+    ranks (32 per process) on 8 processes, configs[4]'s / configs[3]'s shape at a reduced -d, every
+    received byte verified, the report equal in form to the one-process run's"""
+    full = args + ["-d", 16, "--procs", 256, "--verify", "-k", 2]
+    p = _run(exes["test"], full + ["--gpus", 8], tmp_path, timeout=600)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "verify = OK" in p.stdout and "FAILED" not in p.stdout, p.stdout[-2000:]
+    one = _run(exes["test"], full, tmp_path / "one", timeout=600)
+    assert one.returncode == 0, one.stderr[-3000:]
+    assert _normalise(p.stdout) == _normalise(one.stdout)
