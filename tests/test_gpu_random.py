@@ -18,6 +18,7 @@ import pytest
 # XG_RANDOM_N1 / XG_RANDOM_NV: widen the sweep (one GPU / virtual jobs) for an evidence run
 N1 = int(os.environ.get("XG_RANDOM_N1", 120))
 NV = int(os.environ.get("XG_RANDOM_NV", 60))
+SEED = int(os.environ.get("XG_RANDOM_SEED", 0))      # another draw of the same sweep (evidence runs)
 
 pytestmark = pytest.mark.gpu
 
@@ -69,7 +70,7 @@ def ctx(xg):
     c.close()
 
 
-@pytest.mark.parametrize("cfg", _configs(2026, N1), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
+@pytest.mark.parametrize("cfg", _configs(2026 + SEED, N1), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
 def test_random_config_one_gpu(xg, ctx, cfg):
     s, rl = _schedule(xg, cfg)
     run = xg.MethodRun(ctx, s, it=cfg[-1], mode=1)
@@ -112,7 +113,7 @@ def worlds(xg):
             c.close()
 
 
-@pytest.mark.parametrize("cfg", _configs(7, NV), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
+@pytest.mark.parametrize("cfg", _configs(7 + SEED, NV), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
 def test_random_config_virtual_gpus(xg, worlds, cfg):
     rng = random.Random(hash(cfg) & 0xffff)
     G = rng.choice([2, 3, 4, 8])
@@ -153,7 +154,7 @@ def _large_configs(seed, n):
     return out
 
 
-@pytest.mark.parametrize("cfg", _large_configs(11, NL), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
+@pytest.mark.parametrize("cfg", _large_configs(11 + SEED, NL), ids=lambda c: "m%d_P%d_A%d_d%d_c%d_k%d_t%d_pn%d_b%d" % c[:9])
 def test_random_large_p_virtual_gpus(xg, worlds, cfg):
     """P = 48..256 as 4- and 8-GPU virtual jobs (the BASELINE jobs' rank counts), every method,
     direct and packed, copies or RCCL, every slot against the oracle's closed form"""
