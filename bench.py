@@ -237,6 +237,7 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
     t0 = time.time()
     result["cells"] = cells_out = {}
     regions = {}                      # (P, A, d) -> Regions shared by that configuration's cells
+    no_room = set()                   # (P, A, d) whose regions could not be allocated on some GPU
     try:
         for name, P, A, d, c, methods in cells:
             rl = xg.aggregator_list(P, A)
@@ -246,7 +247,10 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                 if ctx.allreduce_max([time.time() - t0])[0] > budget:
                     cells_out[key] = "skipped: phase budget of %.0f s spent" % budget
                     continue
-                run, err = None, ""
+                if (P, A, d) in no_room:
+                    cells_out[key] = "skipped: this configuration's regions did not fit"
+                    continue
+                run, err, no_alloc = None, "", False
                 try:
                     s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
                     need = [0] * xg.NBUF
@@ -258,14 +262,19 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                         for old in regions.values():
                             old.close()
                         regions.clear()
+                        no_alloc = True
                         regions[rk] = xg.Regions(ctx, need)
+                        no_alloc = False
                     run = xg.MethodRun(ctx, s, it=0, mode=0, regions=regions[rk])
                 except xg.XGError as e:
                     err = str(e)
-                if ctx.allreduce_max([1.0 if err else 0.0])[0]:
+                failed, unplaced = ctx.allreduce_max([1.0 if err else 0.0, 1.0 if no_alloc else 0.0])
+                if failed:
                     cells_out[key] = "failed: %s" % (err or "on another GPU")
                     if run is not None:
                         run.close()
+                    if unplaced:      # some GPU never got this configuration's regions: the rest would fail alike
+                        no_room.add((P, A, d))
                     continue
                 try:
                     ctx.barrier()

@@ -167,6 +167,9 @@ def make(real_xg):
     class Regions:
         def __init__(self, ctx, region_bytes):
             self.bytes = list(region_bytes)
+            lim = os.environ.get("XG_FAKE_REGIONS_FAIL")       # "<max bytes>:<rank>"
+            if lim and int(lim.split(":")[1]) == ctx.rank and sum(self.bytes) > int(lim.split(":")[0]):
+                raise real_xg.XGError("xg_regions_alloc failed with code 4 (injected: %d B)" % sum(self.bytes))
             trace.append(["regions", [int(b) for b in region_bytes]])
 
         def fits(self, region_bytes):

@@ -205,3 +205,18 @@ def test_bench_baseline_configs_phase_keeps_to_its_budget(tmp_path):
     out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
     cells = out["baseline_configs_8gpu"]["cells"]
     assert len(cells) == 2 + 4 + 24 and all(str(v).startswith("skipped: phase budget") for v in cells.values())
+
+
+def test_bench_baseline_configs_phase_skips_a_configuration_that_does_not_fit(tmp_path):
+    """GPU 1 cannot allocate configs[4]'s regions (injected past 64 GiB): the first -c 1 cell
+    records the failure on every rank, the other 23 cells of that configuration are skipped without
+    another allocation attempt, and configs[2] / [3] still run"""
+    argv = ARGV2 + ["--baseline-configs", "on", "--no-ktime"]
+    rcs, outs = _run_job(2, argv, tmp_path, {"XG_FAKE_REGIONS_FAIL": "%d:1" % (64 << 30)})
+    assert rcs == [0, 0], [o[1][-1500:] for o in outs]
+    out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+    cells = out["baseline_configs_8gpu"]["cells"]
+    assert cells["configs[4] -c 1 m7"].startswith("failed: ")
+    rest = [k for k in cells if k.startswith("configs[4]") and k != "configs[4] -c 1 m7"]
+    assert len(rest) == 23 and all(cells[k] == "skipped: this configuration's regions did not fit" for k in rest)
+    assert all(cells[k]["verified"] for k in cells if not k.startswith("configs[4]"))
