@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--baseline-budget", type=float, default=90.0,
                     help="seconds the BASELINE-configs phase may take; cells past it are skipped (all ranks "
                          "alike), and a phase still running 45 s later prints the line without the rest")
+    ap.add_argument("--xgmi-budget", type=float, default=120.0,
+                    help="N > 1: seconds the xGMI ceiling + sweep phase may take before the line is printed "
+                         "without the rest of it")
     ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 900)),
                     help="rank process: seconds before a rank that is still running reports the phase it is "
                          "stuck in and exits 124 (0: off) -- a lost peer leaves RCCL waiting forever")
@@ -104,6 +107,36 @@ def start_watchdog(seconds, rank):
     t = threading.Timer(seconds, fire)
     t.daemon = True
     t.start()
+
+
+class LineGuard:
+    """Once the line's value is measured it must come out: a phase run under this guard that is
+    still going `seconds` after it started (a peer lost inside RCCL waits forever) has
+    note(message) record why in `out`, rank 0 print `out` as it stands, and the process end
+    (os._exit(0): the measured line is the result; nothing else runs in the process's place)."""
+
+    def __init__(self, out, rank, seconds, note):
+        self.out, self.rank, self.seconds, self.note = out, rank, seconds, note
+        self.timer = None
+
+    def _fire(self):
+        self.note("still in phase '%s' %.0f s after it started; line printed from what was measured"
+                  % (PHASE[0], self.seconds))
+        if self.rank == 0:
+            print(json.dumps(self.out), flush=True)
+        os._exit(0)
+
+    def __enter__(self):
+        if self.seconds > 0:
+            self.timer = threading.Timer(self.seconds, self._fire)
+            self.timer.daemon = True
+            self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self.timer:
+            self.timer.cancel()
+        return False
 
 
 # ---------------------------------------------------------------- CPU baseline (reference)
@@ -425,6 +458,41 @@ def rendezvous_uid(xg, rank, world):
         time.sleep(0.01)
 
 
+def xgmi_phase(xg, ctx, runs, world, nmethods, steps, elapsed, out):
+    """N > 1: the timed region's cross-GPU bytes against the measured RCCL all-pairs ceiling, and the
+    pt2pt sweep; out["xgmi"] is filled as the figures come in (a guard may print it half done).
+    The ceiling and the sweep are measurements beside the exchange, not the exchange: an RCCL error
+    in them leaves null + the error in the line (as long as the ranks can still agree on it --
+    every rank reduces the error flag with the figures)."""
+    phase("xGMI ceiling (RCCL all-pairs send/recv)")
+    cross_step = 0      # every rank derives every GPU's plan (deterministic, cheap)
+    for r in runs:
+        for g in range(world):
+            cross_step += r.sched.devplan(world, g, r.pack_max_seg).remote_send_bytes
+    per_pair = max(65536, (cross_step // max(1, nmethods * world * (world - 1)) + 4095) & ~4095)
+    achieved = cross_step * steps / elapsed / 1e9
+    xgmi = out["xgmi"] = {"achieved": round(achieved, 1), "peak": None, "unit": "GB/s", "frac": None,
+                          "cross_gpu_bytes_per_step": int(cross_step),
+                          "peak_source": "measured: RCCL all-pairs send/recv, %d B per GPU pair, slowest GPU "
+                                         "egress x %d (xg_p2p_bench mode 0)" % (per_pair, world),
+                          "ceiling_error": None}
+    ceil_err = None
+    try:
+        ceil_gbps, _ = ctx.p2p_bench(per_pair, mode=0, reps=20)
+        err = 0.0
+    except xg.XGError as e:
+        ceil_gbps, err, ceil_err = 0.0, 1.0, str(e)
+    neg, err = ctx.allreduce_max([-ceil_gbps, err])
+    if err:
+        xgmi["ceiling_error"] = ceil_err or "failed on another GPU"
+    else:
+        ceil_min = -neg                                       # slowest GPU's egress
+        xgmi["peak"] = round(ceil_min * world, 1)
+        xgmi["frac"] = round(achieved / (ceil_min * world), 4)
+    phase("xGMI p2p sweep")
+    xgmi["sweep"], xgmi["sweep_error"] = p2p_sweep(ctx, world, xg.XGError)
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -628,39 +696,6 @@ def main():
     seg_bytes = float(a.procs) * a.aggs * a.size * len(methods) * a.steps
     value = seg_bytes / elapsed / 1e9
 
-    # N > 1: cross-GPU (xGMI) bytes of the timed region vs the measured RCCL all-pairs ceiling
-    xgmi = None
-    if world > 1:
-        phase("xGMI ceiling (RCCL all-pairs send/recv)")
-        cross_step = 0      # every rank derives every GPU's plan (deterministic, cheap)
-        for r in runs:
-            for g in range(world):
-                cross_step += r.sched.devplan(world, g, r.pack_max_seg).remote_send_bytes
-        per_pair = max(65536, (cross_step // max(1, len(methods) * world * (world - 1)) + 4095) & ~4095)
-        achieved = cross_step * a.steps / elapsed / 1e9
-        # the ceiling and the sweep are measurements beside the exchange, not the exchange: an
-        # RCCL error in them leaves null + the error in the line (as long as the ranks can still
-        # agree on it -- every rank reduces the error flag with the figures)
-        ceil_min, ceil_err = None, None
-        try:
-            ceil_gbps, _ = ctx.p2p_bench(per_pair, mode=0, reps=20)
-            err = 0.0
-        except xg.XGError as e:
-            ceil_gbps, err, ceil_err = 0.0, 1.0, str(e)
-        neg, err = ctx.allreduce_max([-ceil_gbps, err])
-        if err:
-            ceil_err = ceil_err or "failed on another GPU"
-        else:
-            ceil_min = -neg                                       # slowest GPU's egress
-        peak = round(ceil_min * world, 1) if ceil_min else None
-        xgmi = {"achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
-                "frac": round(achieved / (ceil_min * world), 4) if ceil_min else None,
-                "cross_gpu_bytes_per_step": int(cross_step),
-                "peak_source": "measured: RCCL all-pairs send/recv, %d B per GPU pair, slowest GPU egress x %d "
-                               "(xg_p2p_bench mode 0)" % (per_pair, world),
-                "ceiling_error": ceil_err}
-        phase("xGMI p2p sweep")
-        xgmi["sweep"], xgmi["sweep_error"] = p2p_sweep(ctx, world, xg.XGError)
     roof = None
     if nlaunch and rank == 0:
         avg_s = kms / nlaunch / 1e3
@@ -703,10 +738,14 @@ def main():
                    "parallelism": "block-mapped logical ranks; intra-GPU copy_kernel + grouped RCCL p2p"},
         "max_total_time_s": max_total,      # per method, one -k repetition, median of 3 warm runs
         "roofline": roof,
-        "xgmi": xgmi,
+        "xgmi": None,
         "pack_autotune_ms_per_run": tune or None,
         "cpu_baseline": cpu,
     }
+    if world > 1:
+        # N > 1: cross-GPU (xGMI) bytes of the timed region vs the measured RCCL all-pairs ceiling
+        with LineGuard(out, rank, a.xgmi_budget, lambda msg: out.__setitem__("xgmi_error", msg)):
+            xgmi_phase(xg, ctx, runs, world, len(methods), a.steps, elapsed, out)
     if a.baseline_configs == "on" or (a.baseline_configs == "auto" and world == 8):
         # BASELINE.json's 8-GPU configurations on this job, after everything above is measured.
         # The line must come out whatever happens in there: a rank still in the phase 45 s past its
@@ -716,22 +755,11 @@ def main():
             r.close()
         runs = []
         extra = out["baseline_configs_8gpu"] = {"budget_s": a.baseline_budget}
-
-        def overdue():
-            extra["error"] = "still in phase '%s' %.0f s after the budget; line printed from what was done" % (
-                PHASE[0], 45.0)
-            if rank == 0:
-                print(json.dumps(out), flush=True)
-            os._exit(0)
-
-        guard = threading.Timer(a.baseline_budget + 45.0, overdue)
-        guard.daemon = True
-        guard.start()
-        try:
-            baseline_configs_phase(xg, ctx, world, rank, a.baseline_budget, extra)
-        except xg.XGError as e:
-            extra["error"] = str(e)
-        guard.cancel()
+        with LineGuard(out, rank, a.baseline_budget + 45.0, lambda msg: extra.__setitem__("error", msg)):
+            try:
+                baseline_configs_phase(xg, ctx, world, rank, a.baseline_budget, extra)
+            except xg.XGError as e:
+                extra["error"] = str(e)
     if rank == 0:
         print(json.dumps(out))
     ctx.close()

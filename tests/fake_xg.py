@@ -18,7 +18,8 @@ def make(real_xg):
     """fault injection (bench.py's partial-failure paths), on the rank XG_FAKE_FAIL_RANK names
     (default: every rank): XG_FAKE_VERIFY_FAIL=<method>:<pack_max_seg>:<pack_form>,... makes that
     plan's verify report a wrong slot; XG_FAKE_P2P_FAIL=<n>,... makes the n-th p2p_bench call
-    (0-based: 0 = bench.py's xGMI ceiling, 1.. = its sweep) raise XGError"""
+    (0-based: 0 = bench.py's xGMI ceiling, 1.. = its sweep) raise XGError; XG_FAKE_P2P_HANG=<n>,...
+    makes it never return"""
     fake = types.ModuleType("xg")
     for name in ("aggregator_list", "Schedule", "XGError", "NBUF", "BUF_SEND", "BUF_RECV",
                  "BUF_STAGE_SEND", "BUF_STAGE_RECV", "BUF_SCRATCH", "PACK_TWO_SIDED", "PACK_ONE_SIDED",
@@ -111,6 +112,9 @@ def make(real_xg):
             trace.append(["p2p_bench", int(nbytes), int(mode), int(reps)])
             if _on_fail_rank(self.rank) and (calls["p2p_bench"] - 1,) in _faults("XG_FAKE_P2P_FAIL"):
                 raise real_xg.XGError("xg_p2p_bench failed with code 5 (injected)")
+            if _on_fail_rank(self.rank) and (calls["p2p_bench"] - 1,) in _faults("XG_FAKE_P2P_HANG"):
+                while True:          # a peer lost inside RCCL: this call never returns
+                    time.sleep(1)
             return 50.0, nbytes / 50e9
 
         def close(self):

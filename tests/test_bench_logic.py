@@ -3,6 +3,7 @@ with the REAL host scheduler: per-method direct-vs-packed tuning, the per-launch
 pass, the xGMI object, the JSON line -- the code path only the driver's multi-GPU run
 executes on hardware, checked here for crashes and for the line's schema."""
 import json
+import time
 import os
 import subprocess
 import sys
@@ -220,3 +221,19 @@ def test_bench_baseline_configs_phase_skips_a_configuration_that_does_not_fit(tm
     rest = [k for k in cells if k.startswith("configs[4]") and k != "configs[4] -c 1 m7"]
     assert len(rest) == 23 and all(cells[k] == "skipped: this configuration's regions did not fit" for k in rest)
     assert all(cells[k]["verified"] for k in cells if not k.startswith("configs[4]"))
+
+
+def test_bench_line_survives_a_hang_in_the_xgmi_phase(tmp_path):
+    """the line's value is measured, then one GPU never returns from the sweep's second call (a
+    peer lost inside RCCL): after --xgmi-budget seconds rank 0 prints the line as measured -- the
+    value, the ceiling, the sweep rows so far -- with xgmi_error naming the phase, and every rank
+    ends (exit 0) instead of waiting for the 900 s watchdog"""
+    argv = ARGV2 + ["--xgmi-budget", "8", "--no-ktime"]
+    t0 = time.time()
+    rcs, outs = _run_job(2, argv, tmp_path, {"XG_FAKE_P2P_HANG": "2", "XG_FAKE_FAIL_RANK": "1"})
+    assert rcs == [0, 0], [o[1][-1500:] for o in outs]
+    assert time.time() - t0 < 100
+    out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+    assert out["value"] > 0 and out["xgmi"]["peak"] > 0 and out["xgmi"]["ceiling_error"] is None
+    assert out["xgmi_error"].startswith("still in phase 'xGMI p2p sweep' 8 s after it started")
+    assert "sweep" not in out["xgmi"]          # the sweep never finished
