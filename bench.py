@@ -102,6 +102,9 @@ def start_watchdog(seconds, rank):
     def fire():
         sys.stderr.write("bench: rank %d still in phase '%s' after %.0f s; exiting\n" % (rank, PHASE[0], seconds))
         sys.stderr.flush()
+        if rank == 0:     # no value was measured (phases after it have guards of their own): say where it stopped
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "higher_is_better": True,
+                              "error": "rank 0 still in phase '%s' after %.0f s" % (PHASE[0], seconds)}), flush=True)
         os._exit(124)
 
     t = threading.Timer(seconds, fire)

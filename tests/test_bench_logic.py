@@ -237,3 +237,21 @@ def test_bench_line_survives_a_hang_in_the_xgmi_phase(tmp_path):
     assert out["value"] > 0 and out["xgmi"]["peak"] > 0 and out["xgmi"]["ceiling_error"] is None
     assert out["xgmi_error"].startswith("still in phase 'xGMI p2p sweep' 8 s after it started")
     assert "sweep" not in out["xgmi"]          # the sweep never finished
+
+
+def test_watchdog_on_rank0_prints_a_line_naming_the_phase(tmp_path):
+    """rank 0 of a 2-GPU job whose rank 1 never comes waits in the communicator init: the watchdog
+    prints a line with value null and the phase it stopped in, then exits 124"""
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="2", XG_FAKE_BARRIER_DIR=str(tmp_path),
+               XG_RDZV_KEY="wd0_%s" % tmp_path.name)
+    code = DRIVER.format(repo=REPO, argv=["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                                          "--watchdog", "3"])
+    try:
+        p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    finally:
+        rdzv = "/tmp/xg_bench_rdzv_wd0_%s.bin" % tmp_path.name
+        if os.path.exists(rdzv):
+            os.unlink(rdzv)
+    assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert out["value"] is None and out["error"].startswith("rank 0 still in phase 'RCCL communicator init")
