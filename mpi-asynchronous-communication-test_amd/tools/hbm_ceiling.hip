@@ -27,6 +27,15 @@
 //   kind 24 the same in 4 KiB pieces, copy_kernel_w<4, nt>   kind 25 16 KiB pieces, copy_kernel_w<16, nt>
 //   kind 26 the kind-18 pack in the two-sided order (per peer, per sender), copy_kernel_g<4> 16 KiB
 //   kind 27 the same, copy_kernel_w<8> over 8 KiB pieces (the product since call K)
+//   round 4, the kind-16 gather (448 MiB) against the piece size, the pipeline depth and the cache
+//   policy of the loads and stores (buffer accesses, gfx950 cpol bits: sc0 1, nt 2, sc1 16):
+//   kind 28 copy_kernel_g<4, nt> 64 KiB pieces      kind 29 copy_kernel_g<8, nt> 32 KiB
+//   kind 30 copy_kernel_g<4, nt> 128 KiB            kind 31 copy_kernel_g<4, nt> 16 KiB
+//   kind 32 copy_kernel_bb<4, load nt, store nt>    kind 33 <4, nt, nt|sc1>
+//   kind 34 <4, nt|sc0|sc1, nt|sc0|sc1>             kind 35 <4, nt, sc0|sc1>
+//   kind 36 <4, plain, nt>                          kind 37 <4, nt, plain>
+//   kind 38 the contiguous copy (kind 9's pieces) as copy_kernel_bb<4, nt, nt|sc1>
+//   kind 39 the kind-16 gather, copy_kernel_bb<4, nt|sc1, nt|sc1>
 // *gbps = counted bytes / average launch time (a copy counts read + write).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -59,6 +68,31 @@ __device__ __forceinline__ void pipelined_copy16_b(const uint8_t *src, uint8_t *
         for (int u = 0; u < U; ++u) nxt[u] = xgk::bload16(rs, base + blk + lane + u * xgk::kThreads * 16);
 #pragma unroll
         for (int u = 0; u < U; ++u) xgk::bstore16<AUX>(rd, base + lane + u * xgk::kThreads * 16, cur[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+    }
+}
+
+// copy_kernel_bb<U, LAUX, SAUX>: the same pipelined piece copy with the cache policy of the
+// loads (LAUX) and of the stores (SAUX) chosen (round-4 A/B on the bench's gather, kinds 32-37)
+template <int U, int LAUX, int SAUX>
+__global__ __launch_bounds__(xgk::kThreads) void copy_kernel_bb(const xgk::DCopy *__restrict__ pieces)
+{
+    const xgk::DCopy c = pieces[blockIdx.x];
+    const int n = (int)c.len;
+    const xgk::brsrc rs = xgk::make_rsrc(c.src, n), rd = xgk::make_rsrc(c.dst, n);
+    constexpr int blk = U * xgk::kThreads * 16;
+    const int lane = (int)threadIdx.x * 16;
+    xgk::u32x4 cur[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane + u * xgk::kThreads * 16, 0, LAUX);
+    for (int base = 0; base < n; base += blk) {
+        xgk::u32x4 nxt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            nxt[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, base + blk + lane + u * xgk::kThreads * 16, 0, LAUX);
+#pragma unroll
+        for (int u = 0; u < U; ++u) xgk::bstore16<SAUX>(rd, base + lane + u * xgk::kThreads * 16, cur[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) cur[u] = nxt[u];
     }
@@ -185,7 +219,7 @@ __global__ __launch_bounds__(xgk::kThreads) void gridstride_copy_mix(const xgk::
 extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, double *gbps)
 {
     bytes &= ~(int64_t)32767;
-    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 27) return 3;
+    if (bytes <= 0 || reps < 1 || kind < 0 || kind > 39) return 3;
     CK(hipSetDevice(device));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -195,10 +229,11 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipMalloc(&b, bytes));
     CK(hipMalloc(&sink, 4));
     CK(hipMemsetAsync(a, 1, bytes, st));
-    const int64_t piece = kind == 7 ? 262144 : kind == 8 ? 65536 : kind == 22 || kind == 23 || kind == 27 ? 8192 : kind == 24 ? 4096
+    const int64_t piece = kind == 28 ? 65536 : kind == 30 ? 131072 : kind == 31 ? 16384 : kind >= 29 ? 32768
+                        : kind == 7 ? 262144 : kind == 8 ? 65536 : kind == 22 || kind == 23 || kind == 27 ? 8192 : kind == 24 ? 4096
                         : kind == 25 ? 16384 : kind >= 18 ? 16384 : 32768;
     std::vector<xgk::DCopy> pieces;
-    if (kind == 16 || kind == 17 || kind == 23 || kind == 24 || kind == 25) {   // bytes ignored: 14 x 32 one-MiB segments
+    if (kind == 16 || kind == 17 || kind == 23 || kind == 24 || kind == 25 || (kind >= 28 && kind != 38)) {   // bytes ignored: 14 x 32 one-MiB segments
         const int64_t seg = 1 << 20, stride = 32 * seg + (kind == 17 ? 65536 : 0);
         if (14 * stride > bytes) return 3;
         for (int r = 0; r < 32; ++r)
@@ -282,6 +317,18 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
                                     (int)np, nullptr); break;
         case 27: hipLaunchKernelGGL((xgk::copy_kernel_w<8, false>), dim3(wgrid), dim3(xgk::kThreads), 0, st, dp,
                                     (int)np, nullptr); break;
+        case 28:
+        case 30:
+        case 31: hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
+        case 29: hipLaunchKernelGGL((xgk::copy_kernel_g<8, true>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
+        case 32: hipLaunchKernelGGL((copy_kernel_bb<4, 2, 2>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        case 33: hipLaunchKernelGGL((copy_kernel_bb<4, 2, 18>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        case 34: hipLaunchKernelGGL((copy_kernel_bb<4, 19, 19>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        case 35: hipLaunchKernelGGL((copy_kernel_bb<4, 2, 17>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        case 36: hipLaunchKernelGGL((copy_kernel_bb<4, 0, 2>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        case 37: hipLaunchKernelGGL((copy_kernel_bb<4, 2, 0>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        case 38: hipLaunchKernelGGL((copy_kernel_bb<4, 2, 18>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
+        case 39: hipLaunchKernelGGL((copy_kernel_bb<4, 18, 18>), dim3(np), dim3(xgk::kThreads), 0, st, dp); break;
         default: hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(np), dim3(xgk::kThreads), 0, st, dp, nullptr); break;
         }
         CK(hipGetLastError());
@@ -290,7 +337,7 @@ extern "C" int xgt_copy_ceiling(int device, int64_t bytes, int kind, int reps, d
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    const double moved = kind == 16 || kind == 17 || (kind >= 23 && kind <= 25) ? 448.0 * (1 << 20) : kind >= 18 ? 28.0 * (1 << 20)
+    const double moved = kind == 16 || kind == 17 || (kind >= 23 && kind <= 25) || (kind >= 28 && kind != 38) ? 448.0 * (1 << 20) : kind >= 18 ? 28.0 * (1 << 20)
                                                                                                : (double)bytes;
     *gbps = (kind == 3 || kind == 4 || kind == 10 || kind == 11 ? 1.0 : 2.0) * moved * reps / (ms * 1e-3) / 1e9;
     CK(hipEventDestroy(e0));
