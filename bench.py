@@ -100,16 +100,30 @@ def start_watchdog(seconds, rank):
         return
 
     def fire():
-        sys.stderr.write("bench: rank %d still in phase '%s' after %.0f s; exiting\n" % (rank, PHASE[0], seconds))
-        sys.stderr.flush()
-        if rank == 0:     # no value was measured (phases after it have guards of their own): say where it stopped
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "higher_is_better": True,
-                              "error": "rank 0 still in phase '%s' after %.0f s" % (PHASE[0], seconds)}), flush=True)
-        os._exit(124)
+        try:
+            sys.stderr.write("bench: rank %d still in phase '%s' after %.0f s; exiting\n" % (rank, PHASE[0], seconds))
+            sys.stderr.flush()
+            if rank == 0:     # no value was measured (phases after it have guards of their own): say where it stopped
+                print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "higher_is_better": True,
+                                  "error": "rank 0 still in phase '%s' after %.0f s" % (PHASE[0], seconds)}),
+                      flush=True)
+        finally:
+            os._exit(124)
 
     t = threading.Timer(seconds, fire)
     t.daemon = True
     t.start()
+
+
+def dumps_live(out):
+    """json.dumps of a line another thread may still be adding to (a dict that changes size while
+    it is serialised raises RuntimeError): retried a few times, then a copy made key by key"""
+    for _ in range(20):
+        try:
+            return json.dumps(out)
+        except RuntimeError:
+            time.sleep(0.005)
+    return json.dumps({k: out.get(k) for k in list(out)}, default=str)
 
 
 class LineGuard:
@@ -123,11 +137,13 @@ class LineGuard:
         self.timer = None
 
     def _fire(self):
-        self.note("still in phase '%s' %.0f s after it started; line printed from what was measured"
-                  % (PHASE[0], self.seconds))
-        if self.rank == 0:
-            print(json.dumps(self.out), flush=True)
-        os._exit(0)
+        try:
+            self.note("still in phase '%s' %.0f s after it started; line printed from what was measured"
+                      % (PHASE[0], self.seconds))
+            if self.rank == 0:
+                print(dumps_live(self.out), flush=True)
+        finally:                 # whatever happened above, the process ends
+            os._exit(0)
 
     def __enter__(self):
         if self.seconds > 0:
