@@ -663,8 +663,13 @@ extern "C" int xg_regions_alloc(xg_ctx *c, const int64_t bytes[XG_NBUF], xg_regi
             }
         }
     }
+    const int rc = xg_regions_poison(r);
+    if (rc) {                     /* nothing half made is handed out */
+        (void)xg_regions_free(r);
+        return rc;
+    }
     *out = r;
-    return xg_regions_poison(r);
+    return XG_OK;
 }
 
 extern "C" int xg_regions_poison(xg_regions *r)
