@@ -105,9 +105,10 @@ int xg_plan_nsteps(const xg_plan *p);
 /* Timed run (caller barriers first): enqueues every step, waits, and returns per
  * step the device completion time (seconds since the run started) and the host
  * enqueue time; *wall = host seconds from start to the final synchronisation.
- * What a step's completion time means: per-step launches -- the event after its
- * last launch (or, in a chain of one-launch local steps, the start of the next
- * launch), i.e. its bytes stored; engine segments -- the wall-clock stamp at the
+ * What a step's completion time means: per-step launches -- the clock stamp of a
+ * one-lane kernel that starts after its last launch, RCCL group or join (or, in a
+ * chain of one-launch local steps, the start of the next launch), i.e. its bytes
+ * stored; engine segments -- the wall-clock stamp at the
  * step's barrier, which for steps without a drain flag is when their stores were
  * ISSUED (not yet performed); only drained steps (hazard points and the last step
  * of every segment, which anchors the others) are delivery times.  A run's total

@@ -7,7 +7,7 @@
 //   2. one ncclGroupStart .. ncclSend/ncclRecv .. ncclGroupEnd with the <= 7
 //      peer GPUs this step talks to (xGMI)                  (p2p)
 //   3. one copy_kernel launch unpacking staging into the receive slots (post)
-//   4. hipEventRecord(step event)     -- the reference's Waitall boundary
+//   4. a clock_kernel stamp (step mark) -- the reference's Waitall boundary
 // All on one HIP stream per context, so step s+1 starts after step s; the
 // cross-GPU order comes from RCCL send/recv matching.
 #include <hip/hip_runtime.h>
@@ -213,9 +213,7 @@ struct xg_plan {
     std::vector<StepR> steps;
     std::vector<xg_call> calls;       // every step's RCCL calls, as xg_devplan_step_calls lists them
     std::vector<int32_t> call_begin;  // nsteps + 1: where each step's calls start
-    std::vector<hipEvent_t> ev;
     std::vector<hipEvent_t> fork, join;   // per split step: main -> side, side -> main
-    hipEvent_t ev0;
     int variant;
     bool streaming;                // one run copies more than the Infinity Cache holds (read + write)
     // step engine segments
@@ -236,12 +234,11 @@ struct xg_plan {
     int64_t *d_disp;
     int ndisp;
     int nlaunch;                   // kernel launches per run (copies + engine), RCCL's aside
-    bool rec_ev;                   // xg_plan_run is recording step events (fused launches record the previous step's)
+    bool rec_ev;                   // xg_plan_run is marking steps (fused launches mark the previous step's end)
     // chains: runs of >= 2 consecutive steps that are each ONE local copy launch, or a TAM
-    // stage launch and/or a local launch (outside engine segments, no RCCL, no barrier).  xg_plan_run times them without an event
-    // between launches (an event record costs ~5 us of idle device between two launches):
-    // launch t+1 stamps its start = step t's completion, a clock kernel closes the chain,
-    // one event after it anchors the stamps.  chain_end[s] = end of s's chain (s = its
+    // stage launch and/or a local launch (outside engine segments, no RCCL, no barrier).  xg_plan_run times them with no
+    // mark between launches: launch t+1 stamps its start = step t's completion, a clock kernel
+    // closes the chain, the chain's mark after it anchors the stamps.  chain_end[s] = end of s's chain (s = its
     // first step), 0 elsewhere.
     std::vector<int> chain_end;
     unsigned long long *d_cstamp;  // nsteps wall-clock stamps of chained steps
@@ -251,12 +248,12 @@ struct xg_plan {
     // captured at first use and replayed after (a launch-bound multi-step run then costs one
     // graph launch of host time instead of a launch, an event and an RCCL group per step)
     hipGraphExec_t g_enq, g_run;
-    // Captured HIP events are not re-recorded by a replay on this stack (tools/graph_probe.hip:
-    // elapsed times of a replay read the capture-time values, then 'invalid resource handle'),
-    // so a captured run marks its step boundaries with clock_kernel stamps instead: mark(i)
-    // writes the wall clock to d_gstamp[i + 1] (i = -1: the start) where it would record ev[i]
+    // step marks: mark(i) has a one-lane clock_kernel write the wall clock to d_gstamp[i + 1]
+    // (i = -1: the start) once everything before it on the stream is done.  Not timing events:
+    // an event record left the device idle ~4.7 us per step against ~2.1 us for the stamp
+    // (profiles/r04/stamp_marks/), and captured events are not re-recorded by a graph replay on
+    // this stack (tools/graph_probe.hip), so eager runs, graph replays and virtual jobs all stamp
     unsigned long long *d_gstamp;
-    bool stamp_marks;              // mark() stamps (graph capture) instead of recording events
     bool graph_auto;               // XG_GRAPH unset: this plan replays as a graph (latency-bound, one GPU)
     bool local_only;               // test hook (xg_plan_set_local_only): a virtual GPU runs its share alone,
                                    // its RCCL calls and in-loop barriers left out
@@ -268,29 +265,26 @@ struct xg_plan {
     } vg;                          // plans[0] of a virtual job: the job's captured run
 };
 
-// step boundary i of a run (-1: its start) on `stream`: an event, or in a captured run a stamp
+// step boundary i of a run (-1: its start) on `stream`: a clock stamp (d_gstamp)
 static int mark(xg_plan *p, int i, hipStream_t stream)
 {
-    if (!p->stamp_marks) {
-        HIPCHK(hipEventRecord(i < 0 ? p->ev0 : p->ev[i], stream));
-        return XG_OK;
-    }
     hipLaunchKernelGGL(xgk::clock_kernel, dim3(1), dim3(64), 0, stream, p->d_gstamp + i + 1);
     HIPCHK(hipGetLastError());
     return XG_OK;
 }
 
-// seconds from the run's start to boundary i, after the run (events or stamps, as marked)
-static int mark_elapsed(const xg_plan *p, int i, bool stamps, const std::vector<unsigned long long> &gs, double *sec)
+// the run's step marks, after it: gs[i + 1] = boundary i's stamp, gs[0] the start's
+static int read_marks(const xg_plan *p, std::vector<unsigned long long> &gs)
 {
-    if (stamps) {
-        *sec = (double)(gs[i + 1] - gs[0]) / p->ctx->wall_hz;
-        return XG_OK;
-    }
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, p->ev0, p->ev[i]));
-    *sec = ms * 1e-3;
+    gs.resize((size_t)p->nsteps + 1);
+    HIPCHK(hipMemcpy(gs.data(), p->d_gstamp, 8 * gs.size(), hipMemcpyDeviceToHost));
     return XG_OK;
+}
+
+// seconds from the run's start to boundary i
+static double mark_elapsed(const xg_plan *p, int i, const std::vector<unsigned long long> &gs)
+{
+    return (double)(gs[i + 1] - gs[0]) / p->ctx->wall_hz;
 }
 
 static uint64_t next_plan_id()
@@ -482,7 +476,7 @@ static int init_ctx(xg_ctx *c, const void *uid)
                                                             0));
         c->wave_grid = c->cus * (per_cu < 1 ? 1 : per_cu);
     }
-    env = getenv("XG_STEP_CHAIN");           // "0": an event after every step launch
+    env = getenv("XG_STEP_CHAIN");           // "0": a step mark after every step launch
     c->step_chain = !(env && !strcmp(env, "0"));
     // "1": arm single-segment plans (launched before the timed region, started by the host's
     // doorbell ring).  Off by default: the reference's total_time brackets its request posts
@@ -1164,8 +1158,6 @@ static int plan_upload(xg_plan *p, const std::vector<xgk::DCopy> &pieces, DisplS
         HIPCHK(hipMalloc(&p->d_pieces, sizeof(xgk::DCopy) * pieces.size()));
         HIPCHK(hipMemcpy(p->d_pieces, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
     }
-    p->ev.assign(p->nsteps, nullptr);
-    for (auto &e : p->ev) HIPCHK(hipEventCreate(&e));
     p->fork.assign(p->nsteps, nullptr);
     p->join.assign(p->nsteps, nullptr);
     for (int s = 0; s < p->nsteps; ++s)
@@ -1173,8 +1165,7 @@ static int plan_upload(xg_plan *p, const std::vector<xgk::DCopy> &pieces, DisplS
             HIPCHK(hipEventCreateWithFlags(&p->fork[s], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&p->join[s], hipEventDisableTiming));
         }
-    HIPCHK(hipEventCreate(&p->ev0));
-    if (p->ctx->graph) HIPCHK(hipMalloc(&p->d_gstamp, 8 * ((size_t)p->nsteps + 1)));   // 1 or auto
+    HIPCHK(hipMalloc(&p->d_gstamp, 8 * ((size_t)p->nsteps + 1)));
     if ((rc = run_displ_scan(p, ds)) || (rc = build_segments(p, pieces))) return rc;
     return XG_OK;
 }
@@ -1197,10 +1188,10 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     xg_plan *p = new xg_plan();
     p->ctx = c; p->reg = r; p->nsteps = dp->nsteps; p->variant = c->variant; p->streaming = false;
     p->d_pieces = nullptr; p->d_sb = nullptr; p->d_epieces = nullptr; p->d_engine = nullptr; p->d_disp = nullptr;
-    p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0; p->ev0 = nullptr;
+    p->ndisp = 0; p->engine_base = 0; p->engine_reset = false; p->nlaunch = 0;
     p->db = nullptr; p->epoch = 0; p->d_solo = nullptr; p->rec_ev = false; p->stamp_rails = 1; p->d_cstamp = nullptr;
     p->g_enq = p->g_run = nullptr; p->id = next_plan_id(); p->vg.rccl = false; p->vg.exec = nullptr;
-    p->d_gstamp = nullptr; p->stamp_marks = false; p->graph_auto = false; p->local_only = false;
+    p->d_gstamp = nullptr; p->graph_auto = false; p->local_only = false;
     // One piece per workgroup.  Bytes per piece, per launch (launch_chunk over the launch's
     // copies): c->chunk (32 KiB: profiles/r01_copy_ab.txt) or c->chunk / 2, / 4, / 8 (>= 4 KiB;
     // a halving keeps dividing the power-of-two segment sizes: no ragged tail piece per segment,
@@ -1563,10 +1554,8 @@ extern "C" int xg_plan_free(xg_plan *p)
                     (void *)p->d_disp, (void *)p->d_solo, (void *)p->d_cstamp, (void *)p->d_gstamp})
         if (q) keep(hipFree(q));
     if (p->db) keep(hipHostFree((void *)p->db));
-    for (auto &e : p->ev) if (e) keep(hipEventDestroy(e));
     for (auto &e : p->fork) if (e) keep(hipEventDestroy(e));
     for (auto &e : p->join) if (e) keep(hipEventDestroy(e));
-    if (p->ev0) keep(hipEventDestroy(p->ev0));
     for (hipGraphExec_t g : {p->g_enq, p->g_run, p->vg.exec})
         if (g) keep(hipGraphExecDestroy(g));
     delete p;
@@ -2014,9 +2003,7 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
         // captured once: the grid engine's ticket counter restarts from zero in every replay,
         // the step boundaries are stamps (mark)
         p->engine_reset = true;
-        p->stamp_marks = true;
         rc = capture(c->stream, &p->g_run, [&] { return enqueue_run(p, nullptr); });
-        p->stamp_marks = false;
         if (rc) {
             p->engine_reset = true;      // the host's ticket base moved for launches that never ran
             return rc;
@@ -2054,16 +2041,12 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
         cst.resize(p->nsteps);
         HIPCHK(hipMemcpy(cst.data(), p->d_cstamp, 8 * (size_t)p->nsteps, hipMemcpyDeviceToHost));
     }
-    if (graph) {
-        gs.resize((size_t)p->nsteps + 1);
-        HIPCHK(hipMemcpy(gs.data(), p->d_gstamp, 8 * gs.size(), hipMemcpyDeviceToHost));
-    }
+    if ((rc = read_marks(p, gs))) return rc;
     for (int s = 0; s < p->nsteps;) {
         const int gi = p->seg_of[s];
         if (chains && p->chain_end[s]) {
             const int ce = p->chain_end[s];
-            double end;
-            if ((rc = mark_elapsed(p, ce - 1, graph, gs, &end))) return rc;
+            const double end = mark_elapsed(p, ce - 1, gs);
             for (int t = s; t < ce; ++t) {
                 const double x = end - (double)(cst[ce - 1] - cst[t]) / c->wall_hz;
                 step_done[t] = t == ce - 1 ? end : (x > 0 ? x : 0);
@@ -2072,8 +2055,7 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
             continue;
         }
         const int e = gi >= 0 ? p->segs[gi].s1 : s + 1;
-        double end;
-        if ((rc = mark_elapsed(p, e - 1, graph, gs, &end))) return rc;
+        const double end = mark_elapsed(p, e - 1, gs);
         // inside a segment: the wall-clock stamps, anchored at the event after its launch
         // (the last step of a segment is drained, so its stamp is a delivered time)
         for (int t = s; t < e; ++t) {
@@ -2238,15 +2220,10 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
             if (vg.exec) HIPCHK(hipGraphExecDestroy(vg.exec));
             vg.exec = nullptr;
             if ((rc = pair_calls())) return rc;
-            for (int g = 0; g < n; ++g) {
-                plans[g]->engine_reset = true;
-                plans[g]->stamp_marks = true;      // step boundaries as stamps in the graph
-            }
+            for (int g = 0; g < n; ++g) plans[g]->engine_reset = true;
             rc = capture(st, &vg.exec, body);
-            for (int g = 0; g < n; ++g) {
-                plans[g]->stamp_marks = false;
+            for (int g = 0; g < n; ++g)
                 if (rc) plans[g]->engine_reset = true;   // ticket bases moved for launches that never ran
-            }
             if (rc) return rc;
             vg.ids = ids;
             vg.rccl = rccl;
@@ -2262,14 +2239,9 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
     for (int g = 0; g < n; ++g)
         if ((rc = xg_plan_check(plans[g]))) return rc;
     if (step_done) {
-        const bool graph = c0->graph == 1 && !c0->kt_mode;
         std::vector<unsigned long long> gs;
-        if (graph) {
-            gs.resize((size_t)nst + 1);
-            HIPCHK(hipMemcpy(gs.data(), plans[0]->d_gstamp, 8 * gs.size(), hipMemcpyDeviceToHost));
-        }
-        for (int s = 0; s < nst; ++s)
-            if ((rc = mark_elapsed(plans[0], s, graph, gs, &step_done[s]))) return rc;
+        if ((rc = read_marks(plans[0], gs))) return rc;
+        for (int s = 0; s < nst; ++s) step_done[s] = mark_elapsed(plans[0], s, gs);
     }
     return XG_OK;
 }
