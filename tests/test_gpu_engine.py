@@ -358,9 +358,10 @@ def test_engine_segments_in_multi_gpu_plans(xg, method):
 def test_step_chains_time_like_events(xg, method, d):
     """Runs of one-launch local steps (large steps, outside the engine; TAM steps: a stage
     launch and/or a local launch) are timed by in-kernel start stamps of each step's
-    first launch instead of an event after every step (XG_STEP_CHAIN):
-    same delivered bytes as the evented run, step times ordered and inside the run's
-    wall time, and no later than the evented run's by more than noise."""
+    first launch instead of a step mark after every step (XG_STEP_CHAIN; the marks were HIP
+    events until round 4, clock stamps since -- the test keeps its name): same delivered
+    bytes as the run marked step by step, step times ordered and inside the run's wall time,
+    and no later than that run's by more than noise."""
     import xg_oracle as O
     P, A, c = 32, 14, 3
     rl = xg.aggregator_list(P, A)
