@@ -154,6 +154,11 @@ int xg_vplans_run_rccl(xg_plan *const *plans, int n, double *step_done);
  * keep the poison) -- so one GPU's share of a job too large to emulate whole on one device
  * executes at full size.  XG_EARG for a non-virtual context or a plan with self calls. */
 int xg_plan_set_local_only(xg_plan *p, int on);
+/* Mark only the steps whose completion time a Timer reads (need: xg_sched_timed_steps of the
+ * plan's schedule; NULL = every step, the default; the last step is always marked).  An unmarked
+ * step costs no clock stamp in xg_plan_run and is reported as done when the next marked step is.
+ * Engine segments and chains are marked at their last step regardless. */
+int xg_plan_set_step_marks(xg_plan *p, const uint8_t *need);
 /* Kernel timing session.  mode 1: every copy / engine launch of any plan on this
  * context is bracketed by HIP events on the stream it runs on (at most
  * max_launches); mode 2: one event pair on the main stream around the whole

@@ -125,6 +125,10 @@ int xg_sched_rank_timer(xg_sched *s, int ngpus, int rank, const double *step_don
 int xg_sched_rank_rep_timers(xg_sched *s, int ngpus, int rank, const double *step_done,
                              const double *step_post, xg_timer *reps);
 int xg_sched_ntimes(const xg_sched *s);
+/* The steps whose completion time some rank's Timer reads (need[nsteps]: 1 = read; the last
+ * step always is).  Every other step may be timed as the next read step without changing any
+ * Timer field (a run then marks only these: xg_plan_set_step_marks).  -> how many. */
+int xg_sched_timed_steps(const xg_sched *s, uint8_t *need);
 /* step after which the k-th MPI_Barrier of the method completes (-1: before step 0);
  * returns the number of barriers (out may be NULL). */
 int xg_sched_barrier_epochs(const xg_sched *s, int32_t *out);

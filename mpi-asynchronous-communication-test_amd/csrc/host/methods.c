@@ -153,7 +153,18 @@ static int setup(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size
     rc = xg_fill(*reg, runs, nruns, data_size, iter, o->fingerprint);
     free(runs);
     if (rc) return rc;
-    return xg_plan_load(ctx, *reg, *dp, plan);
+    if ((rc = xg_plan_load(ctx, *reg, *dp, plan))) return rc;
+    {   /* a timed run marks only the steps whose completion time a Timer reads */
+        uint8_t *need = (uint8_t *)malloc((size_t)xg_sched_nsteps(*s) + 1);
+        if (!need) {
+            snprintf(err, errlen, "out of host memory");
+            return XG_ENOMEM;
+        }
+        xg_sched_timed_steps(*s, need);
+        rc = xg_plan_set_step_marks(*plan, need);
+        free(need);
+    }
+    return rc;
 }
 
 int xg_run_method(xg_ctx *ctx, int method, int procs, int cb_nodes, int data_size, const int *rank_list,

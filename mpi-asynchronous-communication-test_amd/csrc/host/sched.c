@@ -1662,6 +1662,53 @@ int xg_sched_rank_rep_timers(xg_sched *s, int ngpus, int rank, const double *ste
     return rank_timers(s, ngpus, rank, step_done, step_post, &g, reps);
 }
 
+/* Which step completion times any rank's Timer reads (rank_timers): a rank's logical clock is the
+ * completion time of the latest step among those it has awaited, and step times never decrease
+ * in step order (one stream per GPU), so the clock is step_done[c] for c = the highest awaited
+ * step so far; a bracket (TMARK, MARK, DELTA) reads it there.  need[c] = 1 for every such c, and
+ * for the last step (a run's total); 0 elsewhere.  A step whose time nobody reads needs no mark
+ * in the run: reporting it as the next read step's time changes no Timer field. */
+int xg_sched_timed_steps(const xg_sched *s, uint8_t *need)
+{
+    int r, i, q, n = 0;
+    if (!s || !need) return -1;
+    memset(need, 0, (size_t)s->nsteps);
+    for (r = 0; r < s->P; ++r) {
+        const prog_t *p = &s->progs[r];
+        int c = -1;
+        for (i = 0; i < p->nops; ++i) {
+            const op_t *o = &p->ops[i];
+            int st = -1;
+            switch (o->kind) {
+            case OP_WAIT:
+                for (q = 0; q < o->wcnt; ++q) {
+                    const int post = p->pool[o->wbeg + q];
+                    if (s->post_eager[r][post]) continue;
+                    st = s->msgs[s->post_msg[r][post]].step;
+                    if (st > c) c = st;
+                }
+                break;
+            case OP_BARRIER:
+                st = s->barrier_epoch[o->post];
+                if (st > c) c = st;
+                break;
+            case OP_SYNC:
+                if (o->idx >= 0 && o->idx < s->nsteps && o->idx > c) c = o->idx;
+                break;
+            case OP_TMARK:
+            case OP_MARK:
+            case OP_DELTA:
+                if (c >= 0) need[c] = 1;
+                break;
+            default: break;
+            }
+        }
+    }
+    if (s->nsteps > 0) need[s->nsteps - 1] = 1;
+    for (i = 0; i < s->nsteps; ++i) n += need[i];
+    return n;
+}
+
 int xg_sched_ntimes(const xg_sched *s) { return s->ntimes; }
 
 int xg_sched_barrier_epochs(const xg_sched *s, int32_t *out)

@@ -254,6 +254,8 @@ struct xg_plan {
     // (profiles/r04/stamp_marks/), and captured events are not re-recorded by a graph replay on
     // this stack (tools/graph_probe.hip), so eager runs, graph replays and virtual jobs all stamp
     unsigned long long *d_gstamp;
+    std::vector<char> need_mark;   // per step: an eager or captured run marks it (xg_plan_set_step_marks;
+                                   // default all) -- engine segments and chains mark their last step always
     bool graph_auto;               // XG_GRAPH unset: this plan replays as a graph (latency-bound, one GPU)
     bool local_only;               // test hook (xg_plan_set_local_only): a virtual GPU runs its share alone,
                                    // its RCCL calls and in-loop barriers left out
@@ -1158,6 +1160,7 @@ static int plan_upload(xg_plan *p, const std::vector<xgk::DCopy> &pieces, DisplS
         HIPCHK(hipMalloc(&p->d_pieces, sizeof(xgk::DCopy) * pieces.size()));
         HIPCHK(hipMemcpy(p->d_pieces, pieces.data(), sizeof(xgk::DCopy) * pieces.size(), hipMemcpyHostToDevice));
     }
+    p->need_mark.assign(p->nsteps, 1);
     p->fork.assign(p->nsteps, nullptr);
     p->join.assign(p->nsteps, nullptr);
     for (int s = 0; s < p->nsteps; ++s)
@@ -1713,7 +1716,7 @@ static int enqueue_pre(xg_plan *p, int s, hipStream_t stream, hipStream_t side)
         const int n = pv.post_n + (st.fused_local ? st.local_n : 0) + st.pack_n;
         const int64_t b = pv.post_bytes + (st.fused_local ? st.local_bytes : 0) + st.pack_bytes;
         if ((rc = timed_copy(p, pv.post_b, n, b, stream, true))) return rc;
-        if (p->rec_ev && (rc = mark(p, s - 1, stream))) return rc;
+        if (p->rec_ev && p->need_mark[s - 1] && (rc = mark(p, s - 1, stream))) return rc;
     }
     if (st.split) {
         // the packs feed the RCCL group (the critical path), the local part does not: by default
@@ -1970,7 +1973,7 @@ static int enqueue_run(xg_plan *p, double *step_post)
             return rc;
         }
         // a deferred step's unpacks run in the next step's fused launch, which records its event
-        if ((gi >= 0 || !p->steps[s].deferred) && (rc = mark(p, e - 1, c->stream))) {
+        if ((gi >= 0 || (!p->steps[s].deferred && p->need_mark[s])) && (rc = mark(p, e - 1, c->stream))) {
             p->rec_ev = false;
             return rc;
         }
@@ -2055,8 +2058,13 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
             continue;
         }
         const int e = gi >= 0 ? p->segs[gi].s1 : s + 1;
+        if (gi < 0 && !p->need_mark[s]) {     // not marked: the next marked step's time (below)
+            step_done[s] = -1;
+            s = e;
+            continue;
+        }
         const double end = mark_elapsed(p, e - 1, gs);
-        // inside a segment: the wall-clock stamps, anchored at the event after its launch
+        // inside a segment: the wall-clock stamps, anchored at the mark after its launch
         // (the last step of a segment is drained, so its stamp is a delivered time)
         for (int t = s; t < e; ++t) {
             const double x = end - (double)(st.empty() ? 0 : st[e - 1] - st[t]) / c->wall_hz;
@@ -2064,6 +2072,10 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
         }
         s = e;
     }
+    // an unmarked step is reported as done when the next marked one is: no Timer reads it
+    // (xg_sched_timed_steps), and the last step is always marked
+    for (int s = p->nsteps - 2; s >= 0; --s)
+        if (step_done[s] < 0) step_done[s] = step_done[s + 1];
     return XG_OK;
 }
 
@@ -2073,6 +2085,17 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
 // at its stated size: 256 GiB per GPU) still executes, its local slots verifiable.  Refused
 // (XG_EARG) for a plan whose local copies travel as self send/recv in an RCCL group
 // (XG_SELF_MAX): leaving the group out would drop them.
+extern "C" int xg_plan_set_step_marks(xg_plan *p, const uint8_t *need)
+{
+    if (!p) return XG_EARG;
+    for (int s = 0; s < p->nsteps; ++s) p->need_mark[s] = !need || need[s] || s == p->nsteps - 1;
+    if (p->g_run) {                  // a captured run holds the old marks: capture again at next use
+        HIPCHK(hipGraphExecDestroy(p->g_run));
+        p->g_run = nullptr;
+    }
+    return XG_OK;
+}
+
 extern "C" int xg_plan_set_local_only(xg_plan *p, int on)
 {
     if (!p || !p->ctx->virt) return XG_EARG;

@@ -137,6 +137,7 @@ def host():
         h.xg_sched_rank_rep_timers.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
                                                C.POINTER(C.c_double), C.POINTER(Timer)]
         h.xg_sched_ntimes.argtypes = [C.c_void_p]
+        h.xg_sched_timed_steps.argtypes = [C.c_void_p, C.POINTER(C.c_uint8)]
         h.xg_sched_barrier_epochs.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
         h.xg_save_all_timing.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(Timer), C.c_char_p]
         h.xg_block_range.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -339,6 +340,14 @@ class Schedule:
         host().xg_sched_trace(self._h, rank, buf, n + 1)
         return buf.value.decode()
 
+    def timed_steps(self):
+        """per step 1 if some rank's Timer reads its completion time (the last step always),
+        else 0 -- the steps a timed run must mark (xg_sched_timed_steps)"""
+        need = (C.c_uint8 * max(1, self.nsteps))()
+        if host().xg_sched_timed_steps(self._h, need) < 0:
+            raise XGError("xg_sched_timed_steps failed")
+        return list(need)[:self.nsteps]
+
     def rank_timer(self, rank, step_done, step_post=None, ngpus=1):
         nd = (C.c_double * max(1, len(step_done)))(*step_done)
         npost = (C.c_double * max(1, len(step_post)))(*step_post) if step_post is not None else None
@@ -515,6 +524,7 @@ def device():
         d.xg_vplans_run.argtypes = [C.POINTER(vp), ip, C.POINTER(C.c_double)]
         d.xg_vplans_run_rccl.argtypes = [C.POINTER(vp), ip, C.POINTER(C.c_double)]
         d.xg_plan_set_local_only.argtypes = [vp, ip]
+        d.xg_plan_set_step_marks.argtypes = [vp, C.POINTER(C.c_uint8)]
         d.xg_self_max.restype = i64
         d.xg_self_max.argtypes = [vp]
         d.xg_barrier.argtypes = [vp]
@@ -718,6 +728,7 @@ class MethodRun:
         self._p = C.c_void_p()
         _check(d.xg_plan_load(ctx.handle, self._r, self.view.ptr, C.byref(self._p)), "xg_plan_load")
         self.nsteps = d.xg_plan_nsteps(self._p)
+        self.set_step_marks(sched.timed_steps())       # as xg_run_method: only the steps a Timer reads
         self.engine_workgroups = d.xg_plan_engine(self._p)   # 0: one launch per step
         self.engine_rails = d.xg_plan_engine_rails(self._p)  # > 0: a solo segment on that many rails
 
@@ -760,6 +771,12 @@ class MethodRun:
 
     def poison(self):
         _check(_dev.xg_regions_poison(self._r), "xg_regions_poison")
+
+    def set_step_marks(self, need=None):
+        """mark only the steps with need[s] set in a timed run (None: every step), the others
+        reported as done with the next marked one (xg_plan_set_step_marks)"""
+        arr = (C.c_uint8 * max(1, self.nsteps))(*need) if need is not None else None
+        _check(_dev.xg_plan_set_step_marks(self._p, arr), "xg_plan_set_step_marks")
 
     def set_local_only(self, on=True):
         """test hook (virtual GPU): run this GPU's share alone -- copy launches only, its RCCL

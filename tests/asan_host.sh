@@ -12,5 +12,5 @@ gcc -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-re
     "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/calls.c" "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/pieces.c"
 cd "$REPO/tests"
 LD_PRELOAD="$(gcc -print-file-name=libasan.so) $(gcc -print-file-name=libubsan.so)" ASAN_OPTIONS=detect_leaks=0 \
-    XG_LIBDIR="$OUT" python -m pytest test_host_sched.py test_devplan.py test_oracle.py test_engine_hazards.py test_hbm_fit.py test_solo_tables.py test_rccl_calls.py test_baseline_golden.py -q -s -m "not gpu" -p no:cacheprovider
+    XG_LIBDIR="$OUT" python -m pytest test_host_sched.py test_devplan.py test_oracle.py test_engine_hazards.py test_hbm_fit.py test_solo_tables.py test_rccl_calls.py test_baseline_golden.py test_timed_steps.py -q -s -m "not gpu" -p no:cacheprovider
 rm -rf "$OUT"

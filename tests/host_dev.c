@@ -54,6 +54,7 @@ struct xg_plan {
     xg_regions *r;
     const xg_devplan *dp;
     int64_t self_max;
+    unsigned char *need;   /* xg_plan_set_step_marks: NULL = every step marked */
 };
 
 double xg_now(void)
@@ -327,6 +328,7 @@ int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_plan **out)
 
 int xg_plan_free(xg_plan *p)
 {
+    if (p) free(p->need);
     free(p);
     return XG_OK;
 }
@@ -364,6 +366,19 @@ static int recv_msg(xg_ctx *c, int peer, unsigned char *dst, int64_t len)
     return XG_OK;
 }
 
+int xg_plan_set_step_marks(xg_plan *p, const uint8_t *need)
+{
+    int s;
+    if (!p) return XG_EARG;
+    free(p->need);
+    p->need = NULL;
+    if (!need) return XG_OK;
+    p->need = (unsigned char *)malloc((size_t)p->dp->nsteps + 1);
+    if (!p->need) return XG_ENOMEM;
+    for (s = 0; s < p->dp->nsteps; ++s) p->need[s] = need[s] || s == p->dp->nsteps - 1;
+    return XG_OK;
+}
+
 int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
 {
     xg_ctx *c = p->ctx;
@@ -398,6 +413,10 @@ int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
         if (step_done) step_done[s] = xg_now() - t0;
     }
     free(calls);
+    /* as the device runtime: an unmarked step is reported as done with the next marked one */
+    if (step_done && p->need && !rc)
+        for (s = dp->nsteps - 2; s >= 0; --s)
+            if (!p->need[s]) step_done[s] = step_done[s + 1];
     if (wall) *wall = xg_now() - t0;
     return rc;
 }
