@@ -425,12 +425,15 @@ def spawn_ranks(a):
     lines = [line for line in outs[0] if line.startswith("{")]
     if rc or not lines:
         sys.stderr.write("bench: %d-GPU job failed (child exit codes %s)\n" % (a.gpus, rcs))
+    if not lines:
         return rc or 1
-    out = json.loads(lines[-1])
+    out = json.loads(lines[-1])           # rank 0's line -- a failed job's too (value null + error)
     out["cpu_baseline"] = cpu
     out["launch"] = "bench.py parent: %d child processes (subprocess), one per GPU" % a.gpus
+    if rc:
+        out["child_exit_codes"] = rcs
     print(json.dumps(out))
-    return 0
+    return rc
 
 
 def child_stub():
@@ -536,12 +539,22 @@ def main():
     import __graft_entry__ as G
     xg = G.load_package().xg
     uid, rdzv = (None, None)
-    if world > 1:
-        phase("rendezvous (RCCL id file)")
-        uid, rdzv = rendezvous_uid(xg, rank, world)
     dev = int(os.environ.get("XG_DEVICE", local))   # XG_DEVICE: test hook (several ranks on one GPU)
-    phase("RCCL communicator init (ncclCommInitRank, %d ranks)" % world)
-    ctx = xg.Context(rank=rank, nranks=world, device=dev, uid=uid)
+    try:
+        if world > 1:
+            phase("rendezvous (RCCL id file)")
+            uid, rdzv = rendezvous_uid(xg, rank, world)
+        phase("RCCL communicator init (ncclCommInitRank, %d ranks)" % world)
+        ctx = xg.Context(rank=rank, nranks=world, device=dev, uid=uid)
+    except xg.XGError as e:
+        # no communicator, so nothing to agree over: each rank reports for itself, rank 0 the line
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world,
+                              "higher_is_better": True, "dtype": "u8",
+                              "error": "device / RCCL init failed on rank 0 (%s): %s" % (PHASE[0], e),
+                              "cpu_baseline": cpu}), flush=True)
+        sys.stderr.write("bench: rank %d: %s\n" % (rank, e))
+        return 1
     ctx.barrier()
     if rdzv:
         os.unlink(rdzv)

@@ -49,6 +49,8 @@ def make(real_xg):
     class Context:
         def __init__(self, rank=0, nranks=1, device=None, uid=None, device_index=None):
             assert nranks == 1 or (uid is not None and len(uid) == 128)
+            if os.environ.get("XG_FAKE_INIT_FAIL") == "1":     # e.g. RCCL's "Duplicate GPU detected"
+                raise real_xg.XGError("xg_init failed with code 2 (injected)")
             self.rank, self.nranks = rank, nranks
             self._kt = None
             self._nbar = 0

@@ -255,3 +255,15 @@ def test_watchdog_on_rank0_prints_a_line_naming_the_phase(tmp_path):
     assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
     assert out["value"] is None and out["error"].startswith("rank 0 still in phase 'RCCL communicator init")
+
+
+def test_failed_communicator_init_still_prints_a_line(tmp_path):
+    """RCCL refuses the communicator on every rank (as it does for two ranks on one GPU,
+    profiles/r04/two_ranks/): no rank hangs, rank 0 prints a line with value null naming the
+    failure, and the job exits 1"""
+    rcs, outs = _run_job(2, ARGV2, tmp_path, {"XG_FAKE_INIT_FAIL": "1"})
+    assert rcs == [1, 1], [o[1][-1500:] for o in outs]
+    lines = [l for l in outs[0][0].splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and not [l for l in outs[1][0].splitlines() if l.startswith("{")]
+    out = json.loads(lines[0])
+    assert out["value"] is None and out["error"].startswith("device / RCCL init failed on rank 0 (RCCL communicator init")

@@ -52,6 +52,8 @@ def test_failed_rank_stops_the_job():
     assert p.returncode != 0
     assert time.time() - t0 < 200
     assert "failed" in p.stderr
+    out = json.loads(p.stdout.strip().splitlines()[-1])     # rank 0's line, passed on by the parent
+    assert out["value"] is None and "init failed" in out["error"] and out["child_exit_codes"]
 
 
 TEST_BIN = os.path.join(REPO, "mpi-asynchronous-communication-test_amd", "bin", "test")
