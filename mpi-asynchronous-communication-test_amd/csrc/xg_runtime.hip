@@ -2089,10 +2089,11 @@ extern "C" int xg_plan_set_step_marks(xg_plan *p, const uint8_t *need)
 {
     if (!p) return XG_EARG;
     for (int s = 0; s < p->nsteps; ++s) p->need_mark[s] = !need || need[s] || s == p->nsteps - 1;
-    if (p->g_run) {                  // a captured run holds the old marks: capture again at next use
-        HIPCHK(hipGraphExecDestroy(p->g_run));
-        p->g_run = nullptr;
-    }
+    for (hipGraphExec_t *g : {&p->g_run, &p->vg.exec})   // captured runs hold the old marks: capture again
+        if (*g) {
+            HIPCHK(hipGraphExecDestroy(*g));
+            *g = nullptr;
+        }
     return XG_OK;
 }
 
@@ -2230,7 +2231,7 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
                 if (plans[g]->seg_of[s] < 0 && (rc = enqueue_post(plans[g], s, st))) return rc;
             if (rccl && plans[0]->steps[s].sync_after)
                 NCCLCHK(ncclAllReduce(c0->d_red, c0->d_red, 1, ncclFloat64, ncclMax, c0->comm, st));
-            if ((rc = mark(plans[0], s, st))) return rc;
+            if (plans[0]->need_mark[s] && (rc = mark(plans[0], s, st))) return rc;   // the job's marks: GPU 0's
         }
         return XG_OK;
     };
@@ -2264,7 +2265,8 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
     if (step_done) {
         std::vector<unsigned long long> gs;
         if ((rc = read_marks(plans[0], gs))) return rc;
-        for (int s = 0; s < nst; ++s) step_done[s] = mark_elapsed(plans[0], s, gs);
+        for (int s = nst - 1; s >= 0; --s)      // an unmarked step: done with the next marked one
+            step_done[s] = plans[0]->need_mark[s] ? mark_elapsed(plans[0], s, gs) : step_done[s + 1];
     }
     return XG_OK;
 }
