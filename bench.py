@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--xgmi-budget", type=float, default=120.0,
                     help="N > 1: seconds the xGMI ceiling + sweep phase may take before the line is printed "
                          "without the rest of it")
-    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 900)),
+    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 420)),
                     help="rank process: seconds before a rank that is still running reports the phase it is "
                          "stuck in and exits 124 (0: off) -- a lost peer leaves RCCL waiting forever")
     return ap.parse_args()

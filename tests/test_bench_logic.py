@@ -227,7 +227,7 @@ def test_bench_line_survives_a_hang_in_the_xgmi_phase(tmp_path):
     """the line's value is measured, then one GPU never returns from the sweep's second call (a
     peer lost inside RCCL): after --xgmi-budget seconds rank 0 prints the line as measured -- the
     value, the ceiling, the sweep rows so far -- with xgmi_error naming the phase, and every rank
-    ends (exit 0) instead of waiting for the 900 s watchdog"""
+    ends (exit 0) instead of waiting for the 420 s watchdog"""
     argv = ARGV2 + ["--xgmi-budget", "8", "--no-ktime"]
     t0 = time.time()
     rcs, outs = _run_job(2, argv, tmp_path, {"XG_FAKE_P2P_HANG": "2", "XG_FAKE_FAIL_RANK": "1"})
