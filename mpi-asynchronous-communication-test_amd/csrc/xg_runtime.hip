@@ -379,8 +379,32 @@ struct StdoutToStderr {
     }
 };
 
+// XG_SHARE_GPU=1 (test harness): several ranks of one job on ONE GPU, each its own process
+// (a one-GPU box running the multi-rank path).  RCCL refuses two ranks with the same bus id on
+// one host ("Duplicate GPU detected"), so every rank names a host of its own (NCCL_HOSTID):
+// the ranks then pair over RCCL's network transport (sockets on loopback) instead of xGMI.
+// The calls, groups, pairing and collectives are the real multi-rank ones; the transport and
+// its rates are not the node's.  Called before the first RCCL call of the process.
+static void share_gpu_env(int rank)
+{
+    const char *v = getenv("XG_SHARE_GPU");
+    if (!v || strcmp(v, "1")) return;
+    char id[64];
+    snprintf(id, sizeof id, "xg-share-gpu-rank-%d", rank);
+    setenv("NCCL_HOSTID", id, 1);
+    setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+}
+
+static int env_rank()
+{
+    const char *v = getenv("RANK");
+    if (!v) v = getenv("PMI_RANK");
+    return v ? atoi(v) : 0;
+}
+
 extern "C" int xg_get_unique_id(void *uid)
 {
+    share_gpu_env(env_rank());
     rccl_log_to_stderr();
     StdoutToStderr quiet;
     ncclUniqueId id;
@@ -515,6 +539,7 @@ static int init_ctx(xg_ctx *c, const void *uid)
         ncclUniqueId id;
         if (!uid) return XG_EARG;
         memcpy(&id, uid, sizeof id);
+        share_gpu_env(rank);
         StdoutToStderr quiet;
         NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
     } else if (getenv("XG_SELF_COMM") && atoi(getenv("XG_SELF_COMM"))) {
