@@ -5,7 +5,7 @@
  * ncclGroupStart/End around its send/recv calls (in this order; with self_max > 0
  * a cross-GPU step's small local part joins them as self send/recv pairs), then
  * one ncclAllReduce when the step ends in an in-loop MPI_Barrier.  The real
- * multi-GPU path of the runtime (xg_runtime.hip, enqueue_step) posts exactly
+ * multi-GPU path of the runtime (runtime/exec.hip, enqueue_step) posts exactly
  * that list; the one-device virtual runner (xg_vplans_run / _rccl) moves exactly
  * the pairs xg_calls_match makes of every GPU's lists.
  *

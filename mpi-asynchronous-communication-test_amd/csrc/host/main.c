@@ -172,11 +172,8 @@ int main(int argc, char **argv)
     device = xg_env_int("LOCAL_RANK", "MPI_LOCALRANKID", rank);
     procs = xg_env_int("XG_PROCS", NULL, 0);
     verify = xg_env_int("XG_VERIFY", NULL, 0);
-    if (getenv("XG_FINGERPRINT") && !strcmp(getenv("XG_FINGERPRINT"), "strong")) fp_mode = XG_FP_STRONG;
-    if (getenv("XG_EAGER_LIMIT")) eager = atoll(getenv("XG_EAGER_LIMIT"));
-    if (getenv("XG_PACK_MAX_SEG")) pack_max = atoll(getenv("XG_PACK_MAX_SEG"));
-    if (getenv("XG_PACK_MIN")) pack_min = atoll(getenv("XG_PACK_MIN"));
-    pack_form = xg_env_int("XG_PACK_FORM", NULL, pack_form);
+    /* --fingerprint, --eager-limit, --pack-max-seg, --pack-min and --pack-form are options
+     * only (their XG_* environment twins were folded in round 5) */
 
     while ((i = getopt_long(argc, argv, "hp:c:m:d:a:i:k:t:r:b:", longopts, NULL)) != EOF) {
         switch (i) {
@@ -224,8 +221,7 @@ int main(int argc, char **argv)
         /* every process plans every GPU's RCCL calls from its own command line: processes
          * started with different ones would post calls nobody pairs and hang -- compare a
          * digest (FNV-1a of argv and the planning settings, in 16-bit parts) first */
-        static const char *keys[] = {"XG_PROCS", "XG_VERIFY", "XG_FINGERPRINT", "XG_EAGER_LIMIT", "XG_PACK_MAX_SEG",
-                                     "XG_PACK_MIN", "XG_PACK_FORM", "XG_SELF_MAX", NULL};
+        static const char *keys[] = {"XG_PROCS", "XG_VERIFY", "XG_SELF_MAX", NULL};
         uint64_t h = 0xcbf29ce484222325ull;
         double red[8];
         int k;

@@ -47,7 +47,7 @@ static int ival_cmp(const void *x, const void *y)
 
 /* Step s's local copies (after its stage copies, before its packs) against the bytes step
  * s-1's unpacks write: 1 if any of them reads or writes such a byte -- then they cannot share
- * one launch, whose workgroups run in any order (xg_runtime.hip fuses them otherwise).
+ * one launch, whose workgroups run in any order (runtime/plan_load.hip fuses them otherwise).
  * Returns -1 for a bad step. */
 int xg_step_local_meets_unpacks(const xg_devplan *dp, int s)
 {

@@ -91,7 +91,9 @@ __device__ __forceinline__ uint64_t expect_word(int mode, uint32_t b0, uint64_t 
 }
 
 // ---------------------------------------------------------------- fill
-__global__ __launch_bounds__(kThreads) void fill_kernel(uint8_t *__restrict__ base, const DSeg *__restrict__ segs,
+// The non-template kernels are static: every runtime translation unit that includes this header
+// gets its own copy (no duplicate host stubs at link time); templates are merged by the linker.
+[[maybe_unused]] static __global__ __launch_bounds__(kThreads) void fill_kernel(uint8_t *__restrict__ base, const DSeg *__restrict__ segs,
                                                         int chunks_per_seg, int64_t d, int64_t chunk, int iter,
                                                         int mode)
 {
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(kThreads) void copy_kernel_w(const DCopy *__restric
 }
 
 // the wall clock after everything before it on the stream: closes a chain of step launches
-__global__ void clock_kernel(unsigned long long *t)
+[[maybe_unused]] static __global__ void clock_kernel(unsigned long long *t)
 {
     if (threadIdx.x == 0) *t = (unsigned long long)wall_clock64();
 }
@@ -875,7 +877,7 @@ __global__ __launch_bounds__(WV * 64) void solo_engine_kernel(const unsigned lon
 // one step = exclusive prefix sum of their lengths.  One workgroup per group
 // (a step's pack list or unpack list, groups[g] .. groups[g+1]): wave64 inclusive
 // scan with shuffles, wave totals through LDS, a carry across 256-entry tiles.  disp[i] = base + sum of len[j] for j < i inside the group.
-__global__ __launch_bounds__(kThreads) void displ_scan_kernel(const int64_t *__restrict__ len,
+[[maybe_unused]] static __global__ __launch_bounds__(kThreads) void displ_scan_kernel(const int64_t *__restrict__ len,
                                                               const int *__restrict__ groups,
                                                               const int64_t *__restrict__ group_base,
                                                               int64_t *__restrict__ disp)
@@ -917,7 +919,7 @@ struct DFix {
     int pad;
 };
 
-__global__ __launch_bounds__(kThreads) void displ_apply_kernel(DCopy *__restrict__ pieces, const DFix *__restrict__ fix,
+[[maybe_unused]] static __global__ __launch_bounds__(kThreads) void displ_apply_kernel(DCopy *__restrict__ pieces, const DFix *__restrict__ fix,
                                                                int nfix, const int64_t *__restrict__ disp,
                                                                uint8_t *stage_send, uint8_t *stage_recv)
 {
@@ -948,7 +950,7 @@ __device__ __forceinline__ uint64_t wave_min(uint64_t v)
 
 // grid: slots x chunks; each lane hashes 8-byte words.  chk excludes the
 // length term (added on the host); first_bad = UINT64_MAX when clean.
-__global__ __launch_bounds__(kThreads) void verify_kernel(const uint8_t *__restrict__ base,
+[[maybe_unused]] static __global__ __launch_bounds__(kThreads) void verify_kernel(const uint8_t *__restrict__ base,
                                                           const DSlot *__restrict__ slots, int chunks_per_slot,
                                                           int64_t d, int64_t chunk, int iter, int mode,
                                                           unsigned long long *chk, unsigned long long *bad,

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # Piece size per launch (XG_COPY_BALANCE): the configs[2] 8-GPU pack / unpack / gather classes
 # on one MI355X (virtual GPUs) and the bench line, with the balanced rule (1) and with 32 KiB
 # pieces everywhere (0); rocprofv3 kernel traces, per class.

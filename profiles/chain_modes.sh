@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # README configuration (configs[0]) through the drop-in CLI under the step-engine modes,
 # interleaved, plus the reference under MPICH on the same box: max total time per method.
 #   launch      default: engine segments launched inside the timed region (like-for-like with

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # Bench copy launches per method by piece size (XG_COPY_CHUNK; pieces in destination order),
 # rocprofv3 kernel traces.  usage: profiles/chunk_ab.sh <outdir>
 out=${1:-gpurun_out/chunk_ab}; mkdir -p $out

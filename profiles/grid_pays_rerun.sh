@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # grid_pays used solo_max (1 GiB since a9cb48e) as "larger than the 256 MiB
 # Infinity Cache", so engine runs of 256 MiB .. 1 GiB that do not go solo always took the grid
 # engine.  Round 3 gives the cache its own constant (XG_GRID_CACHE_MAX, 256 MiB).  Re-run: a

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # One-step GPU-local plans (m5 / m8 alltoallw, m1 / m2 with -c >= P) at README size: a copy launch
 # timed by events (XG_SOLO_MIN_STEPS=2, default) vs an armed solo launch (XG_SOLO_MIN_STEPS=1),
 # interleaved, through the CLI.  usage: profiles/one_step_ab.sh <outdir>

@@ -1,4 +1,6 @@
 #!/usr/bin/env python3
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 """HBM traffic per copy_kernel launch class of profiles/pack_virtual.py from two rocprofv3
 --pmc passes (FETCH_SIZE, WRITE_SIZE in separate runs), grouped by grid size (a launch of W
 workgroups moves W * 32 KiB).  gfx950 correction (MI355X_MICROARCH.md, HBM): read bytes =

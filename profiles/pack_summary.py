@@ -1,4 +1,6 @@
 #!/usr/bin/env python3
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 """Reduce a rocprofv3 kernel trace of profiles/pack_virtual.py to copy-kernel HBM GB/s per
 launch size class.  Every transfer there is a whole number of 32 KiB pieces (256 KiB
 segments), one workgroup per piece, so a launch of W workgroups moves W * 32 KiB and reads +

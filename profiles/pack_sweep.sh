@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # pack/unpack launch rate vs copy piece size and kernel variant (profiles/pack_virtual.py under rocprofv3)
 export TMPDIR=/tmp
 for v in ${VARIANTS:-5 13}; do for ch in ${CHUNKS:-16384 32768 65536}; do

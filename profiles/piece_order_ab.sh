@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # Bench copy launches per method under each local-piece order (XG_PIECE_ORDER 0 message order,
 # 1 by destination, 2 by source), rocprofv3 kernel traces; the contiguous copy ceiling of the
 # same box beside it.  usage: profiles/piece_order_ab.sh <outdir>

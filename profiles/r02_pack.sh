@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # Round 2: pack / unpack / local-gather launches of the 8-GPU configs[2] plans on one MI355X
 # (virtual GPUs): kernel trace with the local gather on the side stream (default) and fused
 # into the pack launch (XG_SPLIT_LOCAL=0), then PMC traffic per launch class (separate passes).

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # Round 3, call L: the wave-persistent copy (copy_kernel_w) A/B.  (1) one GPU's configs[2] pack
 # launch standalone (28 MiB out of its own 32 MiB: cache-resident as on a real 8-GPU node), both
 # pack orders, product copy_kernel_g<4> 16 KiB vs copy_kernel_w<8> 8 KiB, interleaved 3 times;

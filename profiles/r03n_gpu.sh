@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # Round 3, call N: the product's cross-GPU copy launches as one real GPU runs them -- GPU 0's share
 # of the configs[2] 8-GPU plans alone (profiles/share_launches.py), rocprofv3 kernel traces reduced
 # per launch class, the wave copy on / off, two-sided and one-sided.

@@ -1,3 +1,5 @@
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 """Per-step completion times of the README-config chains under the engine modes
 (step_done from the in-kernel wall-clock stamps, anchored at the run's end):
 where a run's time goes -- doorbell in, per step, tail."""

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL RECIPE: it sets XG_* knobs folded into constants by commit 88b890f (round 4);
+# rerun now, those arms are identical (libxg warns about each such variable).  Kept as the record.
 # One-off GPU-local launches larger than the step engine's 16 MiB steps and below the 128 MiB
 # non-temporal switch: m1 / m2 at P32 A14, one launch of 448 x d per -k repetition, d = 64 KiB
 # .. 256 KiB (28 .. 112 MiB per launch; regions 56 .. 224 MiB, so the -k repetitions stay in the

@@ -109,7 +109,7 @@ def test_corrupted_message_is_reported(exes, tmp_path):
 
 @pytest.mark.parametrize("differ", ["argv", "env", "self_max"])
 def test_processes_started_differently_refuse(exes, tmp_path, differ):
-    """ranks launched by hand (RANK / WORLD_SIZE) with another -d, XG_PACK_MIN or XG_SELF_MAX (which
+    """ranks launched by hand (RANK / WORLD_SIZE) with another -d, XG_VERIFY or XG_SELF_MAX (which
     changes the calls a rank posts): both stop before any exchange instead of posting calls nobody
     pairs"""
     procs = []
@@ -117,7 +117,7 @@ def test_processes_started_differently_refuse(exes, tmp_path, differ):
         d = 4000 if differ == "argv" and r == 1 else 3000
         env = _env(tmp_path, RANK=r, WORLD_SIZE=2, LOCAL_RANK=r, XG_RDZV_KEY="differ")
         if differ == "env" and r == 1:
-            env["XG_PACK_MIN"] = "0"
+            env["XG_VERIFY"] = "1"
         if differ == "self_max" and r == 1:
             env["XG_SELF_MAX"] = "0"
         (tmp_path / "cwd").mkdir(exist_ok=True)

@@ -1,5 +1,5 @@
 """Copy launches cut into back-to-back dispatches (XG_COPY_LAUNCH_MAX, launch_cuts in
-xg_runtime.hip).  By default only launches above 768 MiB are cut, which no ordinary test
+runtime/exec.hip).  By default only launches above 768 MiB are cut, which no ordinary test
 plan reaches; here the cap is 64 KiB, so every launch of these plans is cut: local
 gather/scatter launches, chained launches whose first dispatch stamps the previous step's
 completion, and the fused unpack + pack launches of a packed multi-GPU plan.  Every
