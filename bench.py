@@ -79,40 +79,110 @@ def parse():
                     help="N > 1: seconds the xGMI ceiling + sweep phase may take before the line is printed "
                          "without the rest of it")
     ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 420)),
-                    help="rank process: seconds before a rank that is still running reports the phase it is "
-                         "stuck in and exits 124 (0: off) -- a lost peer leaves RCCL waiting forever")
+                    help="rank process: seconds from the communicator init to the measured value before a rank "
+                         "that is still running reports the phase it is stuck in and exits 124 (0: off) -- a lost "
+                         "peer leaves RCCL waiting forever; the phases after the value have guards of their own")
+    ap.add_argument("--cpu-budget", type=float, default=120.0,
+                    help="seconds the reference's configs[1] run under mpiexec may take in all")
+    ap.add_argument("--cpu-configs", choices=("auto", "on", "off"), default="auto",
+                    help="run the reference under mpiexec at BASELINE.json's 8-GPU configurations (configs[2] at "
+                         "full size, configs[3] at -d 64 KiB, configs[4] at -d 4 KiB for -c 1 and 8) before the "
+                         "GPUs start (auto: when the job has 8 GPUs)")
+    ap.add_argument("--cpu-configs-budget", type=float, default=150.0,
+                    help="seconds those reference cells may take in all; a cell past it is recorded as skipped")
     return ap.parse_args()
 
 
 # ---------------------------------------------------------------- watchdog (rank processes)
 PHASE = ["start"]
+PHASE_LOG = []          # (phase, monotonic start) in order: phase_wall_s in the N > 1 line
 
 
 def phase(name):
     PHASE[0] = name
+    PHASE_LOG.append((name, time.monotonic()))
 
 
-def start_watchdog(seconds, rank):
-    """A rank whose peers died (or never came) waits in RCCL with no timeout of its own:
-    after `seconds` this thread names the phase the rank is in and ends the process
-    (os._exit: no exec, nothing else runs in its place)."""
-    if seconds <= 0:
-        return
+def phase_walls():
+    """seconds spent in each phase so far (a phase entered several times: summed)"""
+    out = {}
+    marks = PHASE_LOG + [("", time.monotonic())]
+    for (name, t0), (_n, t1) in zip(marks, marks[1:]):
+        key = re.sub(r"^method \d+: ", "methods: ", name)
+        key = re.sub(r"^BASELINE configs: .*", "BASELINE configs", key)
+        out[key] = round(out.get(key, 0.0) + (t1 - t0), 2)
+    return out
 
-    def fire():
+
+class Watchdog:
+    """A rank whose peers died (or never came) waits in RCCL with no timeout of its own: once armed,
+    after `seconds` it names the phase the rank is in and ends the process (os._exit: no exec,
+    nothing else runs in its place).  It guards the road to the measured value only: main() re-arms
+    it at the communicator init and cancels it once `value` is known -- every phase after that has
+    a LineGuard of its own, which prints the measured line instead of a null one."""
+
+    def __init__(self, rank):
+        self.rank, self.timer, self.seconds = rank, None, 0
+
+    def _fire(self):
         try:
-            sys.stderr.write("bench: rank %d still in phase '%s' after %.0f s; exiting\n" % (rank, PHASE[0], seconds))
+            sys.stderr.write("bench: rank %d still in phase '%s' after %.0f s; exiting\n"
+                             % (self.rank, PHASE[0], self.seconds))
             sys.stderr.flush()
-            if rank == 0:     # no value was measured (phases after it have guards of their own): say where it stopped
-                print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "higher_is_better": True,
-                                  "error": "rank 0 still in phase '%s' after %.0f s" % (PHASE[0], seconds)}),
-                      flush=True)
+            if self.rank == 0:     # no value was measured: say where it stopped
+                line = {"metric": METRIC, "value": None, "unit": "GB/s", "higher_is_better": True,
+                        "error": "rank 0 still in phase '%s' after %.0f s" % (PHASE[0], self.seconds)}
+                tails = rccl_log_tails()
+                if tails:
+                    line["rccl_log_tail"] = tails
+                print(json.dumps(line), flush=True)
         finally:
             os._exit(124)
 
-    t = threading.Timer(seconds, fire)
-    t.daemon = True
-    t.start()
+    def arm(self, seconds):
+        self.cancel()
+        self.seconds = seconds
+        if seconds > 0:
+            self.timer = threading.Timer(seconds, self._fire)
+            self.timer.daemon = True
+            self.timer.start()
+
+    def cancel(self):
+        if self.timer:
+            self.timer.cancel()
+            self.timer = None
+
+
+def start_watchdog(seconds, rank):
+    """a Watchdog armed for `seconds` (0: off)"""
+    w = Watchdog(rank)
+    w.arm(seconds)
+    return w
+
+
+GUARD_GRACE = 45.0      # a LineGuard fires this long after its phase's own budget
+
+
+def pre_value_allowance(a, rank, world, parent):
+    """seconds a rank may legitimately wait before its communicator exists: under a launcher (no
+    parent process) rank 0 runs the reference's CPU phases first and writes the RCCL id only after
+    them, so every rank allows their budgets"""
+    if parent or a.no_cpu_baseline or world == 1:
+        return 0.0
+    return a.cpu_budget + (a.cpu_configs_budget + GUARD_GRACE if cpu_configs_on(a, world) else 0.0)
+
+
+def wall_bound(a, world, parent=False):
+    """the longest a rank process can run (seconds) with every phase at its budget and every guard
+    firing: pre-communicator CPU phases, the watchdog up to the value, then the LineGuarded xGMI and
+    BASELINE-configs phases -- INTEGRATION.md states this bound for the driver's 8-GPU run"""
+    pre = pre_value_allowance(a, 0, world, parent) if not parent else 0.0
+    post = 0.0
+    if world > 1:
+        post += a.xgmi_budget
+    if a.baseline_configs == "on" or (a.baseline_configs == "auto" and world == 8):
+        post += a.baseline_budget + GUARD_GRACE
+    return pre + a.watchdog + post
 
 
 def dumps_live(out):
@@ -141,6 +211,7 @@ class LineGuard:
             self.note("still in phase '%s' %.0f s after it started; line printed from what was measured"
                       % (PHASE[0], self.seconds))
             if self.rank == 0:
+                finish_line(self.out, self.out.get("n_gpus") or 2)
                 print(dumps_live(self.out), flush=True)
         finally:                 # whatever happened above, the process ends
             os._exit(0)
@@ -183,30 +254,51 @@ def host_cpus():
     return n, how
 
 
-def cpu_baseline(a, methods):
-    """The reference ./test (oracle/_ref/test, built from /root/reference by oracle/Makefile)
-    under MPICH on this box's host cores, same P/A/d/methods, bounded -k."""
+def run_reference(args, timeout):
+    """one mpiexec of the reference ./test (oracle/_ref/test) in a session of its own, so a run past
+    `timeout` ends with every one of its processes (its exact process group) -- busy-polling MPI
+    ranks left behind would share the host with everything after.  -> (max total time or None,
+    wall seconds, error text)"""
+    import signal
     ref = os.path.join(REPO, "oracle", "_ref", "test")
     mpiexec = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
     if not (os.path.exists(ref) and os.path.exists(mpiexec)):
+        return None, 0.0, "no reference build (oracle/_ref/test) or mpiexec on this host"
+    t0 = time.time()
+    p = subprocess.Popen([mpiexec, "-launcher", "fork"] + args[:2] + [ref] + args[2:], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True, cwd="/tmp", start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=max(1.0, timeout))
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        return None, time.time() - t0, "over budget: stopped after %.0f s" % (time.time() - t0)
+    mt = re.findall(r"max total time = ([0-9.]+)", out)
+    if p.returncode != 0 or not mt:
+        return None, time.time() - t0, "reference run failed (exit %d): %s" % (p.returncode, err[-200:])
+    return float(mt[0]), time.time() - t0, ""
+
+
+def cpu_baseline(a, methods):
+    """The reference ./test (oracle/_ref/test, built from /root/reference by oracle/Makefile)
+    under MPICH on this box's host cores, same P/A/d/methods, bounded -k, --cpu-budget s in all."""
+    if not os.path.exists(os.path.join(REPO, "oracle", "_ref", "test")):
         return cpu_baseline_port(a, methods)
     tot_bytes, tot_time, per = 0.0, 0.0, {}
     t0 = time.time()
     for m in methods:
-        cmd = [mpiexec, "-launcher", "fork", "-n", str(a.procs), ref, "-a", str(a.aggs), "-p", "1",
-               "-d", str(a.size), "-m", str(m), "-i", "1", "-k", str(a.cpu_reps)]
+        args = ["-n", str(a.procs), "-a", str(a.aggs), "-p", "1", "-d", str(a.size), "-m", str(m), "-i", "1",
+                "-k", str(a.cpu_reps)]
         if a.comm_size != 200000000:
-            cmd += ["-c", str(a.comm_size)]
-        try:
-            out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd="/tmp")
-        except subprocess.TimeoutExpired:
+            args += ["-c", str(a.comm_size)]
+        mt, _wall, err = run_reference(args, a.cpu_budget - (time.time() - t0))
+        if err.startswith("over budget"):
             return {"value": None, "unit": "GB/s", "cores": a.procs, "kind": "reference",
-                    "sample": "timed out after 120 s (method %d)" % m}
-        mt = re.findall(r"max total time = ([0-9.]+)", out.stdout)
-        if out.returncode != 0 or not mt:
-            return cpu_baseline_port(a, methods, note="reference run failed: %s" % out.stderr[-200:])
-        per[m] = float(mt[0])
-        tot_time += float(mt[0])
+                    "sample": "method %d %s (--cpu-budget %.0f s)" % (m, err, a.cpu_budget)}
+        if mt is None:
+            return cpu_baseline_port(a, methods, note=err)
+        per[m] = mt
+        tot_time += mt
         tot_bytes += float(a.procs) * a.aggs * a.size * a.cpu_reps
     ncpu, how = host_cpus()
     return {"value": round(tot_bytes / tot_time / 1e9, 4), "unit": "GB/s", "cores": min(a.procs, ncpu),
@@ -217,6 +309,64 @@ def cpu_baseline(a, methods):
                       % (a.procs, ncpu, how, ", oversubscribed: MPICH busy-polls" if a.procs > ncpu else "",
                          a.aggs, a.size, a.cpu_reps, ",".join(map(str, methods)), time.time() - t0),
             "max_total_time_s": per}
+
+
+# (cell key, P, A, d, -c, method): BASELINE.json's 8-GPU configurations at sizes the host runs --
+# configs[2] at its stated size, configs[3]'s shape at -d 64 KiB, configs[4]'s at -d 4 KiB for -c 1
+# and 8 (64 MiB would be 1 TiB per direction in host RAM); the same keys as the GPU cells at the
+# same -d in baseline_configs_8gpu, so the two sit side by side
+CPU_CELLS = ([("configs[2] m%d" % m, 64, 16, 256 << 10, 200000000, m) for m in (5, 8)] +
+             [("configs[3] at -d 64 KiB m%d" % m, 256, 32, 64 << 10, 200000000, m) for m in (1, 2, 9, 10)] +
+             [("configs[4] -c %d at -d 4 KiB m%d" % (c, m), 256, 64, 4 << 10, c, m) for c in (1, 8)
+              for m in (7, 11, 12)])
+
+
+def cpu_configs_on(a, world):
+    return a.cpu_configs == "on" or (a.cpu_configs == "auto" and world == 8)
+
+
+def cpu_baseline_configs(a, cells=CPU_CELLS):
+    """The reference itself under mpiexec at BASELINE.json's 8-GPU configurations (CPU_CELLS), one
+    process per logical rank on this box's host cores, --cpu-configs-budget seconds in all: a cell
+    that would start past it, or runs past it, is recorded as skipped.  Run before any process
+    touches a GPU (the parent of an N-GPU job, or rank 0 under a launcher)."""
+    ncpu, how = host_cpus()
+    t0 = time.time()
+    res = {"budget_s": a.cpu_configs_budget, "cores": ncpu, "cores_how": how, "kind": "reference",
+           "launch": "mpiexec -launcher fork -n P oracle/_ref/test -a A -p 1 -d D -m M -i 1 -k 1 [-c C] "
+                     "(MPICH 3.3.2 ch3:nemesis, busy-polling ranks)", "cells": {}}
+    for key, P, A, d, c, m in cells:
+        left = a.cpu_configs_budget - (time.time() - t0)
+        if left <= 1:
+            res["cells"][key] = "skipped: budget of %.0f s spent" % a.cpu_configs_budget
+            continue
+        args = ["-n", str(P), "-a", str(A), "-p", "1", "-d", str(d), "-m", str(m), "-i", "1", "-k", "1"]
+        if c != 200000000:
+            args += ["-c", str(c)]
+        mt, wall, err = run_reference(args, left)
+        if mt is None:
+            res["cells"][key] = ("skipped: " if err.startswith("over budget") else "failed: ") + err
+            continue
+        res["cells"][key] = {"P": P, "A": A, "d": d, "c": c, "max_total_time_s": mt,
+                             "GBps_delivered": round(P * A * d / mt / 1e9, 4) if mt > 0 else None,
+                             "wall_s": round(wall, 1), "oversubscription": round(P / max(1, ncpu), 1)}
+    res["spent_s"] = round(time.time() - t0, 1)
+    return res
+
+
+def side_by_side(out):
+    """the reference's max total time beside the GPU job's at the same cell (same P, A, d, -c,
+    method): {cell: {"gpu_max_total_time_s", "reference_max_total_time_s", "speedup"}}"""
+    cpu = ((out.get("cpu_baseline_configs") or {}).get("cells")) or {}
+    gpu = ((out.get("baseline_configs_8gpu") or {}).get("cells")) or {}
+    rows = {}
+    for key, c in cpu.items():
+        g = gpu.get(key)
+        if isinstance(c, dict) and isinstance(g, dict) and g.get("max_total_time_s"):
+            rows[key] = {"gpu_max_total_time_s": g["max_total_time_s"],
+                         "reference_max_total_time_s": c["max_total_time_s"],
+                         "speedup": round(c["max_total_time_s"] / g["max_total_time_s"], 1)}
+    return rows or None
 
 
 def cpu_baseline_port(a, methods, note=""):
@@ -272,10 +422,60 @@ def p2p_sweep(ctx, world, error=RuntimeError):
     return out, None
 
 
+def pair_rounds(n):
+    """a 1-factorisation of the n ranks (circle method; odd n: one rank idle per round): round k
+    -> partner[r] (-1: idle).  Every pair meets exactly once in n - 1 (n odd: n) rounds."""
+    m = n + (n % 2)
+    rounds = []
+    for k in range(m - 1):
+        partner = [-1] * n
+        ring = [m - 1] + [(k + i) % (m - 1) for i in range(m - 1)]
+        for i in range(m // 2):
+            x, y = ring[i], ring[m - 1 - i]
+            if x < n and y < n:
+                partner[x], partner[y] = y, x
+        rounds.append(partner)
+    return rounds
+
+
+def link_sweep(ctx, world, nbytes=16 << 20, reps=5, error=RuntimeError):
+    """per-link rates: in each round of a 1-factorisation every rank exchanges `nbytes` each way
+    with its partner (xg_p2p_pair_bench), all pairs of the round at once -- every link of the node
+    measured under its neighbours' load; a min / max spread shows link asymmetry.  -> (result,
+    error or None): every rank stops at the same round on an error (its flag is MAX-reduced)."""
+    rates = [[None] * world for _ in range(world)]
+    res = {"bytes": nbytes, "reps": reps, "rounds": 0, "GBps": rates}
+    for partner in pair_rounds(world):
+        ctx.barrier()
+        msg = None
+        try:
+            gbps, _sec = ctx.p2p_pair_bench(nbytes, partner[ctx.rank], reps)
+        except error as e:
+            gbps, msg = 0.0, str(e)
+        row = [0.0] * (world * world) + [1.0 if msg else 0.0]
+        if partner[ctx.rank] >= 0:
+            row[ctx.rank * world + partner[ctx.rank]] = gbps
+        got = ctx.allreduce_max(row)
+        if got[-1]:
+            return res, "round %d: %s" % (res["rounds"], msg or "failed on another GPU")
+        for r in range(world):
+            if partner[r] >= 0:
+                rates[r][partner[r]] = round(got[r * world + partner[r]], 2)
+        res["rounds"] += 1
+    vals = [v for row in rates for v in row if v is not None]
+    if vals:
+        res.update(min=min(vals), max=max(vals), spread=round(max(vals) / min(vals), 3) if min(vals) > 0 else None)
+    return res, None
+
+
 # ---------------------------------------------------------------- BASELINE.json's 8-GPU configurations
-# (name, P, A, d, -c, methods): configs[2], configs[3], configs[4] at their stated sizes
+# (name, P, A, d, -c, methods): configs[2], configs[3], configs[4] at their stated sizes, and
+# configs[3] / [4] at the reduced -d the reference runs at on the host (CPU_CELLS: the same keys),
+# ahead of configs[4]'s stated-size cells, which take most of the phase's budget
 BASELINE_CELLS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
-                   ("configs[3]", 256, 32, 4 << 20, 200000000, (1, 2, 9, 10))] +
+                   ("configs[3]", 256, 32, 4 << 20, 200000000, (1, 2, 9, 10)),
+                   ("configs[3] at -d 64 KiB", 256, 32, 64 << 10, 200000000, (1, 2, 9, 10))] +
+                  [("configs[4] -c %d at -d 4 KiB" % c, 256, 64, 4 << 10, c, (7, 11, 12)) for c in (1, 8)] +
                   [("configs[4] -c %d" % c, 256, 64, 64 << 20, c, (7, 11, 12)) for c in range(1, 9)])
 
 
@@ -283,13 +483,51 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
     """Every method of BASELINE.json's 8-GPU configurations on this job: per (config, method) one
     verified run (every slot checked on its GPU, bad slots MAX-reduced), one timed run (device
     time, MAX over GPUs), delivered and cross-GPU (xGMI) GB/s and the reference's max total time.
-    Collective throughout: every rank takes the same cells in the same order, and every decision
-    (budget spent, a plan or allocation that failed on some GPU) is MAX-reduced first, so all ranks
-    skip alike.  Fills result["cells"] as it goes (a watchdog may print it half done)."""
+    Where the relay form (XG_RELAY) changes the plan -- configs[3]'s pairwise m9 / m10, whose
+    XOR rounds put each GPU on one link -- it is verified and timed too, and the faster form is
+    the cell's figure ("forms", "chosen").  Collective throughout: every rank takes the same cells
+    in the same order, and every decision (budget spent, a plan or allocation that failed on some
+    GPU) is MAX-reduced first, so all ranks skip alike.  Fills result["cells"] as it goes (a
+    watchdog may print it half done)."""
     t0 = time.time()
     result["cells"] = cells_out = {}
     regions = {}                      # (P, A, d) -> Regions shared by that configuration's cells
     no_room = set()                   # (P, A, d) whose regions could not be allocated on some GPU
+    default, relay = (4 << 20, -1), (0, xg.RELAY)
+
+    def measure(s, P, A, d, c, form, reg):
+        """one verified + one timed run of a plan form -> (figures, None) or (None, why)"""
+        run, err = None, ""
+        try:
+            run = xg.MethodRun(ctx, s, it=0, mode=0, regions=reg, pack_max_seg=form[0], pack_form=form[1])
+        except xg.XGError as e:
+            err = str(e)
+        if ctx.allreduce_max([1.0 if err else 0.0])[0]:
+            if run is not None:
+                run.close()
+            return None, "failed: %s" % (err or "on another GPU")
+        try:
+            ctx.barrier()
+            done, post, _wall = run.run_timed()
+            lo, hi = s.block_range(world, rank)
+            tmax = max(s.rank_timer(q, done, post, world).total_time for q in range(lo, hi)) if hi > lo else 0.0
+            _chk, bad, _first = run.verify()
+            tmax, nbad = ctx.allreduce_max([tmax, float(sum(1 for b in bad if b))])
+            ctx.barrier()
+            ctx.device_sync()
+            t1 = time.perf_counter()
+            run.enqueue()
+            ctx.device_sync()
+            run.check()
+            t_run = ctx.allreduce_max([time.perf_counter() - t1])[0]
+        finally:
+            run.close()
+        cross = sum(s.devplan(world, g).remote_send_bytes for g in range(world))
+        return {"P": P, "A": A, "d": d, "c": c, "ms_per_run": round(t_run * 1e3, 4),
+                "GBps_delivered": round(P * A * d / t_run / 1e9, 2),
+                "GBps_cross_gpu": round(cross / t_run / 1e9, 2), "cross_gpu_bytes": int(cross),
+                "max_total_time_s": tmax, "verified": nbad == 0, "bad_slots_max_gpu": int(nbad)}, None
+
     try:
         for name, P, A, d, c, methods in cells:
             rl = xg.aggregator_list(P, A)
@@ -302,13 +540,17 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                 if (P, A, d) in no_room:
                     cells_out[key] = "skipped: this configuration's regions did not fit"
                     continue
-                run, err, no_alloc = None, "", False
+                err, no_alloc, relayed = "", False, 0.0
                 try:
                     s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
+                    # does the relay form change this plan (a permutation step with lists >= 1 MiB)?
+                    relayed = 1.0 if world > 2 and any(o[5] for o in s.devplan(world, rank, relay[0], 0, relay[1]).p2p) else 0.0
                     need = [0] * xg.NBUF
                     for mm in methods:          # one allocation per configuration, sized for all its methods
-                        v = xg.Schedule(mm, P, A, d, c, rl, ntimes=1).devplan(world, rank)
-                        need = [max(x, y) for x, y in zip(need, v.region_bytes)]
+                        sm = xg.Schedule(mm, P, A, d, c, rl, ntimes=1)
+                        for f in (default, relay):
+                            v = sm.devplan(world, rank, f[0], 0, f[1])
+                            need = [max(x, y) for x, y in zip(need, v.region_bytes)]
                     rk = (P, A, d)
                     if rk not in regions:
                         for old in regions.values():
@@ -317,43 +559,111 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                         no_alloc = True
                         regions[rk] = xg.Regions(ctx, need)
                         no_alloc = False
-                    run = xg.MethodRun(ctx, s, it=0, mode=0, regions=regions[rk])
                 except xg.XGError as e:
                     err = str(e)
-                failed, unplaced = ctx.allreduce_max([1.0 if err else 0.0, 1.0 if no_alloc else 0.0])
+                failed, unplaced, relayed = ctx.allreduce_max([1.0 if err else 0.0, 1.0 if no_alloc else 0.0, relayed])
                 if failed:
                     cells_out[key] = "failed: %s" % (err or "on another GPU")
-                    if run is not None:
-                        run.close()
                     if unplaced:      # some GPU never got this configuration's regions: the rest would fail alike
                         no_room.add((P, A, d))
                     continue
-                try:
-                    ctx.barrier()
-                    done, post, _wall = run.run_timed()
-                    lo, hi = s.block_range(world, rank)
-                    tmax = max(s.rank_timer(q, done, post, world).total_time for q in range(lo, hi)) if hi > lo else 0.0
-                    _chk, bad, _first = run.verify()
-                    tmax, nbad = ctx.allreduce_max([tmax, float(sum(1 for b in bad if b))])
-                    ctx.barrier()
-                    ctx.device_sync()
-                    t1 = time.perf_counter()
-                    run.enqueue()
-                    ctx.device_sync()
-                    run.check()
-                    t_run = ctx.allreduce_max([time.perf_counter() - t1])[0]
-                    cross = sum(s.devplan(world, g).remote_send_bytes for g in range(world))
-                    cells_out[key] = {"P": P, "A": A, "d": d, "c": c, "ms_per_run": round(t_run * 1e3, 4),
-                                      "GBps_delivered": round(P * A * d / t_run / 1e9, 2),
-                                      "GBps_cross_gpu": round(cross / t_run / 1e9, 2),
-                                      "cross_gpu_bytes": int(cross), "max_total_time_s": tmax,
-                                      "verified": nbad == 0, "bad_slots_max_gpu": int(nbad)}
-                finally:
-                    run.close()
+                forms = {"direct": default}
+                if relayed:
+                    forms["relay"] = relay
+                figs = {}
+                for fname, form in forms.items():
+                    figs[fname], why = measure(s, P, A, d, c, form, regions[(P, A, d)])
+                    if why:
+                        figs[fname] = why
+                ok = {k: v for k, v in figs.items() if isinstance(v, dict) and v["verified"]}
+                if not ok:
+                    cells_out[key] = figs["direct"] if len(figs) == 1 else {"forms": figs}
+                    continue
+                best = min(ok, key=lambda k: ok[k]["ms_per_run"])
+                cell = dict(ok[best])
+                if len(figs) > 1:
+                    cell["chosen"] = best
+                    cell["forms"] = {k: (v["ms_per_run"] if isinstance(v, dict) and v["verified"] else str(v))
+                                     for k, v in figs.items()}
+                cells_out[key] = cell
     finally:
         for r in regions.values():
             r.close()
     result["spent_s"] = round(time.time() - t0, 1)
+
+
+# ---------------------------------------------------------------- diagnostics of the N > 1 line
+LOG_DIR = [None]        # per-job directory of the ranks' RCCL logs (NCCL_DEBUG_FILE)
+
+
+def job_key():
+    """one name per job, the same on every rank: the parent's rendezvous key, else the launcher's
+    port + run id + the launcher's pid (every local rank's parent)"""
+    key = os.environ.get("XG_RDZV_KEY")
+    if not key:
+        key = "%s_%s_pp%d" % (os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", ""),
+                              os.getppid())
+    return re.sub(r"[^A-Za-z0-9_-]", "_", key)
+
+
+def rccl_log_setup(rank):
+    """N > 1: every rank's RCCL warnings into a file of its own (unless NCCL_DEBUG_FILE is set), so
+    rank 0 can attach their tails to the line when something fails"""
+    d = "/tmp/xg_bench_nccl_%s" % job_key()
+    os.makedirs(d, exist_ok=True)
+    os.environ.setdefault("NCCL_DEBUG", "WARN")
+    if "NCCL_DEBUG_FILE" not in os.environ:
+        os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "rank%d.log" % rank)
+        LOG_DIR[0] = d
+
+
+NOISE = ("LL cutoff points not detected", "Could not read node")
+
+
+def rccl_log_tails(lines=6):
+    """{rank: last RCCL warning lines} of every rank of this job (same host), or None"""
+    d = LOG_DIR[0]
+    if not d or not os.path.isdir(d):
+        return None
+    out = {}
+    for f in sorted(os.listdir(d)):
+        m = re.match(r"rank(\d+)\.log$", f)
+        if not m:
+            continue
+        try:
+            txt = [x.strip() for x in open(os.path.join(d, f), errors="replace").read().splitlines()]
+        except OSError:
+            continue
+        txt = [x for x in txt if x and not any(n in x for n in NOISE)]
+        if txt:
+            out[m.group(1)] = [x[-300:] for x in txt[-lines:]]
+    return out or None
+
+
+def line_failed(out):
+    """anything in the line that says a phase or cell failed"""
+    x = out.get("xgmi") or {}
+    b = out.get("baseline_configs_8gpu") or {}
+    return bool(out.get("error") or out.get("xgmi_error") or out.get("failed_methods") or x.get("ceiling_error")
+                or x.get("sweep_error") or x.get("links_error") or b.get("error") or
+                any(str(v).startswith("failed") for v in (b.get("cells") or {}).values()))
+
+
+def finish_line(out, world):
+    """what every N > 1 line carries at print time, wherever it is printed: the wall time of each
+    phase and, when something failed, the tail of every rank's RCCL warnings"""
+    if world > 1:
+        out["phase_wall_s"] = phase_walls()
+        if line_failed(out):
+            out["rccl_log_tail"] = rccl_log_tails()
+    return out
+
+
+def transport():
+    if os.environ.get("XG_SHARE_GPU") == "1":
+        return ("every rank on ONE GPU (XG_SHARE_GPU=1): RCCL's socket transport on loopback, not xGMI -- "
+                "the multi-rank path's calls are real, its rates are not the node's")
+    return "RCCL p2p between the node's GPUs (xGMI)"
 
 
 # ---------------------------------------------------------------- N-GPU job without a launcher
@@ -366,17 +676,21 @@ def spawn_ranks(a):
     with the code XG_BENCH_STUB_RC lists for it; the parent prints them all."""
     stub = os.environ.get("XG_BENCH_CHILD_STUB") == "1"
     methods = [int(x) for x in a.methods.split(",")]
-    cpu = None
+    cpu = cpu_cfg = None
     if not a.no_cpu_baseline and not stub:
         cpu = cpu_baseline(a, methods)
+        if cpu_configs_on(a, a.gpus):
+            cpu_cfg = cpu_baseline_configs(a)
     key = "bench%d_%d" % (os.getpid(), int(time.time() * 1e3))
     argv = [x for x in sys.argv[1:]]
     if "--no-cpu-baseline" not in argv:
         argv.append("--no-cpu-baseline")
     procs, outs = [], []
+    share = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "2")} \
+        if os.environ.get("XG_SHARE_GPU") == "1" else {}     # ranks sharing one GPU: runtime/ctx.hip
     for r in range(a.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
-                   LOCAL_WORLD_SIZE=str(a.gpus), XG_RDZV_KEY=key, XG_BENCH_PARENT=str(os.getpid()))
+                   LOCAL_WORLD_SIZE=str(a.gpus), XG_RDZV_KEY=key, XG_BENCH_PARENT=str(os.getpid()), **share)
         p = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
                              stdout=subprocess.PIPE, text=True)
         procs.append(p)
@@ -429,6 +743,9 @@ def spawn_ranks(a):
         return rc or 1
     out = json.loads(lines[-1])           # rank 0's line -- a failed job's too (value null + error)
     out["cpu_baseline"] = cpu
+    if cpu_cfg is not None:
+        out["cpu_baseline_configs"] = cpu_cfg
+        out["reference_vs_gpu_max_total_time"] = side_by_side(out)
     out["launch"] = "bench.py parent: %d child processes (subprocess), one per GPU" % a.gpus
     if rc:
         out["child_exit_codes"] = rcs
@@ -513,6 +830,8 @@ def xgmi_phase(xg, ctx, runs, world, nmethods, steps, elapsed, out):
         xgmi["frac"] = round(achieved / (ceil_min * world), 4)
     phase("xGMI p2p sweep")
     xgmi["sweep"], xgmi["sweep_error"] = p2p_sweep(ctx, world, xg.XGError)
+    phase("xGMI per-link sweep")
+    xgmi["links"], xgmi["links_error"] = link_sweep(ctx, world, error=xg.XGError)
 
 
 def main():
@@ -527,14 +846,22 @@ def main():
     if world != a.gpus:
         raise SystemExit("WORLD_SIZE=%d but --gpus %d" % (world, a.gpus))
     methods = [int(x) for x in a.methods.split(",")]
-    start_watchdog(a.watchdog, rank)
+    parent = "XG_BENCH_PARENT" in os.environ
+    # up to the communicator: the reference's CPU phases on rank 0 (under a launcher) come first
+    wd = start_watchdog(a.watchdog + pre_value_allowance(a, rank, world, parent) if a.watchdog > 0 else 0, rank)
+    phase("start")
 
-    # host-MPI baseline first, before this process touches the GPU (rank 0; a parent
-    # process of an N-GPU job runs it itself and passes --no-cpu-baseline)
-    cpu = None
+    # host-MPI baselines first, before this process touches the GPU (rank 0; a parent
+    # process of an N-GPU job runs them itself and passes --no-cpu-baseline)
+    cpu = cpu_cfg = None
     if rank == 0 and not a.no_cpu_baseline:
         phase("cpu baseline")
         cpu = cpu_baseline(a, methods)
+        if cpu_configs_on(a, world):
+            phase("cpu baseline at the BASELINE 8-GPU configurations")
+            cpu_cfg = cpu_baseline_configs(a)
+    if world > 1:
+        rccl_log_setup(rank)
 
     import __graft_entry__ as G
     xg = G.load_package().xg
@@ -549,12 +876,13 @@ def main():
     except xg.XGError as e:
         # no communicator, so nothing to agree over: each rank reports for itself, rank 0 the line
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world,
-                              "higher_is_better": True, "dtype": "u8",
-                              "error": "device / RCCL init failed on rank 0 (%s): %s" % (PHASE[0], e),
-                              "cpu_baseline": cpu}), flush=True)
+            print(json.dumps(finish_line({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world,
+                                          "higher_is_better": True, "dtype": "u8",
+                                          "error": "device / RCCL init failed on rank 0 (%s): %s" % (PHASE[0], e),
+                                          "cpu_baseline": cpu}, world)), flush=True)
         sys.stderr.write("bench: rank %d: %s\n" % (rank, e))
         return 1
+    wd.arm(a.watchdog)              # from the communicator to the measured value
     ctx.barrier()
     if rdzv:
         os.unlink(rdzv)
@@ -650,6 +978,9 @@ def main():
             continue
         if len(cands) > 1:
             tune[str(m)]["chosen"] = names[best[3]]
+            times = sorted(v for k, v in tune[str(m)].items() if k.endswith("_ms"))
+            # how far ahead the chosen form is: (runner-up - chosen) / chosen
+            tune[str(m)]["margin"] = round((times[1] - times[0]) / times[0], 4) if len(times) > 1 and times[0] > 0 else None
         max_total[str(m)] = best[2]
         runs.append(best[1])
     if failed:
@@ -658,11 +989,12 @@ def main():
         for r in runs:
             r.close()
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": a.steps,
-                              "warmup": a.warmup, "higher_is_better": True, "dtype": "u8",
-                              "error": "every plan form of method(s) %s failed" % ",".join(sorted(failed)),
-                              "failed_methods": failed, "pack_autotune_ms_per_run": tune or None,
-                              "cpu_baseline": cpu}))
+            print(json.dumps(finish_line({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world,
+                                          "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+                                          "dtype": "u8",
+                                          "error": "every plan form of method(s) %s failed" % ",".join(sorted(failed)),
+                                          "failed_methods": failed, "pack_autotune_ms_per_run": tune or None,
+                                          "cpu_baseline": cpu}, world)))
         ctx.close()
         return 1
 
@@ -727,6 +1059,7 @@ def main():
 
     seg_bytes = float(a.procs) * a.aggs * a.size * len(methods) * a.steps
     value = seg_bytes / elapsed / 1e9
+    wd.cancel()      # the value is measured: the LineGuards own every phase after this
 
     roof = None
     if nlaunch and rank == 0:
@@ -775,6 +1108,11 @@ def main():
         "cpu_baseline": cpu,
     }
     if world > 1:
+        out["rccl_version"] = xg.rccl_version()
+        out["transport"] = transport()
+    if cpu_cfg is not None:
+        out["cpu_baseline_configs"] = cpu_cfg
+    if world > 1:
         # N > 1: cross-GPU (xGMI) bytes of the timed region vs the measured RCCL all-pairs ceiling
         with LineGuard(out, rank, a.xgmi_budget, lambda msg: out.__setitem__("xgmi_error", msg)):
             xgmi_phase(xg, ctx, runs, world, len(methods), a.steps, elapsed, out)
@@ -793,7 +1131,9 @@ def main():
             except xg.XGError as e:
                 extra["error"] = str(e)
     if rank == 0:
-        print(json.dumps(out))
+        if cpu_cfg is not None:
+            out["reference_vs_gpu_max_total_time"] = side_by_side(out)
+        print(json.dumps(finish_line(out, world)))
     ctx.close()
     return 0
 

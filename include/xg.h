@@ -76,6 +76,15 @@ double xg_now(void);                                           /* host seconds (
 /* Diagnostics: where this process's host thread last was in the library -- entry point, step,
  * posting or waiting for the device -- for a watchdog to print when a run does not return. */
 const char *xg_debug_where(void);
+/* ROCm runtime libraries (libamdhip64, librccl, libhsa-runtime64) mapped into this process from
+ * outside the ROCm install (/opt/rocm*, $ROCM_PATH): e.g. torch's wheel bundles its own under the
+ * same sonames, and a process that loaded them first binds libxg.so to another HIP runtime and
+ * RCCL than it was built against (profiles/r04/torch_runtime/).  Returns how many; their paths,
+ * comma-separated, in buf (may be NULL).  xg_get_unique_id and xg_init refuse (XG_EARG) when
+ * this is > 0, so every entry point (bin/test, bin/pt2pt_test, bench.py, xg.py) does. */
+int xg_foreign_runtime(char *buf, size_t len);
+/* RCCL's version as ncclGetVersion reports it (e.g. 22703 for 2.27.3). */
+int xg_rccl_version(int *version);
 
 /* ------------------------------------------------------------------ HBM regions */
 /* region_bytes: XG_BUF_SEND, XG_BUF_RECV, XG_BUF_STAGE_SEND, XG_BUF_STAGE_RECV,
@@ -175,6 +184,12 @@ int xg_ktime_launch(xg_ctx *ctx, int k, double *ms, int64_t *bytes);
  * 2: one direction rank 1 -> rank 0.  *gbps = bytes sent by this rank per
  * second (mode 2: bytes moved 1 -> 0), *sec = seconds per repetition. */
 int xg_p2p_bench(xg_ctx *ctx, int64_t bytes, int mode, int reps, double *gbps, double *sec);
+/* One link: `bytes` each way between this rank and `peer` (send + receive in one group), reps
+ * times; peer < 0 or peer == this rank: idle (returns 0 rates).  Every rank of a round calls it
+ * with its partner of that round (a 1-factorisation of the ranks), so all links of the round run
+ * at once and each is measured under the others' load (the per-peer sweep of the N > 1 bench
+ * line: link asymmetry shows as the spread).  *gbps = bytes this rank sent per second. */
+int xg_p2p_pair_bench(xg_ctx *ctx, int64_t bytes, int peer, int reps, double *gbps, double *sec);
 
 /* Tuning: bytes per copy workgroup (default 32768; chunk_bytes 0 keeps it) and copy kernel
  * variant: 0 (default) = copy_kernel_g<4> with non-temporal loads/stores for launches moving

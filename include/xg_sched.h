@@ -156,7 +156,7 @@ typedef struct {
     int64_t off, len;
     int32_t peer, buf;
     int32_t is_send;
-    int32_t pad;
+    int32_t group;                    /* RCCL group of the step: 0, or 1 (relay form: the forwards) */
 } xg_p2p;
 
 typedef struct {
@@ -212,9 +212,21 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
  * (profiles/r03/pack_forms/), so it is the default; bench.py times direct, one-sided and
  * two-sided per method at N > 1 and keeps the fastest.  Any other form value means
  * XG_PACK_FORM_DEFAULT.  The alltoallw translate this replaces: mpi_test.c:233-302. */
-enum { XG_PACK_TWO_SIDED = 0, XG_PACK_ONE_SIDED = 1 };
+/*   XG_RELAY           no packing; a step whose cross-GPU traffic is a (partial) permutation of the
+ *                      GPUs -- every GPU sends to at most one peer and receives from at most one, each
+ *                      such list moving >= XG_RELAY_MIN_BYTES (pairwise m9 / m10: one XOR partner per
+ *                      round) -- is sent over every link instead of one: each message is cut into G
+ *                      16-B aligned pieces; pieces 0 and 1 go straight to the destination (piece 0 in
+ *                      the step's first RCCL group, piece 1 in its second), piece 2 + i through relay
+ *                      GPU R[i] (the G - 2 GPUs other than source and destination, ascending): received
+ *                      into the relay's STAGE_RECV in the first group and forwarded to the destination
+ *                      in the second.  Per link and group that is 1/G of the list instead of all of it
+ *                      on one link: ~G/2 x less time per round at the link rate (link-load
+ *                      table).  Other steps: direct.  No copy kernel touches a relayed byte. */
+enum { XG_PACK_TWO_SIDED = 0, XG_PACK_ONE_SIDED = 1, XG_RELAY = 2 };
 #define XG_PACK_FORM_DEFAULT XG_PACK_TWO_SIDED
 #define XG_RUN_CALL_BYTES (1 << 20)
+#define XG_RELAY_MIN_BYTES (1 << 20)
 xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
                                   int form);
 /* All three return NULL (nothing leaked) when the host runs out of memory while building: every
@@ -224,7 +236,8 @@ void xg_devplan_free(xg_devplan *p);
 
 /* ---------------------------------------------------------------- RCCL calls (calls.c)
  * The calls GPU dp->gpu posts in step `step`, in issue order: its send/recv calls
- * (one ncclGroupStart/End around them), then XG_CALL_BARRIER (one ncclAllReduce)
+ * (one ncclGroupStart/End around them; a relay step's second group follows an
+ * XG_CALL_FENCE), then XG_CALL_BARRIER (one ncclAllReduce)
  * when the step ends in an in-loop MPI_Barrier.  self_max > 0: a step that posts
  * cross-GPU calls and whose local gather/scatter copies move <= self_max bytes
  * posts those copies inside the same group as self send/recv pairs (peer = dp->gpu,
@@ -233,7 +246,7 @@ void xg_devplan_free(xg_devplan *p);
  * runtime posts exactly this list (replaces the Issend/Irecv/Sendrecv/Alltoallw
  * posts, mpi_test.c:1776,1790, :551,558, :627,912).  Returns the count (out may be
  * NULL), -1 for a bad step. */
-enum { XG_CALL_SEND = 1, XG_CALL_RECV = 2, XG_CALL_BARRIER = 3 };
+enum { XG_CALL_SEND = 1, XG_CALL_RECV = 2, XG_CALL_BARRIER = 3, XG_CALL_FENCE = 4 };
 typedef struct {
     int32_t kind, peer, buf, pad;     /* peer: GPU; buf: region (XG_BUF_*) */
     int64_t off, len;
@@ -245,14 +258,15 @@ int xg_devplan_step_self_calls(const xg_devplan *dp, int step, int64_t self_max)
  * k-th send of src to dst with the k-th receive of dst from src, in issue order
  * over the WHOLE run (RCCL's per-peer FIFO knows no steps).  calls[g] / step_begin[g]
  * (nsteps + 1 entries): GPU g's calls and where each step's start.  Accepted only if
- * every pair falls in one step with one length and every GPU ends the same steps
- * with a barrier (each its step's last call) -- then no group can wait for one a
- * peer posts later.  Returns the number of pairs, written step-major (inside a step
- * by src, dst, k) to out when max_pairs suffices; -1 and a reason in err otherwise. */
+ * every pair falls in one step and one group of it (groups: separated by XG_CALL_FENCE)
+ * with one length and every GPU ends the same steps with a barrier (each its step's
+ * last call) -- then no group can wait for one a peer posts later.  Returns the number
+ * of pairs, written in (step, group) order (inside a group by src, dst, k) to out when
+ * max_pairs suffices; -1 and a reason in err otherwise. */
 typedef struct {
     int32_t step, src, dst;
     int32_t send_call, recv_call;     /* indices into calls[src] / calls[dst] */
-    int32_t pad;
+    int32_t group;                    /* the step's RCCL group both calls are in */
     int64_t len;
 } xg_call_pair;
 int64_t xg_calls_match(int ngpus, int nsteps, const xg_call *const *calls, const int32_t *const *step_begin,

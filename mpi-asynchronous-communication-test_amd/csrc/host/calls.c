@@ -12,7 +12,8 @@
  * xg_calls_match pairs calls the way RCCL does: per ordered GPU pair (g, h), the
  * k-th send of g to h with the k-th receive of h from g, in issue order over the
  * whole run -- RCCL's per-(peer, communicator) FIFO knows no steps.  A job is
- * accepted only if every such pair falls in ONE step with ONE length and every
+ * accepted only if every such pair falls in ONE step and ONE group of it (a relay
+ * step has two, separated by XG_CALL_FENCE) with ONE length and every
  * GPU ends the same steps with a barrier: then each step's groups pair among
  * themselves, every GPU posts its collectives in the same order, and no group
  * waits for one a peer posts later (the job cannot hang on a mismatch).
@@ -57,22 +58,25 @@ int xg_devplan_step_self_calls(const xg_devplan *dp, int step, int64_t self_max)
     return n;
 }
 
+static void put_p2p(xg_call *c, const xg_p2p *o)
+{
+    c->kind = o->is_send ? XG_CALL_SEND : XG_CALL_RECV;
+    c->peer = o->peer;
+    c->buf = o->buf;
+    c->pad = 0;
+    c->off = o->off;
+    c->len = o->len;
+}
+
 int xg_devplan_step_calls(const xg_devplan *dp, int step, int64_t self_max, xg_call *out)
 {
     const xg_stepplan *sp;
-    int i, n = 0;
+    int i, n = 0, g1;
     if (!dp || step < 0 || step >= dp->nsteps) return -1;
     sp = &dp->steps[step];
-    for (i = 0; i < sp->p2p_count; ++i, ++n) {
-        const xg_p2p *o = &dp->p2p[sp->p2p_begin + i];
-        if (!out) continue;
-        out[n].kind = o->is_send ? XG_CALL_SEND : XG_CALL_RECV;
-        out[n].peer = o->peer;
-        out[n].buf = o->buf;
-        out[n].pad = 0;
-        out[n].off = o->off;
-        out[n].len = o->len;
-    }
+    /* group 0's send/recv calls (the plan lists a relay step's group 1 after them) */
+    for (g1 = 0; g1 < sp->p2p_count && dp->p2p[sp->p2p_begin + g1].group == 0; ++g1, ++n)
+        if (out) put_p2p(&out[n], &dp->p2p[sp->p2p_begin + g1]);
     if (xg_devplan_step_self_calls(dp, step, self_max)) {
         /* the step's local copies as self send + receive pairs inside its group: one RCCL
          * launch carries the whole step (RCCL pairs the k-th self send with the k-th self
@@ -91,6 +95,19 @@ int xg_devplan_step_calls(const xg_devplan *dp, int step, int64_t self_max, xg_c
             }
             n += 2;
         }
+    }
+    if (g1 < sp->p2p_count) {
+        /* a relay step's second group (the forwards and the direct second pieces) behind a fence:
+         * the runtime closes group 0 (ncclGroupEnd) before it opens this one */
+        if (out) {
+            memset(&out[n], 0, sizeof out[n]);
+            out[n].kind = XG_CALL_FENCE;
+            out[n].peer = -1;
+            out[n].buf = -1;
+        }
+        ++n;
+        for (i = g1; i < sp->p2p_count; ++i, ++n)
+            if (out) put_p2p(&out[n], &dp->p2p[sp->p2p_begin + i]);
     }
     if (sp->sync_after) {
         if (out) {
@@ -129,10 +146,11 @@ int64_t xg_calls_match(int ngpus, int nsteps, const xg_call *const *calls, const
                        xg_call_pair *out, int64_t max_pairs, char *err, size_t errlen)
 {
     const int G = ngpus;
-    int g, h, s;
+    int g, h, s, ngrp = 1;
     int64_t k, nsend = 0, nrecv = 0, np = 0;
     int64_t *soff = NULL, *roff = NULL, *sfill = NULL, *rfill = NULL, *cnt = NULL;
     int32_t *sidx = NULL, *ridx = NULL;
+    int32_t **grp = NULL;       /* per GPU and call: the group of its step the call is in */
     xg_call_pair *pairs = NULL;
     int64_t rc = -1;
     if (err && errlen) err[0] = 0;
@@ -149,7 +167,7 @@ int64_t xg_calls_match(int ngpus, int nsteps, const xg_call *const *calls, const
             return -1;
         }
         for (s = 0; s < nsteps; ++s) {
-            int i, bar = 0;
+            int i, bar = 0, gi = 0;
             if (sb[s + 1] < sb[s]) {
                 fail(err, errlen, "GPU %d: step %d has a negative call count", g, s);
                 return -1;
@@ -158,6 +176,14 @@ int64_t xg_calls_match(int ngpus, int nsteps, const xg_call *const *calls, const
                 const xg_call *c = &calls[g][i];
                 if (c->kind == XG_CALL_BARRIER) {
                     bar = 1;
+                    continue;
+                }
+                if (c->kind == XG_CALL_FENCE) {
+                    if (bar) {
+                        fail(err, errlen, "GPU %d step %d: a group fence after the step's barrier", g, s);
+                        return -1;
+                    }
+                    if (++gi + 1 > ngrp) ngrp = gi + 1;
                     continue;
                 }
                 if (c->kind != XG_CALL_SEND && c->kind != XG_CALL_RECV) {
@@ -224,10 +250,25 @@ int64_t xg_calls_match(int ngpus, int nsteps, const xg_call *const *calls, const
             }
         }
     pairs = (xg_call_pair *)malloc(sizeof(xg_call_pair) * (size_t)(nsend + 1));
-    cnt = (int64_t *)calloc((size_t)nsteps + 1, sizeof(int64_t));
-    if (!pairs || !cnt) {
+    cnt = (int64_t *)calloc((size_t)nsteps * ngrp + 1, sizeof(int64_t));
+    grp = (int32_t **)calloc((size_t)G, sizeof(int32_t *));
+    if (!pairs || !cnt || !grp) {
         fail(err, errlen, "xg_calls_match: out of memory");
         goto done;
+    }
+    for (g = 0; g < G; ++g) {
+        const int32_t *sb = step_begin[g];
+        if (!(grp[g] = (int32_t *)malloc(sizeof(int32_t) * ((size_t)sb[nsteps] + 1)))) {
+            fail(err, errlen, "xg_calls_match: out of memory");
+            goto done;
+        }
+        for (s = 0; s < nsteps; ++s) {
+            int i, gi = 0;
+            for (i = sb[s]; i < sb[s + 1]; ++i) {
+                gi += calls[g][i].kind == XG_CALL_FENCE;
+                grp[g][i] = gi;
+            }
+        }
     }
     for (g = 0; g < G; ++g)
         for (h = 0; h < G; ++h) {
@@ -248,24 +289,31 @@ int64_t xg_calls_match(int ngpus, int nsteps, const xg_call *const *calls, const
                          (long long)k, g, h, ss, rs);
                     goto done;
                 }
+                if (grp[g][si] != grp[h][ri]) {
+                    fail(err, errlen, "step %d: send %lld of GPU %d to GPU %d is in group %d, its receive in group %d",
+                         ss, (long long)k, g, h, grp[g][si], grp[h][ri]);
+                    goto done;
+                }
                 if (sc->len != rcv->len) {
                     fail(err, errlen, "step %d: send %lld of GPU %d to GPU %d carries %lld bytes, its receive %lld", ss,
                          (long long)k, g, h, (long long)sc->len, (long long)rcv->len);
                     goto done;
                 }
-                q->step = ss; q->src = g; q->dst = h; q->send_call = si; q->recv_call = ri; q->pad = 0;
+                q->step = ss; q->src = g; q->dst = h; q->send_call = si; q->recv_call = ri; q->group = grp[g][si];
                 q->len = sc->len;
-                cnt[ss + 1]++;
+                cnt[(size_t)ss * ngrp + q->group + 1]++;
             }
         }
-    /* step-major, stable: inside a step by (src, dst, k) */
-    for (s = 0; s < nsteps; ++s) cnt[s + 1] += cnt[s];
+    /* (step, group)-major, stable: inside a group by (src, dst, k) */
+    for (k = 0; k < (int64_t)nsteps * ngrp; ++k) cnt[k + 1] += cnt[k];
     if (out && max_pairs >= np) {
-        for (k = 0; k < np; ++k) out[cnt[pairs[k].step]++] = pairs[k];
+        for (k = 0; k < np; ++k) out[cnt[(size_t)pairs[k].step * ngrp + pairs[k].group]++] = pairs[k];
     }
     rc = np;
 done:
     free(soff); free(roff); free(sfill); free(rfill); free(sidx); free(ridx); free(pairs); free(cnt);
+    for (g = 0; grp && g < G; ++g) free(grp[g]);
+    free(grp);
     return rc;
 }
 

@@ -2007,6 +2007,96 @@ static void os_free(oneside *o)
     o->fail = fail;
 }
 
+/* ---- relay form (XG_RELAY, xg_sched.h).  A step is relayed when its cross-GPU messages form a
+ * (partial) permutation of the GPUs -- every GPU sends to <= 1 peer and receives from <= 1 -- and
+ * every such list moves >= XG_RELAY_MIN_BYTES: pairwise m9 / m10 (mpi_test.c:510-597, :421-508;
+ * partner rank ^ i, :531-545) at configs[3] put every GPU's round on ONE of its 7 links.  Every GPU
+ * decides from the same message list, so all agree. */
+static int relay_step(const xg_sched *s, const int *order, int b, int e, int G, int *to, int *from, int64_t *bytes)
+{
+    int k, g, any = 0;
+    if (G < 3) return 0;
+    for (g = 0; g < G; ++g) { to[g] = from[g] = -1; bytes[g] = 0; }
+    for (k = b; k < e; ++k) {
+        const xg_msg *m = &s->msgs[order[k]];
+        const int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
+        if (!moves(m) || is_stage(m) || gs == gd) continue;
+        if ((to[gs] >= 0 && to[gs] != gd) || (from[gd] >= 0 && from[gd] != gs)) return 0;
+        to[gs] = gd;
+        from[gd] = gs;
+        bytes[gs] += m->len;
+        any = 1;
+    }
+    for (g = 0; g < G; ++g)
+        if (to[g] >= 0 && bytes[g] < XG_RELAY_MIN_BYTES) return 0;
+    return any;
+}
+
+/* piece k of a relayed message of len bytes: [relay_cut(k), relay_cut(k + 1)), 16-B aligned cuts */
+static int64_t relay_cut(int64_t len, int k, int G) { return k >= G ? len : ((len * k / G) & ~(int64_t)15); }
+
+/* relay i (0 .. G-3) of a message from GPU gs to GPU gd: the GPUs other than gs, gd, ascending */
+static int relay_gpu(int i, int gs, int gd)
+{
+    const int lo = gs < gd ? gs : gd, hi = gs < gd ? gd : gs;
+    int h = i;
+    if (h >= lo) ++h;
+    if (h >= hi) ++h;
+    return h;
+}
+
+static void relay_push(pvec *pp, int peer, int is_send, int buf, int64_t off, int64_t len, int group)
+{
+    xg_p2p *o;
+    if (len <= 0) return;            /* a 0-byte piece (len < 16 G): no call on either side */
+    o = ppush(pp);
+    o->peer = peer; o->is_send = is_send; o->buf = buf; o->off = off; o->len = len; o->group = group;
+}
+
+/* GPU g's calls of one relayed step: group 0 = pieces 0 straight to the destination and pieces
+ * 2 + i to relay R[i] (into its STAGE_RECV at *rbase on); group 1 = pieces 1 straight, and what g
+ * holds as a relay forwarded to the destination.  Every list is in message order, so the k-th
+ * send of any GPU to any other pairs with the k-th receive there, group by group. */
+static void relay_calls(const xg_sched *s, const plan_bases *pb, const int *order, int b, int e, int G, int g,
+                        pvec *pp, int64_t *rbase)
+{
+    int grp, k, i;
+    int64_t roff = *rbase;
+    for (grp = 0; grp < 2; ++grp) {
+        roff = *rbase;
+        for (k = b; k < e; ++k) {
+            const xg_msg *m = &s->msgs[order[k]];
+            const int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
+            const int ri = g != gs && g != gd ? g - (g > gs) - (g > gd) : -1;   /* g's relay index */
+            int64_t so, dof;
+            if (!moves(m) || is_stage(m) || gs == gd) continue;
+            so = src_off(pb, m);
+            dof = dst_off(pb, m);
+            if (g == gs) {
+                relay_push(pp, gd, 1, m->sbuf, so + relay_cut(m->len, grp, G),
+                           relay_cut(m->len, grp + 1, G) - relay_cut(m->len, grp, G), grp);
+                for (i = 0; grp == 0 && i < G - 2; ++i)
+                    relay_push(pp, relay_gpu(i, gs, gd), 1, m->sbuf, so + relay_cut(m->len, 2 + i, G),
+                               relay_cut(m->len, 3 + i, G) - relay_cut(m->len, 2 + i, G), 0);
+            }
+            if (ri >= 0) {
+                const int64_t len = relay_cut(m->len, 3 + ri, G) - relay_cut(m->len, 2 + ri, G);
+                if (grp == 0) relay_push(pp, gs, 0, XG_BUF_STAGE_RECV, roff, len, 0);
+                else relay_push(pp, gd, 1, XG_BUF_STAGE_RECV, roff, len, 1);
+                roff += len > 0 ? len : 0;
+            }
+            if (g == gd) {
+                relay_push(pp, gs, 0, m->dbuf, dof + relay_cut(m->len, grp, G),
+                           relay_cut(m->len, grp + 1, G) - relay_cut(m->len, grp, G), grp);
+                for (i = 0; grp == 1 && i < G - 2; ++i)
+                    relay_push(pp, relay_gpu(i, gs, gd), 0, m->dbuf, dof + relay_cut(m->len, 2 + i, G),
+                               relay_cut(m->len, 3 + i, G) - relay_cut(m->len, 2 + i, G), 1);
+            }
+        }
+    }
+    *rbase = roff;
+}
+
 xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
                                   int form)
 {
@@ -2020,11 +2110,15 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
     int *bucket_n = (int *)calloc((size_t)G * 2, sizeof(int));
     int64_t *bucket_b = (int64_t *)calloc((size_t)G * 2, sizeof(int64_t));
     oneside *os_out = (oneside *)calloc((size_t)G, sizeof(oneside)), *os_in = (oneside *)calloc((size_t)G, sizeof(oneside));
+    int *rl_to = (int *)calloc((size_t)G, sizeof(int)), *rl_from = (int *)calloc((size_t)G, sizeof(int));
+    int64_t *rl_b = (int64_t *)calloc((size_t)G, sizeof(int64_t));
     plan_bases pb;
     memset(&pre, 0, sizeof pre); memset(&post, 0, sizeof post); memset(&pp, 0, sizeof pp);
     memset(&pb, 0, sizeof pb);
-    if (form != XG_PACK_TWO_SIDED && form != XG_PACK_ONE_SIDED) form = XG_PACK_FORM_DEFAULT;
-    if (!dp || !cnt || !order || !pos || !bucket_n || !bucket_b || !os_out || !os_in || plan_bases_init(&pb, s, G, g) ||
+    if (form != XG_PACK_TWO_SIDED && form != XG_PACK_ONE_SIDED && form != XG_RELAY) form = XG_PACK_FORM_DEFAULT;
+    if (form == XG_RELAY) pack_max_seg = 0;         /* relay form: every other step is direct */
+    if (!dp || !cnt || !order || !pos || !bucket_n || !bucket_b || !os_out || !os_in || !rl_to || !rl_from || !rl_b ||
+        plan_bases_init(&pb, s, G, g) ||
         !(dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan)))) {
         oom = 1;
         goto done;
@@ -2119,7 +2213,15 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
         /* the grouped exchange: per peer, sends then receives, message order */
         sp->p2p_begin = pp.n;
         sp->post_begin = post.n;
-        {
+        if (form == XG_RELAY && relay_step(s, order, b, e, G, rl_to, rl_from, rl_b)) {
+            /* a permutation step: every list over all G - 1 links of its source (two groups) */
+            relay_calls(s, &pb, order, b, e, G, g, &pp, &rbase);
+            for (p = 0; p < G; ++p)
+                if (p != g) {
+                    dp->remote_send_bytes += bucket_b[p];
+                    dp->remote_recv_bytes += bucket_b[G + p];
+                }
+        } else {
             int64_t soff = 0;
             for (p = 0; p < G; ++p) {
                 int pk;
@@ -2244,7 +2346,7 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
     oom |= !dp->copies || !dp->p2p;
 done:
     free(pre.v); free(post.v); free(pp.v); free(cnt); free(order); free(pos); free(bucket_n); free(bucket_b);
-    free(os_out); free(os_in);
+    free(os_out); free(os_in); free(rl_to); free(rl_from); free(rl_b);
     plan_bases_free(&pb);
     if (oom) {
         xg_devplan_free(dp);

@@ -1,6 +1,12 @@
 // ctx.hip -- context (streams, communicator, tuning), HBM regions, fill / verify.
 #include "rt.h"
 
+#include <dirent.h>
+#include <limits.h>
+#include <link.h>
+
+#include <string>
+
 extern "C" double xg_now(void)
 {
     struct timespec ts;
@@ -13,7 +19,12 @@ extern "C" double xg_now(void)
 // one host ("Duplicate GPU detected"), so every rank names a host of its own (NCCL_HOSTID):
 // the ranks then pair over RCCL's network transport (sockets on loopback) instead of xGMI.
 // The calls, groups, pairing and collectives are the real multi-rank ones; the transport and
-// its rates are not the node's.  Called before the first RCCL call of the process.
+// its rates are not the node's.  (More than ~16 hardware queues on the device -- 8 ranks x HIP's
+// default 4 -- and the command processor time-slices them: a README run of m9 took 0.79 s at 8
+// ranks against 9 ms with 2 queues per process, profiles/r05/share_gpu_queues/.  HIP reads
+// GPU_MAX_HW_QUEUES when it loads, so the launchers -- bench.py, xg_spawn_ranks, the tests --
+// set it to 2 for the processes they start on a shared device.)  Called before the first RCCL
+// call of the process.
 static void share_gpu_env(int rank)
 {
     const char *v = getenv("XG_SHARE_GPU");
@@ -22,6 +33,82 @@ static void share_gpu_env(int rank)
     snprintf(id, sizeof id, "xg-share-gpu-rank-%d", rank);
     setenv("NCCL_HOSTID", id, 1);
     setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+    // every rank's RCCL kernels share the one device's CUs and spin until their peer's proxy
+    // delivers: few channels per rank keep all ranks' kernels resident at once
+    setenv("NCCL_MAX_NCHANNELS", "2", 0);
+}
+
+// ---- the ROCm runtime this process runs on (xg.h: xg_foreign_runtime)
+static bool under(const std::string &path, const std::string &root)
+{
+    return !root.empty() && path.size() > root.size() && path.compare(0, root.size(), root) == 0 &&
+           path[root.size()] == '/';
+}
+
+static std::string real(const char *p)
+{
+    char buf[PATH_MAX];
+    return p && realpath(p, buf) ? std::string(buf) : std::string();
+}
+
+struct Foreign {
+    std::vector<std::string> roots, bad;
+};
+
+static int foreign_cb(struct dl_phdr_info *info, size_t, void *arg)
+{
+    Foreign *f = static_cast<Foreign *>(arg);
+    const char *name = info->dlpi_name;
+    if (!name || !*name) return 0;
+    const char *base = strrchr(name, '/');
+    base = base ? base + 1 : name;
+    static const char *const libs[] = {"libamdhip64.so", "librccl.so", "libhsa-runtime64.so"};
+    bool rocm = false;
+    for (const char *l : libs) rocm |= strncmp(base, l, strlen(l)) == 0;
+    if (!rocm) return 0;
+    const std::string rp = real(name);
+    for (const std::string &r : f->roots)
+        if (under(rp.empty() ? std::string(name) : rp, r)) return 0;
+    f->bad.push_back(rp.empty() ? std::string(name) : rp);
+    return 0;
+}
+
+extern "C" int xg_foreign_runtime(char *buf, size_t len)
+{
+    Foreign f;
+    f.roots.push_back(real("/opt/rocm"));
+    if (getenv("ROCM_PATH")) f.roots.push_back(real(getenv("ROCM_PATH")));
+    if (DIR *d = opendir("/opt")) {                  // versioned installs (/opt/rocm-7.2.0)
+        while (struct dirent *e = readdir(d))
+            if (!strncmp(e->d_name, "rocm", 4)) f.roots.push_back(real(("/opt/" + std::string(e->d_name)).c_str()));
+        closedir(d);
+    }
+    dl_iterate_phdr(foreign_cb, &f);
+    if (buf && len) {
+        std::string all;
+        for (const std::string &b : f.bad) all += (all.empty() ? "" : ", ") + b;
+        snprintf(buf, len, "%s", all.c_str());
+    }
+    return (int)f.bad.size();
+}
+
+// refuse to start on another ROCm runtime than the one libxg.so is built against
+static int check_runtime(const char *who)
+{
+    char bad[1024];
+    if (xg_foreign_runtime(bad, sizeof bad) > 0) {
+        fprintf(stderr, "xg: %s refused: a foreign ROCm runtime is mapped in this process (%s), e.g. loaded by "
+                        "`import torch` before the framework; libxg.so is built against /opt/rocm\n", who, bad);
+        return XG_EARG;
+    }
+    return XG_OK;
+}
+
+extern "C" int xg_rccl_version(int *version)
+{
+    if (!version) return XG_EARG;
+    NCCLCHK(ncclGetVersion(version));
+    return XG_OK;
 }
 
 static int env_rank()
@@ -33,6 +120,7 @@ static int env_rank()
 
 extern "C" int xg_get_unique_id(void *uid)
 {
+    if (check_runtime("xg_get_unique_id")) return XG_EARG;
     share_gpu_env(env_rank());
     rccl_log_to_stderr();
     StdoutToStderr quiet;
@@ -49,6 +137,8 @@ extern "C" int xg_init(xg_ctx **out, int rank, int nranks, int device, const voi
 {
     int ndev = 0;
     if (!out || nranks < 1 || rank < 0 || rank >= nranks) return XG_EARG;
+    if (check_runtime("xg_init")) return XG_EARG;
+    if (nranks > 1) share_gpu_env(rank);
     HIPCHK(hipGetDeviceCount(&ndev));
     if (device >= ndev && ndev > 0 && nranks > 1) {
         // a launcher that narrows each rank's view (HIP_VISIBLE_DEVICES per rank) leaves
@@ -187,7 +277,6 @@ static int init_ctx(xg_ctx *c, const void *uid)
         ncclUniqueId id;
         if (!uid) return XG_EARG;
         memcpy(&id, uid, sizeof id);
-        share_gpu_env(rank);
         StdoutToStderr quiet;
         NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
     } else if (getenv("XG_SELF_COMM") && atoi(getenv("XG_SELF_COMM"))) {

@@ -205,20 +205,27 @@ static int enqueue_step(xg_plan *p, int s)
     }
     if ((rc = enqueue_pre(p, s, c->stream, c->side))) return rc;
     if (p->local_only) return enqueue_post(p, s, c->stream);
-    // the step's send/recv calls, in the order libxghost lists them (xg_devplan_step_calls),
-    // as one group; the barrier call, if any, is the step's last and follows the unpacks
+    // the step's send/recv calls, in the order libxghost lists them (xg_devplan_step_calls), one
+    // group per run of them between fences (a relay step: two, the second forwarding what the
+    // first delivered to this GPU's staging -- stream order puts it behind the first); the
+    // barrier call, if any, is the step's last and follows the unpacks
     const xg_call *cl = p->calls.data() + st.call_b;
-    if (st.p2p_n && (rc = rccl_group(
-                         st.p2p_n,
-                         [&](int i) {
-                             const xg_call &o = cl[i];
-                             uint8_t *ptr = p->reg->ptr[o.buf] + o.off;
-                             return o.kind == XG_CALL_SEND
-                                        ? ncclSend(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream)
-                                        : ncclRecv(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream);
-                         },
-                         "step exchange")))
-        return rc;
+    for (int i = 0; i < st.call_n && st.p2p_n;) {
+        int e = i;
+        while (e < st.call_n && (cl[e].kind == XG_CALL_SEND || cl[e].kind == XG_CALL_RECV)) ++e;
+        if (e > i && (rc = rccl_group(
+                          e - i,
+                          [&](int k) {
+                              const xg_call &o = cl[i + k];
+                              uint8_t *ptr = p->reg->ptr[o.buf] + o.off;
+                              return o.kind == XG_CALL_SEND
+                                         ? ncclSend(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream)
+                                         : ncclRecv(ptr, (size_t)o.len, ncclUint8, o.peer, c->comm, c->stream);
+                          },
+                          st.groups > 1 ? "relay step exchange" : "step exchange")))
+            return rc;
+        i = e + 1;            // past the fence (or the barrier, which ends the list)
+    }
     if ((rc = enqueue_post(p, s, c->stream))) return rc;
     if (st.sync_after)   /* in-loop MPI_Barrier: every GPU finishes this step before any goes on */
         NCCLCHK(ncclAllReduce(c->d_red, c->d_red, 1, ncclFloat64, ncclMax, c->comm, c->stream));

@@ -122,3 +122,44 @@ extern "C" int xg_p2p_bench(xg_ctx *c, int64_t bytes, int mode, int reps, double
     return XG_OK;
 }
 
+
+extern "C" int xg_p2p_pair_bench(xg_ctx *c, int64_t bytes, int peer, int reps, double *gbps, double *sec)
+{
+    if (bytes <= 0 || reps < 1 || c->virt || !c->comm || peer >= c->nranks) return XG_EARG;
+    if (gbps) *gbps = 0;
+    if (sec) *sec = 0;
+    if (peer < 0 || peer == c->rank) return XG_OK;        // idle this round
+    HIPCHK(hipSetDevice(c->device));
+    DevMem m_sb, m_rb;
+    EventPair ev;
+    HIPCHK(hipMalloc(&m_sb.p, bytes));
+    HIPCHK(hipMalloc(&m_rb.p, bytes));
+    uint8_t *sb = m_sb.as<uint8_t>(), *rb = m_rb.as<uint8_t>();
+    HIPCHK(hipMemsetAsync(sb, c->rank & 0xff, bytes, c->stream));
+    HIPCHK(hipEventCreate(&ev.e[0]));
+    HIPCHK(hipEventCreate(&ev.e[1]));
+    auto one = [&]() -> int {
+        return rccl_group(
+            2,
+            [&](int i) {
+                return i == 0 ? ncclSend(sb, (size_t)bytes, ncclUint8, peer, c->comm, c->stream)
+                              : ncclRecv(rb, (size_t)bytes, ncclUint8, peer, c->comm, c->stream);
+            },
+            "xg_p2p_pair_bench");
+    };
+    int rc = XG_OK;
+    for (int w = 0; w < 2 && !rc; ++w) rc = one();          // connection set-up + warm-up
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventRecord(ev.e[0], c->stream));
+    for (int k = 0; k < reps && !rc; ++k) rc = one();
+    HIPCHK(hipEventRecord(ev.e[1], c->stream));
+    HIPCHK(hipEventSynchronize(ev.e[1]));
+    if (rc) return rc;
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ev.e[0], ev.e[1]));
+    const double s_rep = ms * 1e-3 / reps;
+    if (sec) *sec = s_rep;
+    if (gbps) *gbps = (double)bytes / s_rep / 1e9;
+    return XG_OK;
+}

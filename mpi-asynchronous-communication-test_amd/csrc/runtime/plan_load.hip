@@ -522,10 +522,15 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             xg_devplan_step_calls(dp, s, c->self_max, p->calls.data() + st.call_b);
             st.p2p_n = 0;
             st.sync_after = 0;
+            st.groups = 1;
             for (int i = 0; i < nc; ++i) {
                 const xg_call &o = p->calls[st.call_b + i];
                 if (o.kind == XG_CALL_BARRIER) {
                     st.sync_after = c->nranks > 1;
+                    continue;
+                }
+                if (o.kind == XG_CALL_FENCE) {        // a relay step's second RCCL group follows
+                    st.groups++;
                     continue;
                 }
                 if ((o.kind != XG_CALL_SEND && o.kind != XG_CALL_RECV) || o.peer < 0 || o.peer >= c->nranks ||

@@ -85,20 +85,26 @@ static int vplans_run(xg_plan *const *plans, int n, double *step_done, bool rccl
                     ends(pairs[q], &src, &dst);
                     if (pairs[q].len) HIPCHK(hipMemcpyAsync(dst, src, (size_t)pairs[q].len, hipMemcpyDeviceToDevice, st));
                 }
-            } else if (q1 > q0) {
+            } else {
                 where("xg_vplans_run_rccl", s, nst, "posting the RCCL group (ncclGroupEnd)");
-                // every pair of the step as a self send + receive in ONE group (issue order = pair order)
-                if ((rc = rccl_group(
-                         (int)(2 * (q1 - q0)),
-                         [&](int i) {
-                             uint8_t *src, *dst;
-                             const xg_call_pair &q = pairs[q0 + i / 2];
-                             ends(q, &src, &dst);
-                             return i % 2 == 0 ? ncclSend(src, (size_t)q.len, ncclUint8, 0, c0->comm, st)
-                                               : ncclRecv(dst, (size_t)q.len, ncclUint8, 0, c0->comm, st);
-                         },
-                         "virtual job step")))
-                    return rc;
+                // every pair of one group of the step (pairs come in (step, group) order; a relay
+                // step has two) as a self send + receive in ONE RCCL group (issue order = pair order)
+                for (size_t g0 = q0; g0 < q1;) {
+                    size_t g1 = g0;
+                    while (g1 < q1 && pairs[g1].group == pairs[g0].group) ++g1;
+                    if ((rc = rccl_group(
+                             (int)(2 * (g1 - g0)),
+                             [&](int i) {
+                                 uint8_t *src, *dst;
+                                 const xg_call_pair &q = pairs[g0 + i / 2];
+                                 ends(q, &src, &dst);
+                                 return i % 2 == 0 ? ncclSend(src, (size_t)q.len, ncclUint8, 0, c0->comm, st)
+                                                   : ncclRecv(dst, (size_t)q.len, ncclUint8, 0, c0->comm, st);
+                             },
+                             "virtual job step")))
+                        return rc;
+                    g0 = g1;
+                }
             }
             q0 = q1;
             for (int g = 0; g < n; ++g)

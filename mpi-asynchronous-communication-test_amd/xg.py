@@ -43,7 +43,7 @@ class Copy(C.Structure):
 
 class P2P(C.Structure):
     _fields_ = [("off", C.c_int64), ("len", C.c_int64), ("peer", C.c_int32), ("buf", C.c_int32),
-                ("is_send", C.c_int32), ("pad", C.c_int32)]
+                ("is_send", C.c_int32), ("group", C.c_int32)]
 
 
 class StepPlan(C.Structure):
@@ -68,7 +68,7 @@ class Call(C.Structure):
 
 class CallPair(C.Structure):
     _fields_ = [("step", C.c_int32), ("src", C.c_int32), ("dst", C.c_int32), ("send_call", C.c_int32),
-                ("recv_call", C.c_int32), ("pad", C.c_int32), ("len", C.c_int64)]
+                ("recv_call", C.c_int32), ("group", C.c_int32), ("len", C.c_int64)]
 
 
 CALL_SEND, CALL_RECV, CALL_BARRIER = 1, 2, 3
@@ -94,7 +94,8 @@ class Slot(C.Structure):
 
 A2M, M2A = 0, 1
 BUF_SEND, BUF_RECV, BUF_STAGE_SEND, BUF_STAGE_RECV, BUF_SCRATCH = 0, 1, 2, 3, 4
-PACK_TWO_SIDED, PACK_ONE_SIDED = 0, 1   # xg_devplan_build_form
+PACK_TWO_SIDED, PACK_ONE_SIDED, RELAY = 0, 1, 2   # xg_devplan_build_form (RELAY: xg_sched.h XG_RELAY)
+CALL_SEND, CALL_RECV, CALL_BARRIER, CALL_FENCE = 1, 2, 3, 4   # xg_call kinds
 MSG_COPY, MSG_COLL, MSG_CTRL = 1, 2, 4
 TAM_METHODS = (15, 16)
 MPICH_EAGER_LIMIT = 65424
@@ -240,7 +241,9 @@ def solo_reduce_stamps(stamps, s0, s1):
     return list(out)
 
 
-def _pairs(n, arr):
+def _pairs(n, arr, groups=False):
+    if groups:
+        return [(q.step, q.group, q.src, q.dst, q.send_call, q.recv_call, q.len) for q in arr[:n]]
     return [(q.step, q.src, q.dst, q.send_call, q.recv_call, q.len) for q in arr[:n]]
 
 
@@ -269,10 +272,10 @@ def calls_match(calls, nsteps):
     return _pairs(n, out)
 
 
-def devplans_match(plans, self_max=0):
+def devplans_match(plans, self_max=0, groups=False):
     """xg_devplans_match over the G device plans (DevicePlanView or raw POINTER(DevPlan)) of one
-    job (calls listed with self_max): the pairs, or XGError naming the first call that RCCL
-    would pair differently."""
+    job (calls listed with self_max): the pairs (groups: (step, group, src, dst, send_call,
+    recv_call, len)), or XGError naming the first call that RCCL would pair differently."""
     ptrs = [p.ptr if isinstance(p, DevicePlanView) else p for p in plans]
     G = len(ptrs)
     arr = (C.POINTER(DevPlan) * G)(*ptrs)
@@ -282,7 +285,7 @@ def devplans_match(plans, self_max=0):
         raise XGError(err.value.decode())
     out = (CallPair * max(1, n))()
     host().xg_devplans_match(arr, G, self_max, out, n, err, 512)
-    return _pairs(n, out)
+    return _pairs(n, out, groups)
 
 
 def piece_size(lens, chunk=32768, cus=256, wg_cost=2048):
@@ -444,7 +447,8 @@ class DevicePlanView:
         self.gpu, self.ngpus, self.nsteps = p.gpu, p.ngpus, p.nsteps
         self.region_bytes = list(p.region_bytes)
         self.copies = [(c.src_buf, c.src_off, c.dst_buf, c.dst_off, c.len) for c in p.copies[:p.ncopy]]
-        self.p2p = [(o.peer, o.is_send, o.buf, o.off, o.len) for o in p.p2p[:p.np2p]]
+        # (peer, is_send, region, offset, length, group): group 1 = a relay step's second RCCL group
+        self.p2p = [(o.peer, o.is_send, o.buf, o.off, o.len, o.group) for o in p.p2p[:p.np2p]]
         self.steps = [(s.pre_begin, s.pre_count, s.p2p_begin, s.p2p_count, s.post_begin, s.post_count)
                       for s in p.steps[:p.nsteps]]
         self.sync_after = [s.sync_after for s in p.steps[:p.nsteps]]
@@ -516,6 +520,13 @@ def device():
                           "(e.g. by `import torch`), not the one it is built against: load the framework "
                           "before torch, or in a process without it" % ", ".join(bad))
         d = _load("libxg.so")
+        # ... and after loading it: a foreign runtime found first on the library search path
+        # (LD_LIBRARY_PATH) binds libxg.so's own dependencies to it
+        d.xg_foreign_runtime.argtypes = [C.c_char_p, C.c_size_t]
+        buf = C.create_string_buffer(1024)
+        if d.xg_foreign_runtime(buf, 1024) > 0:
+            raise XGError("libxg.so is bound to a ROCm runtime from outside /opt/rocm (%s): refused"
+                          % buf.value.decode())
         vp, ip, i64 = C.c_void_p, C.c_int, C.c_int64
         d.xg_get_unique_id.argtypes = [vp]
         d.xg_init.argtypes = [C.POINTER(vp), ip, ip, ip, vp]
@@ -559,6 +570,8 @@ def device():
         d.xg_ktime_launch.argtypes = [vp, ip, C.POINTER(C.c_double), C.POINTER(i64)]
         d.xg_set_copy_params.argtypes = [vp, i64, ip]
         d.xg_p2p_bench.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        d.xg_p2p_pair_bench.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        d.xg_rccl_version.argtypes = [C.POINTER(C.c_int)]
         _dev = d
     return _dev
 
@@ -566,6 +579,13 @@ def device():
 def _check(rc, what):
     if rc != 0:
         raise XGError("%s failed with code %d (see stderr)" % (what, rc))
+
+
+def rccl_version():
+    """ncclGetVersion of the RCCL libxg.so runs on, e.g. 22703 (no GPU call)"""
+    v = C.c_int()
+    _check(device().xg_rccl_version(C.byref(v)), "xg_rccl_version")
+    return v.value
 
 
 def unique_id():
@@ -627,6 +647,12 @@ class Context:
     def p2p_bench(self, nbytes, mode=0, reps=20):
         g, sec = C.c_double(), C.c_double()
         _check(_dev.xg_p2p_bench(self._c, nbytes, mode, reps, C.byref(g), C.byref(sec)), "xg_p2p_bench")
+        return g.value, sec.value
+
+    def p2p_pair_bench(self, nbytes, peer, reps=10):
+        """one link, both directions at once, with `peer` (< 0: idle this round) -> (GB/s sent, s per rep)"""
+        g, sec = C.c_double(), C.c_double()
+        _check(_dev.xg_p2p_pair_bench(self._c, nbytes, peer, reps, C.byref(g), C.byref(sec)), "xg_p2p_pair_bench")
         return g.value, sec.value
 
     def ktime_begin(self, max_launches=4096, per_launch=True):

@@ -23,7 +23,7 @@ def make(real_xg):
     fake = types.ModuleType("xg")
     for name in ("aggregator_list", "Schedule", "XGError", "NBUF", "BUF_SEND", "BUF_RECV",
                  "BUF_STAGE_SEND", "BUF_STAGE_RECV", "BUF_SCRATCH", "PACK_TWO_SIDED", "PACK_ONE_SIDED",
-                 "method_label", "host"):
+                 "RELAY", "CALL_SEND", "CALL_RECV", "CALL_BARRIER", "CALL_FENCE", "method_label", "host"):
         setattr(fake, name, getattr(real_xg, name))
     calls = {"p2p_bench": 0, "ktime": [], "runs": 0}
     fake.calls = calls
@@ -45,6 +45,16 @@ def make(real_xg):
 
     def unique_id():
         return b"\x01" * 128
+
+    def _rccl_warn(msg):
+        """what RCCL would write under NCCL_DEBUG=WARN when a call fails: one line in this rank's
+        NCCL_DEBUG_FILE (bench.py attaches every rank's tail to a failed line)"""
+        f = os.environ.get("NCCL_DEBUG_FILE")
+        if f:
+            with open(f, "a") as fh:
+                fh.write("host:1:1 [0] NCCL WARN %s\n" % msg)
+
+    fake.rccl_version = lambda: 22703
 
     class Context:
         def __init__(self, rank=0, nranks=1, device=None, uid=None, device_index=None):
@@ -113,11 +123,22 @@ def make(real_xg):
             calls["p2p_bench"] += 1
             trace.append(["p2p_bench", int(nbytes), int(mode), int(reps)])
             if _on_fail_rank(self.rank) and (calls["p2p_bench"] - 1,) in _faults("XG_FAKE_P2P_FAIL"):
+                _rccl_warn("xg_p2p_bench: injected RCCL failure on rank %d" % self.rank)
                 raise real_xg.XGError("xg_p2p_bench failed with code 5 (injected)")
             if _on_fail_rank(self.rank) and (calls["p2p_bench"] - 1,) in _faults("XG_FAKE_P2P_HANG"):
                 while True:          # a peer lost inside RCCL: this call never returns
                     time.sleep(1)
             return 50.0, nbytes / 50e9
+
+        def p2p_pair_bench(self, nbytes, peer, reps=10):
+            calls["pair_bench"] = calls.get("pair_bench", 0) + 1
+            trace.append(["p2p_pair_bench", int(nbytes), int(reps)])     # the peer differs by rank (pair_rounds)
+            if _on_fail_rank(self.rank) and (calls["pair_bench"] - 1,) in _faults("XG_FAKE_PAIR_FAIL"):
+                _rccl_warn("xg_p2p_pair_bench: injected RCCL failure on rank %d" % self.rank)
+                raise real_xg.XGError("xg_p2p_pair_bench failed with code 2 (injected)")
+            if peer < 0:
+                return 0.0, 0.0
+            return 40.0 + peer + self.rank, nbytes / 40e9      # distinct per link: the spread is visible
 
         def close(self):
             pass

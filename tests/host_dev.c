@@ -401,13 +401,19 @@ int xg_plan_run(xg_plan *p, double *step_done, double *step_post, double *wall)
                 ++local_end;
         for (i = sp->pre_begin; i < sp->pre_begin + sp->pre_count; ++i)
             if (!self || i < sp->pre_begin + sp->stage_count || i >= local_end) copy(r, &dp->copies[i]);
-        for (i = 0; i < n && !rc; ++i)     /* the group: every send posted, then every receive */
-            if (calls[i].kind == XG_CALL_SEND)
-                rc = c->nranks == 1 ? XG_EARG   /* a one-GPU plan posts no calls */
-                                    : send_msg(c, calls[i].peer, r->p[calls[i].buf] + calls[i].off, calls[i].len);
+        for (int g0 = 0; g0 < n && !rc;) {   /* per group (a relay step: two, split by a fence) */
+            int g1 = g0;
+            while (g1 < n && calls[g1].kind != XG_CALL_FENCE && calls[g1].kind != XG_CALL_BARRIER) ++g1;
+            for (i = g0; i < g1 && !rc; ++i)     /* the group: every send posted, then every receive */
+                if (calls[i].kind == XG_CALL_SEND)
+                    rc = c->nranks == 1 ? XG_EARG   /* a one-GPU plan posts no calls */
+                                        : send_msg(c, calls[i].peer, r->p[calls[i].buf] + calls[i].off, calls[i].len);
+            for (i = g0; i < g1 && !rc; ++i)
+                if (calls[i].kind == XG_CALL_RECV)
+                    rc = recv_msg(c, calls[i].peer, r->p[calls[i].buf] + calls[i].off, calls[i].len);
+            g0 = g1 + 1;
+        }
         if (step_post) step_post[s] = xg_now() - t0;
-        for (i = 0; i < n && !rc; ++i)
-            if (calls[i].kind == XG_CALL_RECV) rc = recv_msg(c, calls[i].peer, r->p[calls[i].buf] + calls[i].off, calls[i].len);
         for (i = sp->post_begin; i < sp->post_begin + sp->post_count && !rc; ++i) copy(r, &dp->copies[i]);
         if (!rc && n && calls[n - 1].kind == XG_CALL_BARRIER) rc = xg_barrier(c);
         if (step_done) step_done[s] = xg_now() - t0;

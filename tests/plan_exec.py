@@ -67,19 +67,22 @@ def simulate(s, G, it=0, mode=0, pack=1 << 20, form=-1):
         for g in range(G):
             copies(regs[g], parts[g][0], "stage")
             copies(regs[g], parts[g][1], "pre")
-        for g in range(G):   # a recv of the group must not land on bytes a send of the group reads
-            ops = parts[g][2]
-            check_races([(o[2], o[3], o[2], o[3], o[4]) if o[1] else (-1, 0, o[2], o[3], o[4]) for o in ops], "p2p")
-        for g in range(G):
-            for p in range(G):
-                if p == g:
-                    continue
-                sends = [o for o in parts[g][2] if o[0] == p and o[1]]
-                recvs = [o for o in parts[p][2] if o[0] == g and not o[1]]
-                assert len(sends) == len(recvs), (st, g, p)
-                for (_, _, sb, so, sl), (_, _, rb, ro, rl) in zip(sends, recvs):
-                    assert sl == rl, (st, g, p)
-                    regs[p][rb][ro:ro + rl] = regs[g][sb][so:so + sl]
+        # the step's RCCL groups in order (a relay step: group 1 forwards what group 0 delivered)
+        for grp in sorted({o[5] for g in range(G) for o in parts[g][2]}):
+            for g in range(G):   # a recv of the group must not land on bytes a send of the group reads
+                ops = [o for o in parts[g][2] if o[5] == grp]
+                check_races([(o[2], o[3], o[2], o[3], o[4]) if o[1] else (-1, 0, o[2], o[3], o[4]) for o in ops],
+                            "p2p group %d" % grp)
+            for g in range(G):
+                for p in range(G):
+                    if p == g:
+                        continue
+                    sends = [o for o in parts[g][2] if o[0] == p and o[1] and o[5] == grp]
+                    recvs = [o for o in parts[p][2] if o[0] == g and not o[1] and o[5] == grp]
+                    assert len(sends) == len(recvs), (st, grp, g, p)
+                    for (_, _, sb, so, sl, _g), (_, _, rb, ro, rl, _h) in zip(sends, recvs):
+                        assert sl == rl, (st, grp, g, p)
+                        regs[p][rb][ro:ro + rl] = regs[g][sb][so:so + sl]
         for g in range(G):
             copies(regs[g], parts[g][3], "post")
     return views, regs

@@ -53,3 +53,42 @@ def test_device_library_refuses_a_foreign_rocm_runtime():
     for pre, want in (("", "loaded []"), ("import torch;", "refused")):
         out = subprocess.run([sys.executable, "-c", code % (REPO, pre)], capture_output=True, text=True, timeout=300)
         assert out.returncode == 0 and out.stdout.startswith(want), (pre, out.stdout, out.stderr[-1000:])
+
+
+def _foreign_hip(tmp_path):
+    """a copy of /opt/rocm's libamdhip64.so.7 outside the ROCm install: what the loader binds first
+    when LD_LIBRARY_PATH points at a directory holding one (torch's wheel bundles its own)"""
+    import shutil
+    d = tmp_path / "foreign"
+    d.mkdir()
+    shutil.copy("/opt/rocm/lib/libamdhip64.so.7", str(d))
+    return dict(os.environ, LD_LIBRARY_PATH=str(d))
+
+
+def test_cli_refuses_a_foreign_rocm_runtime(tmp_path):
+    """bin/test and bin/pt2pt_test link libxg.so directly: with another libamdhip64.so.7 first on
+    the search path they would run on it; xg_init refuses before any HIP call (xg_foreign_runtime)"""
+    import subprocess
+    env = _foreign_hip(tmp_path)
+    exe = os.path.join(PKG, "bin", "test")
+    out = subprocess.run([exe, "-m", "1", "-a", "2", "-d", "64", "--procs", "4"], capture_output=True, text=True,
+                         timeout=60, env=env, cwd=str(tmp_path))
+    assert out.returncode == 1 and "foreign ROCm runtime" in out.stderr, out.stderr[-2000:]
+    assert "max total time" not in out.stdout
+    pt = subprocess.run([os.path.join(PKG, "bin", "pt2pt_test"), "-d", "64", "-k", "1", "-i", "1"],
+                        capture_output=True, text=True, timeout=60, env=dict(env, XG_PT2PT_SELF="1"), cwd=str(tmp_path))
+    assert pt.returncode == 1 and "foreign ROCm runtime" in pt.stderr, pt.stderr[-2000:]
+
+
+def test_bench_refuses_a_foreign_rocm_runtime(tmp_path):
+    """bench.py (N = 1, no launcher) on a foreign runtime: libxg.so is refused after loading, the
+    line says why (value null) and the process exits 1 -- nothing is measured on another runtime"""
+    import json
+    import subprocess
+    import sys
+    env = _foreign_hip(tmp_path)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "1", "--warmup", "0",
+                          "--no-cpu-baseline"], capture_output=True, text=True, timeout=120, env=env, cwd=str(tmp_path))
+    assert out.returncode == 1, (out.stdout[-2000:], out.stderr[-2000:])
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["value"] is None and "outside /opt/rocm" in line["error"], line

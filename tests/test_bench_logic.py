@@ -50,8 +50,22 @@ def test_bench_multi_gpu_rank0_line(world, tmp_path):
     assert set(out["pack_autotune_ms_per_run"]) == {"1", "2", "3", "4"}
     forms = ("direct", "packed_one_sided", "packed_two_sided")
     for m, tune in out["pack_autotune_ms_per_run"].items():      # every form timed, the fastest kept
-        assert set(tune) == {f + "_ms" for f in forms} | {"chosen"}, tune
+        assert set(tune) == {f + "_ms" for f in forms} | {"chosen", "margin"}, tune
         assert tune["chosen"] in forms and tune[tune["chosen"] + "_ms"] == min(tune[f + "_ms"] for f in forms)
+        assert tune["margin"] is not None and tune["margin"] >= 0
+    # the self-diagnosing fields: RCCL's version, each phase's wall time, the per-link sweep
+    assert out["rccl_version"] == 22703 and "not xGMI" not in out["transport"]
+    pw = out["phase_wall_s"]
+    for ph in ("start", "RCCL communicator init (ncclCommInitRank, %d ranks)" % world, "methods: verify + plan choice",
+               "warm-up", "timed steps", "xGMI ceiling (RCCL all-pairs send/recv)", "xGMI p2p sweep",
+               "xGMI per-link sweep"):
+        assert ph in pw and pw[ph] >= 0, (ph, pw)
+    links = out["xgmi"]["links"]
+    assert out["xgmi"]["links_error"] is None and links["rounds"] == world - 1
+    assert all((links["GBps"][r][q] is None) == (r == q) for r in range(world) for q in range(world))
+    # (one process here: the MAX reduction holds this rank's row only; a real job's in the fault tests)
+    assert all(links["GBps"][0][q] == 40.0 + q for q in range(1, world)) and links["max"] == 40.0 + world - 1
+    assert "rccl_log_tail" not in out                 # nothing failed
     calls = json.loads([l for l in p.stdout.splitlines() if l.startswith("CALLS ")][0][6:])
     sweep = out["xgmi"]["sweep"]          # the pt2pt_test analogue: 1 -> 0 latency + all pairs, 4 sizes
     assert calls["p2p"] == 1 + len(sweep) == 9
@@ -82,6 +96,8 @@ def test_bench_single_gpu_line(tmp_path):
     assert p.returncode == 0, p.stderr[-2000:]
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
     assert out["n_gpus"] == 1 and out["xgmi"] is None
+    for key in ("phase_wall_s", "rccl_version", "transport", "rccl_log_tail", "cpu_baseline_configs"):
+        assert key not in out, key           # the N = 1 line is unchanged
     assert out["roofline"]["measured"].startswith("one HIP event pair")
     assert out["roofline"]["avg_launch_us"] * out["roofline"]["launches_per_step"] <= out["ms_per_step"] * 1e3 * 1.001
 
@@ -147,6 +163,8 @@ def test_bench_excludes_a_form_that_fails_verification_on_one_gpu(tmp_path):
     assert t1["chosen"] in ("direct", "packed_two_sided") and "packed_one_sided_ms" not in t1
     assert set(out["pack_autotune_ms_per_run"]["2"]) >= {"direct_ms", "packed_one_sided_ms", "packed_two_sided_ms"}
     assert out["value"] > 0 and out["xgmi"]["sweep"] and out["xgmi"]["sweep_error"] is None
+    links = out["xgmi"]["links"]          # both ranks' rows, through the real MAX reduction
+    assert links["GBps"] == [[None, 41.0], [41.0, None]] and links["spread"] == 1.0
 
 
 def test_bench_fails_with_a_line_when_every_form_of_a_method_fails(tmp_path):
@@ -171,6 +189,9 @@ def test_bench_survives_a_failing_ceiling_and_sweep(tmp_path):
     assert x["peak"] is None and x["frac"] is None and x["ceiling_error"] == "failed on another GPU"
     assert x["achieved"] > 0 and out["value"] > 0
     assert x["sweep_error"] == "all_pairs 1048576 B: failed on another GPU"
+    # GPU 1's RCCL warnings (its NCCL_DEBUG_FILE) are attached to rank 0's line
+    tail = out["rccl_log_tail"]
+    assert list(tail) == ["1"] and "injected RCCL failure on rank 1" in tail["1"][-1], tail
     assert [(r["mode"], r["bytes"]) for r in x["sweep"]] == [("one_way_1_to_0", 4096), ("all_pairs", 4096),
                                                              ("one_way_1_to_0", 65536), ("all_pairs", 65536),
                                                              ("one_way_1_to_0", 1 << 20)]
@@ -189,11 +210,17 @@ def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
     ex = out["baseline_configs_8gpu"]
     cells = ex["cells"]
     want = ["configs[2] m5", "configs[2] m8"] + ["configs[3] m%d" % m for m in (1, 2, 9, 10)] + \
+           ["configs[3] at -d 64 KiB m%d" % m for m in (1, 2, 9, 10)] + \
+           ["configs[4] -c %d at -d 4 KiB m%d" % (c, m) for c in (1, 8) for m in (7, 11, 12)] + \
            ["configs[4] -c %d m%d" % (c, m) for c in range(1, 9) for m in (7, 11, 12)]
     assert list(cells) == want
-    assert cells["configs[3] m9"].startswith("failed")
+    # every reference cell run on the host has a GPU cell of the same key (side_by_side)
+    import bench
+    assert {k for k, *_ in bench.CPU_CELLS} <= set(want)
+    assert cells["configs[3] m9"].startswith("failed") and cells["configs[3] at -d 64 KiB m9"].startswith("failed")
+    assert "injected" in str(out["rccl_log_tail"]) or out.get("rccl_log_tail") is None
     for k, v in cells.items():
-        if k != "configs[3] m9":
+        if k not in ("configs[3] m9", "configs[3] at -d 64 KiB m9"):
             assert v["verified"] and v["ms_per_run"] > 0 and v["GBps_cross_gpu"] > 0, (k, v)
     assert cells["configs[4] -c 1 m7"]["cross_gpu_bytes"] == 256 * 64 * (64 << 20) // 2   # half the pairs cross
     assert "error" not in ex and ex["spent_s"] >= 0
@@ -205,7 +232,7 @@ def test_bench_baseline_configs_phase_keeps_to_its_budget(tmp_path):
     assert rcs == [0, 0], [o[1][-1500:] for o in outs]
     out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
     cells = out["baseline_configs_8gpu"]["cells"]
-    assert len(cells) == 2 + 4 + 24 and all(str(v).startswith("skipped: phase budget") for v in cells.values())
+    assert len(cells) == 2 + 4 + 4 + 6 + 24 and all(str(v).startswith("skipped: phase budget") for v in cells.values())
 
 
 def test_bench_baseline_configs_phase_skips_a_configuration_that_does_not_fit(tmp_path):
@@ -218,9 +245,10 @@ def test_bench_baseline_configs_phase_skips_a_configuration_that_does_not_fit(tm
     out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
     cells = out["baseline_configs_8gpu"]["cells"]
     assert cells["configs[4] -c 1 m7"].startswith("failed: ")
-    rest = [k for k in cells if k.startswith("configs[4]") and k != "configs[4] -c 1 m7"]
+    stated = [k for k in cells if k.startswith("configs[4]") and "at -d" not in k]
+    rest = [k for k in stated if k != "configs[4] -c 1 m7"]
     assert len(rest) == 23 and all(cells[k] == "skipped: this configuration's regions did not fit" for k in rest)
-    assert all(cells[k]["verified"] for k in cells if not k.startswith("configs[4]"))
+    assert all(cells[k]["verified"] for k in cells if k not in stated)
 
 
 def test_bench_line_survives_a_hang_in_the_xgmi_phase(tmp_path):
@@ -267,3 +295,95 @@ def test_failed_communicator_init_still_prints_a_line(tmp_path):
     assert len(lines) == 1 and not [l for l in outs[1][0].splitlines() if l.startswith("{")]
     out = json.loads(lines[0])
     assert out["value"] is None and out["error"].startswith("device / RCCL init failed on rank 0 (RCCL communicator init")
+
+
+def test_measured_line_outlives_a_short_watchdog(tmp_path):
+    """the watchdog guards the road to the value only.  With --watchdog 6 and the sweep
+    hanging on GPU 1 under a 12 s xGMI budget, the watchdog (cancelled once the value is measured)
+    must not replace the line with a null one: the xGMI LineGuard prints the measured line, exit 0"""
+    argv = ARGV2 + ["--xgmi-budget", "12", "--no-ktime", "--watchdog", "6"]
+    rcs, outs = _run_job(2, argv, tmp_path, {"XG_FAKE_P2P_HANG": "2", "XG_FAKE_FAIL_RANK": "1"})
+    assert rcs == [0, 0], [o[1][-1500:] for o in outs]
+    out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+    assert out["value"] > 0 and out["xgmi_error"].startswith("still in phase 'xGMI p2p sweep' 12 s")
+    assert out["phase_wall_s"]["xGMI p2p sweep"] >= 0
+
+
+def test_pair_rounds_cover_every_link_once():
+    import bench
+    for n in range(2, 10):
+        seen = set()
+        rounds = bench.pair_rounds(n)
+        assert len(rounds) == (n - 1 if n % 2 == 0 else n)
+        for partner in rounds:
+            for r, q in enumerate(partner):
+                assert q == -1 or partner[q] == r
+                if q >= 0:
+                    assert (r, q) not in seen
+                    seen.add((r, q))
+        assert seen == {(r, q) for r in range(n) for q in range(n) if r != q}
+
+
+def test_wall_bound_of_the_driver_runs():
+    """the longest a rank of the driver's runs can take with every phase at its budget and every
+    guard firing: N = 1 the watchdog only; N = 8 under torch.distributed.run rank 0
+    runs both CPU phases first (the others allow for them), then watchdog + xGMI + BASELINE phases"""
+    import bench
+    sys.argv = ["bench.py"]
+    a = bench.parse()
+    assert bench.wall_bound(a, 1) == a.watchdog == 420
+    b8 = bench.wall_bound(a, 8)
+    assert b8 == a.cpu_budget + a.cpu_configs_budget + 45 + a.watchdog + a.xgmi_budget + a.baseline_budget + 45
+    assert b8 <= 1000, b8
+    # every guard fires after its phase's own budget, never before
+    assert bench.GUARD_GRACE > 0 and bench.pre_value_allowance(a, 1, 8, parent=True) == 0
+
+
+def test_cpu_baseline_configs_budget_and_schema(tmp_path):
+    """the reference itself at BASELINE's 8-GPU cells: a zero budget skips every cell; one real cell
+    (configs[2] m5 at full size, 64 MPI processes) when the reference build is here; side_by_side
+    pairs it with the GPU cell of the same key"""
+    import bench
+    sys.argv = ["bench.py", "--cpu-configs-budget", "0"]
+    a = bench.parse()
+    r = bench.cpu_baseline_configs(a)
+    assert list(r["cells"]) == [k for k, *_ in bench.CPU_CELLS] and len(r["cells"]) == 12
+    assert all(v.startswith("skipped: budget") for v in r["cells"].values())
+    if not os.path.exists(os.path.join(REPO, "oracle", "_ref", "test")):
+        pytest.skip("no reference build here")
+    sys.argv = ["bench.py", "--cpu-configs-budget", "100"]
+    a = bench.parse()
+    r = bench.cpu_baseline_configs(a, cells=bench.CPU_CELLS[:1])
+    c = r["cells"]["configs[2] m5"]
+    assert c["P"] == 64 and c["d"] == 256 << 10 and c["max_total_time_s"] > 0 and c["GBps_delivered"] > 0, c
+    out = {"cpu_baseline_configs": r,
+           "baseline_configs_8gpu": {"cells": {"configs[2] m5": {"max_total_time_s": c["max_total_time_s"] / 100}}}}
+    assert bench.side_by_side(out)["configs[2] m5"]["speedup"] == 100.0
+
+
+def test_link_sweep_failure_is_recorded_with_the_rccl_tail(tmp_path):
+    """an RCCL error on GPU 1 in the per-link sweep's second round: every rank stops the sweep at
+    that round, the line records links_error and the rounds before it, and GPU 1's RCCL warning"""
+    rcs, outs = _run_job(3, ["--gpus", "3", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--methods", "1"],
+                         tmp_path, {"XG_FAKE_PAIR_FAIL": "1", "XG_FAKE_FAIL_RANK": "1"})
+    assert rcs == [0, 0, 0], [o[1][-1500:] for o in outs]
+    out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+    x = out["xgmi"]
+    assert x["links"]["rounds"] >= 1 and x["links_error"].startswith("round ")
+    assert "1" in out["rccl_log_tail"] and "pair_bench" in out["rccl_log_tail"]["1"][-1]
+
+
+def test_bench_baseline_configs_time_the_relay_form_where_it_applies(tmp_path):
+    """a 4-GPU job with the BASELINE phase on: configs[3]'s pairwise m9 / m10 (permutation rounds of
+    >= 1 MiB per GPU pair) are verified and timed in the direct and the relay form and the faster is
+    kept; m1 / m2 (every GPU to every GPU) have one form only"""
+    argv = ["--gpus", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--methods", "1",
+            "--baseline-configs", "on", "--no-ktime"]
+    rcs, outs = _run_job(4, argv, tmp_path, {})
+    assert rcs == [0] * 4, [o[1][-1500:] for o in outs]
+    cells = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])["baseline_configs_8gpu"]["cells"]
+    for m in (9, 10):
+        c = cells["configs[3] m%d" % m]
+        assert set(c["forms"]) == {"direct", "relay"} and c["chosen"] in c["forms"] and c["verified"], c
+    for m in (1, 2):
+        assert "forms" not in cells["configs[3] m%d" % m]

@@ -200,7 +200,7 @@ def test_one_sided_moves_contiguous_runs_without_copies(xg):
         s = xg.Schedule(m, P, A, d, 200000000, rl)
         v0, v1 = (s.devplan(G, g, 4 << 20, 0, xg.PACK_ONE_SIDED) for g in range(G))
         assert _copied(v0) == _copied(v1) == (0, 0)
-        assert [o[1:] for o in v1.p2p] == [(1, 0, 0, 4 * d)]                      # SEND, offset 0
-        assert [o[1:] for o in v0.p2p] == [(0, 1, s.recv_offset(G, 0) + 4 * d, 4 * d)]
+        assert [o[1:5] for o in v1.p2p] == [(1, 0, 0, 4 * d)]                      # SEND, offset 0
+        assert [o[1:5] for o in v0.p2p] == [(0, 1, s.recv_offset(G, 0) + 4 * d, 4 * d)]
         _views, regs = simulate(s, G, it=0, mode=1, pack=4 << 20, form=xg.PACK_ONE_SIDED)
         check_recv(s, G, regs, it=0, mode=1)

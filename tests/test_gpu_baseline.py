@@ -140,14 +140,15 @@ def _check_strong(s, res, d, it, tag, sample=7):
 @pytest.mark.parametrize("method", [1, 2, 9, 10])
 def test_config3_full_size_virtual8(xg, world8, method):
     """configs[3] at full size (P256 A32 -d 4 MiB: 32 GiB per direction) as an 8-GPU job: the
-    cross-GPU pairs as device copies in RCCL's pairing for direct / one-sided / two-sided, and
-    through RCCL itself for the direct form"""
+    cross-GPU pairs as device copies in RCCL's pairing for direct / one-sided / two-sided / relay,
+    and through RCCL itself for the direct and relay forms"""
     P, A, d, it = 256, 32, 4 << 20, 1
     rl = xg.aggregator_list(P, A)
     s = xg.Schedule(method, P, A, d, 200000000, rl, ntimes=1, iteration=it)
-    regions = _shared_regions(xg, world8, [s], PACKINGS)
+    relay = (0, 2)           # XG_RELAY: m9 / m10's cross-GPU rounds over every link, two RCCL groups
+    regions = _shared_regions(xg, world8, [s], PACKINGS + (relay,))
     try:
-        for (pack, form), rccl in [(p, False) for p in PACKINGS] + [(PACKINGS[0], True)]:
+        for (pack, form), rccl in [(p, False) for p in PACKINGS + (relay,)] + [(PACKINGS[0], True), (relay, True)]:
             res = _run_job(xg, world8, s, it, 1, pack, form, rccl, regions)
             _check_strong(s, res, d, it, ("m%d" % method, pack, form, rccl))
     finally:

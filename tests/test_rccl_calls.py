@@ -18,6 +18,8 @@ CONFIGS = golden_configs()
 # direct (one call per segment), packed one-sided (runs; the default packed form), packed
 # two-sided (one staging buffer per peer and direction)
 PACKS = ((0, -1), (4 << 20, 1), (4 << 20, 0))
+# ... and the relay form (two RCCL groups in a permutation step; tests/test_relay.py)
+PACKS_RELAY = PACKS + ((0, 2),)
 
 
 def _ref_pairs(views):
@@ -51,7 +53,7 @@ def test_golden_jobs_pair_step_by_step(xg, cfg):
         s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], rl, ntimes=meta["ntimes"],
                         proc_node=meta["proc_node"], barrier_type=meta["barrier"])
         for G in range(2, min(8, meta["P"]) + 1):
-            for pack, form in PACKS:
+            for pack, form in PACKS_RELAY:
                 n = s.check_pairing(G, pack, 0, form)
                 views = [s.devplan(G, g, pack, 0, form) for g in range(G)]
                 assert n == sum(1 for v in views for st in range(v.nsteps) for c in v.calls(st) if c[0] == 1)
@@ -101,7 +103,7 @@ def test_baseline_configs_pair_on_2_to_8_gpus(xg, case):
         for c in cs:
             s = xg.Schedule(m, P, A, d, c, rl)
             for G in (2, 3, 4, 8):
-                for pack, form in PACKS:
+                for pack, form in PACKS_RELAY:
                     assert s.check_pairing(G, pack, 0, form) > 0
 
 

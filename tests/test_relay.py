@@ -1,0 +1,148 @@
+"""The relay form (XG_RELAY, sched.c relay_calls) on the CPU: a step whose cross-GPU messages form a
+permutation of the GPUs -- pairwise m9 / m10's XOR rounds (mpi_test.c:510-597, :421-508; partner
+rank ^ i at :531-545) -- sends every message over all G - 1 links of its source in two RCCL groups
+instead of over one link.  Every byte still lands where the reference puts it (race-checked CPU
+executor, oracle closed form), RCCL pairs the calls within one step AND one group, the other steps
+stay exactly the direct form's, and the busiest link of configs[3]'s pairwise rounds carries a
+quarter of what it carries direct (profiles/r05/link_load.txt)."""
+import pytest
+
+import xg_oracle as O
+from plan_exec import check_recv, simulate
+
+DIRECT, RELAY = (0, -1), (0, 2)
+SEND, RECV, BARRIER, FENCE = 1, 2, 3, 4
+
+
+@pytest.mark.parametrize("G, d", [(3, 1 << 20), (4, (1 << 20) + 48), (8, 1000003), (8, 1 << 20)])
+def test_relay_plans_deliver_every_byte(xg, G, d):
+    """P16 A8 (lists of >= 1 MiB per XOR round at every G), every method, collision-free
+    fingerprint; 16-B aligned cuts of an unaligned -d included"""
+    P, A = 16, 8
+    rl = xg.aggregator_list(P, A)
+    relayed = set()
+    for m in O.METHODS:
+        s = xg.Schedule(m, P, A, d, 3, rl, ntimes=1, iteration=1)
+        views, regs = simulate(s, G, it=1, mode=1, pack=RELAY[0], form=RELAY[1])
+        check_recv(s, G, regs, it=1, mode=1)
+        if any(o[5] == 1 for v in views for o in v.p2p):
+            relayed.add(m)
+    if d >= 1 << 20:                 # (one-message lists of less than XG_RELAY_MIN_BYTES stay direct)
+        assert {9, 10} <= relayed, relayed
+
+
+def _ref_group_pairs(views):
+    """independent restatement: in each step and each group of it (calls split at the fence), the
+    k-th send of g to h with the k-th receive of h from g -> {(step, group, g, h, len)} counts"""
+    from collections import Counter
+    G = len(views)
+    out = Counter()
+    for st in range(views[0].nsteps):
+        groups = []
+        for v in views:
+            gs, cur = [], []
+            for c in v.calls(st):
+                if c[0] == FENCE:
+                    gs.append(cur)
+                    cur = []
+                elif c[0] in (SEND, RECV):
+                    cur.append(c)
+            gs.append(cur)
+            groups.append(gs)
+        for q in range(max(len(x) for x in groups)):
+            for g in range(G):
+                for h in range(G):
+                    sends = [c for c in (groups[g][q] if q < len(groups[g]) else []) if c[0] == SEND and c[1] == h]
+                    recvs = [c for c in (groups[h][q] if q < len(groups[h]) else []) if c[0] == RECV and c[1] == g]
+                    assert len(sends) == len(recvs), (st, q, g, h)
+                    for a, b in zip(sends, recvs):
+                        assert a[4] == b[4], (st, q, g, h)
+                        out[(st, q, g, h, a[4])] += 1
+    return out
+
+
+@pytest.mark.parametrize("m", [9, 10, 12])
+def test_relay_pairs_by_step_and_group(xg, m):
+    from collections import Counter
+    P, A, d, G = 16, 8, 1 << 20, 8
+    s = xg.Schedule(m, P, A, d, 3, xg.aggregator_list(P, A), ntimes=1)
+    views = [s.devplan(G, g, RELAY[0], 0, RELAY[1]) for g in range(G)]
+    pairs = xg.devplans_match(views, groups=True)
+    got = Counter((st, grp, src, dst, ln) for st, grp, src, dst, _sc, _rc, ln in pairs)
+    assert got == _ref_group_pairs(views)
+    # pairs come in (step, group) order; a relay step's group 1 forwards what group 0 delivered
+    assert [(p[0], p[1]) for p in pairs] == sorted((p[0], p[1]) for p in pairs)
+    for v in views:
+        for st in range(v.nsteps):
+            c = v.calls(st)
+            assert [x[0] for x in c].count(FENCE) <= 1
+            if FENCE in [x[0] for x in c]:
+                f = [x[0] for x in c].index(FENCE)
+                assert all(x[0] in (SEND, RECV) for x in c[f + 1:] if x[0] != BARRIER)
+    if m in (9, 10):
+        assert any(p[1] == 1 for p in pairs)
+
+
+def test_relay_refused_when_a_pair_spans_two_groups(xg):
+    """the matcher's new rule: a send in a step's first group whose receive sits in the second
+    group is refused (the two groups are separate ncclGroupEnd launches: such a pair could wait
+    for a group its peer posts later)"""
+    S, R, F = SEND, RECV, FENCE
+    calls = [[[(S, 1, 0, 0, 8), (F, -1, -1, 0, 0)]],
+             [[(F, -1, -1, 0, 0), (R, 0, 1, 0, 8)]]]
+    with pytest.raises(xg.XGError) as e:
+        xg.calls_match(calls, 1)
+    assert "group 0, its receive in group 1" in str(e.value)
+    ok = [[[(S, 1, 0, 0, 8), (F, -1, -1, 0, 0), (S, 1, 0, 8, 8)]],
+          [[(R, 0, 1, 0, 8), (F, -1, -1, 0, 0), (R, 0, 1, 8, 8)]]]
+    assert len(xg.calls_match(ok, 1)) == 2
+
+
+def _busiest(views, xg):
+    """sum over steps and groups of the busiest directed link's bytes"""
+    tot = 0
+    for st in range(views[0].nsteps):
+        per = {}
+        for g, v in enumerate(views):
+            q = 0
+            for kind, peer, _b, _o, ln in v.calls(st):
+                if kind == FENCE:
+                    q += 1
+                elif kind == SEND and peer != g:
+                    per[(q, g, peer)] = per.get((q, g, peer), 0) + ln
+        for q in {k[0] for k in per}:
+            tot += max(b for k, b in per.items() if k[0] == q)
+    return tot
+
+
+@pytest.mark.parametrize("m", [9, 10])
+def test_relay_at_configs3_full_size(xg, m):
+    """configs[3] (P256 A32 -d 4 MiB) on 8 GPUs: the 224 cross-GPU XOR rounds are relayed, the 32
+    GPU-local ones are not; RCCL pairs every call; the busiest link carries 1/4 of the direct form's
+    bytes (3584 -> 896 MiB over the run: DESIGN.md's link-load table)"""
+    P, A, d, G = 256, 32, 4 << 20, 8
+    s = xg.Schedule(m, P, A, d, 200000000, xg.aggregator_list(P, A), ntimes=1)
+    assert s.check_pairing(G, RELAY[0], 0, RELAY[1]) > 0
+    relay = [s.devplan(G, g, RELAY[0], 0, RELAY[1]) for g in range(G)]
+    direct = [s.devplan(G, g, DIRECT[0], 0, DIRECT[1]) for g in range(G)]
+    steps = sum(1 for st in range(relay[0].nsteps) if FENCE in [c[0] for c in relay[0].calls(st)])
+    assert steps == 224
+    assert _busiest(direct, xg) == 3584 << 20 and _busiest(relay, xg) == 896 << 20
+    assert [v.remote_send_bytes for v in relay] == [v.remote_send_bytes for v in direct]
+    # relay staging: a relay holds one 1/8 piece of each of the 6 other sources' 16 MiB -> 12 MiB
+    assert max(v.region_bytes[3] for v in relay) == 12 << 20
+
+
+@pytest.mark.parametrize("m", [1, 2, 5, 7, 11])
+def test_relay_leaves_non_permutation_steps_direct(xg, m):
+    """steps where a GPU talks to several peers (unordered, alltoallw, half-sync) are the direct
+    form's, call for call; so are lists below XG_RELAY_MIN_BYTES (P16 A8 -d 64 KiB)"""
+    for P, A, d in ((16, 8, 1 << 20), (16, 8, 64 << 10)):
+        s = xg.Schedule(m, P, A, d, 3, xg.aggregator_list(P, A), ntimes=1)
+        for g in range(8):
+            r, dr = s.devplan(8, g, RELAY[0], 0, RELAY[1]), s.devplan(8, g, DIRECT[0], 0, DIRECT[1])
+            for st in range(r.nsteps):
+                if FENCE not in [c[0] for c in r.calls(st)]:
+                    assert r.calls(st) == dr.calls(st), (m, P, A, d, g, st)
+    s = xg.Schedule(9, 16, 8, 64 << 10, 3, xg.aggregator_list(16, 8), ntimes=1)
+    assert not any(o[5] for g in range(8) for o in s.devplan(8, g, RELAY[0], 0, RELAY[1]).p2p)
