@@ -552,7 +552,11 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                             v = sm.devplan(world, rank, f[0], 0, f[1])
                             need = [max(x, y) for x, y in zip(need, v.region_bytes)]
                     rk = (P, A, d)
-                    if rk not in regions:
+                    if rk not in regions or not regions[rk].fits(need):
+                        # a new configuration, or one whose -c needs more staging than the cells
+                        # before it (configs[4] at -d 4 KiB: -c 8 after -c 1): regions sized for both
+                        if rk in regions:
+                            need = [max(x, y) for x, y in zip(need, regions[rk].bytes)]
                         for old in regions.values():
                             old.close()
                         regions.clear()
@@ -686,8 +690,9 @@ def spawn_ranks(a):
     if "--no-cpu-baseline" not in argv:
         argv.append("--no-cpu-baseline")
     procs, outs = [], []
-    share = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "2")} \
-        if os.environ.get("XG_SHARE_GPU") == "1" else {}     # ranks sharing one GPU: runtime/ctx.hip
+    # ranks sharing one GPU (XG_SHARE_GPU=1, runtime/ctx.hip): 2 hardware queues each, whatever the
+    # environment says (the one-GPU boxes export HIP's default 4: 8 ranks x 4 queues time-slice)
+    share = {"GPU_MAX_HW_QUEUES": "2"} if os.environ.get("XG_SHARE_GPU") == "1" else {}
     for r in range(a.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
                    LOCAL_WORLD_SIZE=str(a.gpus), XG_RDZV_KEY=key, XG_BENCH_PARENT=str(os.getpid()), **share)

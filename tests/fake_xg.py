@@ -153,6 +153,8 @@ def make(real_xg):
                 sched.check_pairing(G, pack_max_seg, pack_min, pack_form,
                                     int(os.environ.get("XG_SELF_MAX", 256 << 10)))
             self.view = sched.devplan(G, g, pack_max_seg, pack_min, pack_form)
+            if regions is not None and not regions.fits(self.view.region_bytes):     # as the real MethodRun
+                raise real_xg.XGError("MethodRun: shared regions too small for this plan")
             # the RCCL calls this GPU's plan posts per run: per step its send/recv group and
             # its barrier (xg_devplan_step_calls), as a signature the ranks must agree on in
             # everything collective (the barriers) -- the p2p pairing is xg_devplans_match's

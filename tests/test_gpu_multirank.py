@@ -33,7 +33,7 @@ DIRECT, ONE_SIDED, TWO_SIDED, RELAY = [0, -1], [1 << 30, 1], [1 << 30, 0], [0, 2
 
 def _env(tmp_path, **kw):
     env = dict(os.environ, XG_SHARE_GPU="1", NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"),
-               XG_MR_DIR=str(tmp_path), GPU_MAX_HW_QUEUES=os.environ.get("GPU_MAX_HW_QUEUES", "2"))
+               XG_MR_DIR=str(tmp_path), GPU_MAX_HW_QUEUES="2")     # the box exports 4: 8 x 4 queues time-slice
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "XG_RDZV_KEY"):
         env.pop(k, None)
     env.update({k: str(v) for k, v in kw.items()})
@@ -41,34 +41,46 @@ def _env(tmp_path, **kw):
 
 
 def _wait_all(procs, timeout):
-    """wait for every process of the job; past `timeout` s end each one's session (its exact
-    process group) and fail with what each rank printed last"""
+    """wait for every process of the job (their output goes to files: a rank -- or its RCCL proxy
+    thread logging a warning -- blocked on a full pipe nobody reads would stall every rank in
+    RCCL); past `timeout` s end each one's session (its exact process group) and fail with what
+    each rank printed last.  procs: [(Popen, stdout path, stderr path)] -> [(stdout, stderr)]"""
     import time
-    outs, t0 = [], time.time()
+    t0 = time.time()
     try:
-        for p in procs:
-            outs.append(p.communicate(timeout=max(1.0, timeout - (time.time() - t0))))
+        for p, _o, _e in procs:
+            p.wait(timeout=max(1.0, timeout - (time.time() - t0)))
     except subprocess.TimeoutExpired:
-        for p in procs:
+        for p, _o, _e in procs:
             if p.poll() is None:
                 os.killpg(p.pid, signal.SIGKILL)
-        tails = []
-        for r, p in enumerate(procs):
-            out, err = p.communicate()
-            tails.append("rank %d: ...%s | stderr ...%s" % (r, (out or "")[-300:], (err or "")[-600:]))
+        for p, _o, _e in procs:
+            p.wait()
+        tails = ["rank %d: ...%s | stderr ...%s" % (r, open(o).read()[-300:], open(e).read()[-600:])
+                 for r, (p, o, e) in enumerate(procs)]
         pytest.fail("multi-rank job still running after %d s\n%s" % (timeout, "\n".join(tails)))
-    return outs
+    return [(open(o).read(), open(e).read()) for _p, o, e in procs]
+
+
+def _spawn(cmd, env, cwd, tag, tmp_path):
+    o, e = str(tmp_path / ("%s.out" % tag)), str(tmp_path / ("%s.err" % tag))
+    with open(o, "w") as fo, open(e, "w") as fe:
+        p = subprocess.Popen(cmd, env=env, cwd=cwd, stdout=fo, stderr=fe, text=True, start_new_session=True)
+    return p, o, e
 
 
 def _job(tmp_path, G, cases, timeout=120):
     """G worker processes over one RCCL communicator; -> rank 0's result lines"""
-    procs = [subprocess.Popen([sys.executable, "-u", WORKER, json.dumps(cases)],
-                              env=_env(tmp_path, RANK=r, WORLD_SIZE=G, LOCAL_RANK=r, XG_MR_DEADLINE=timeout - 10),
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    import pathlib
+    import tempfile
+    tmp_path = pathlib.Path(tempfile.mkdtemp(prefix="job", dir=str(tmp_path)))   # its own RCCL id file
+    procs = [_spawn([sys.executable, "-u", WORKER, json.dumps(cases)],
+                    _env(tmp_path, RANK=r, WORLD_SIZE=G, LOCAL_RANK=r, XG_MR_DEADLINE=timeout - 10), None,
+                    "rank%d" % r, tmp_path)
              for r in range(G)]
     outs = _wait_all(procs, timeout)
     failed = ["rank %d exit %d: %s" % (r, p.returncode, " | ".join(err.strip().splitlines()[-3:]))
-              for r, (p, (out, err)) in enumerate(zip(procs, outs)) if p.returncode]
+              for r, ((p, _o, _e), (out, err)) in enumerate(zip(procs, outs)) if p.returncode]
     assert not failed, "\n".join(failed)
     lines = [json.loads(x) for x in outs[0][0].splitlines() if x.startswith("{")]
     assert lines and lines[-1] == {"done": True}, outs[0]
@@ -146,10 +158,9 @@ def test_relay_form_as_multi_rank_job(tmp_path, G):
 def _cli(args, tmp_path, G, timeout=120, exe="test"):
     env = _env(tmp_path, XG_GPUS=G, XG_RDZV_DIR=tmp_path)
     (tmp_path / "cwd").mkdir(exist_ok=True)
-    p = subprocess.Popen([os.path.join(BIN, exe)] + [str(a) for a in args], cwd=tmp_path / "cwd", env=env,
-                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
-    (out, err), = _wait_all([p], timeout)
-    assert p.returncode == 0, err[-3000:]
+    job = _spawn([os.path.join(BIN, exe)] + [str(a) for a in args], env, str(tmp_path / "cwd"), exe, tmp_path)
+    (out, err), = _wait_all([job], timeout)
+    assert job[0].returncode == 0, err[-3000:]
     return out
 
 
@@ -189,11 +200,10 @@ def test_bench_line_from_a_real_two_rank_job(tmp_path):
     sweep, RCCL's version, each phase's wall time -- from a real 2-rank RCCL job, labelled as not
     xGMI (the transport is RCCL's sockets)"""
     env = _env(tmp_path)
-    p = subprocess.Popen([sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3",
-                          "--warmup", "1", "--no-cpu-baseline", "--baseline-configs", "off"], env=env, cwd=str(tmp_path),
-                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
-    (out, err), = _wait_all([p], 130)
-    assert p.returncode == 0, err[-3000:]
+    job = _spawn([sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                  "--no-cpu-baseline", "--baseline-configs", "off"], env, str(tmp_path), "bench", tmp_path)
+    (out, err), = _wait_all([job], 130)
+    assert job[0].returncode == 0, err[-3000:]
     line = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0 and "not xGMI" in line["transport"]
     assert line["rccl_version"] >= 22700 and line["roofline"]["launches"] > 0
