@@ -167,6 +167,9 @@ typedef struct {
     int32_t stage_count;              /* the first stage_count pre copies (rank-local
                                          memcpy's through SCRATCH) run in a launch of
                                          their own, ahead of the other pre copies     */
+    int32_t posts;                    /* request posts (Isend/Irecv/... ) the GPU's ranks
+                                         make in this step: a graph replay shares its
+                                         launch time out in proportion (xg_plan_run)  */
 } xg_stepplan;
 
 typedef struct {

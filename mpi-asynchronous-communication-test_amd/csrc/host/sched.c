@@ -1571,6 +1571,23 @@ static void count_posts(xg_sched *s, int ngpus)
     }
 }
 
+/* the request posts of GPU g's ranks per step (out[nsteps], zeroed here): what count_posts counts,
+ * for one GPU, without touching the schedule's cache (the device-plan builder takes it const) */
+static void step_posts_of(const xg_sched *s, int ngpus, int g, int32_t *out, int nout)
+{
+    int r, i, lo, hi;
+    memset(out, 0, sizeof(int32_t) * (size_t)nout);
+    xg_block_range(s->P, ngpus, g, &lo, &hi);
+    for (r = lo; r < hi; ++r) {
+        const prog_t *p = &s->progs[r];
+        for (i = 0; i < p->nops; ++i)
+            if (p->ops[i].kind == OP_SEND || p->ops[i].kind == OP_RECV) {
+                const int st = s->msgs[s->post_msg[r][p->ops[i].post]].step;
+                if (st >= 0 && st < nout) out[st]++;
+            }
+    }
+}
+
 static void set_field(xg_timer *t, int f, double v)
 {
     double *d = (double *)t;
@@ -2124,6 +2141,14 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
         goto done;
     }
     dp->gpu = g; dp->ngpus = G; dp->nsteps = nst;
+    {   /* per step, the request posts of this GPU's ranks (graph replays share their launch time
+         * out by them: xg_plan_run) */
+        int32_t *posts = (int32_t *)calloc((size_t)nst + 1, sizeof(int32_t));
+        if (!posts) { oom = 1; goto done; }
+        step_posts_of(s, G, g, posts, nst);
+        for (st = 0; st < nst; ++st) dp->steps[st].posts = posts[st];
+        free(posts);
+    }
     /* in-loop MPI_Barrier -> device-side barrier after the step it completes at (G > 1) */
     for (i = 0; i < s->nbarrier; ++i)
         if (G > 1 && s->barrier_epoch[i] >= 0 && s->barrier_epoch[i] < nst) dp->steps[s->barrier_epoch[i]].sync_after = 1;

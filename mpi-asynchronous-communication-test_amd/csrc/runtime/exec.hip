@@ -471,11 +471,16 @@ extern "C" int xg_plan_run(xg_plan *p, double *step_done, double *step_post, dou
         // the next eager launch must zero the state again
         p->engine_reset = true;
         if (step_post && p->nsteps > 0) {
-            // the whole run is posted by one graph launch: its host time is shared evenly over the
-            // steps, so each step (and each rank posting in it, xg_sched_rank_timer) keeps a share
-            // as under per-step enqueueing, and the shares sum to the launch time
-            const double tp = (xg_now() - t0) / p->nsteps;
-            for (int s = 0; s < p->nsteps; ++s) step_post[s] = tp;
+            // the whole run is posted by one graph launch: its host time is shared out over the
+            // steps in proportion to the request posts this GPU's ranks make in each
+            // (xg_stepplan.posts), so xg_sched_rank_timer credits all of it to the ranks that post
+            // -- no share lands on a step without posts, where no Timer would read it -- and the
+            // shares sum to the launch time (evenly over the steps if nothing is posted)
+            const double tl = xg_now() - t0;
+            int64_t tot = 0;
+            for (int s = 0; s < p->nsteps; ++s) tot += p->steps[s].posts;
+            for (int s = 0; s < p->nsteps; ++s)
+                step_post[s] = tot > 0 ? tl * p->steps[s].posts / (double)tot : tl / p->nsteps;
         }
     } else if ((rc = enqueue_run(p, step_post))) {
         return rc;

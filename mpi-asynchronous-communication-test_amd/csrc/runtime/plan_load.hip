@@ -523,6 +523,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
             st.p2p_n = 0;
             st.sync_after = 0;
             st.groups = 1;
+            st.posts = sp.posts;
             for (int i = 0; i < nc; ++i) {
                 const xg_call &o = p->calls[st.call_b + i];
                 if (o.kind == XG_CALL_BARRIER) {

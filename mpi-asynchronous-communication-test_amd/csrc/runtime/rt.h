@@ -169,6 +169,7 @@ struct StepR {
     // p2p_n of them are send/recv (one group), sync_after: the last is the in-loop barrier
     int stage_b, stage_n, local_b, local_n, pack_b, pack_n, post_b, post_n, call_b, call_n, p2p_n, sync_after;
     int groups;                      // RCCL groups of the step: 1, or 2 for a relay step (XG_CALL_FENCE between)
+    int posts;                       // request posts of this GPU's ranks in the step (xg_stepplan.posts)
     int pre_n;                       // local_n + pack_n
     int64_t stage_bytes, local_bytes, pack_bytes, post_bytes;   // bytes copied by each part (read + written once)
     bool split, fused, deferred;

@@ -49,7 +49,7 @@ class P2P(C.Structure):
 class StepPlan(C.Structure):
     _fields_ = [("pre_begin", C.c_int32), ("pre_count", C.c_int32), ("p2p_begin", C.c_int32),
                 ("p2p_count", C.c_int32), ("post_begin", C.c_int32), ("post_count", C.c_int32),
-                ("sync_after", C.c_int32), ("stage_count", C.c_int32)]
+                ("sync_after", C.c_int32), ("stage_count", C.c_int32), ("posts", C.c_int32)]
 
 
 class DevPlan(C.Structure):
@@ -453,6 +453,7 @@ class DevicePlanView:
                       for s in p.steps[:p.nsteps]]
         self.sync_after = [s.sync_after for s in p.steps[:p.nsteps]]
         self.stage_count = [s.stage_count for s in p.steps[:p.nsteps]]
+        self.posts = [s.posts for s in p.steps[:p.nsteps]]         # request posts of this GPU's ranks
         self.local_bytes = p.local_bytes
         self.remote_send_bytes = p.remote_send_bytes
         self.remote_recv_bytes = p.remote_recv_bytes

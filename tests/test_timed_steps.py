@@ -75,3 +75,32 @@ def test_readme_configuration_marks(xg):
         _check(xg, s, random.Random(m), m)
     assert got == {1: (11, 11), 2: (11, 11), 3: (11, 11), 4: (11, 11), 6: (38, 21), 7: (5, 5), 9: (32, 1),
                    10: (32, 1), 11: (22, 22), 12: (38, 29)}, got
+
+
+@pytest.mark.parametrize("cfg", ["readme_p32_a14", "p20_a6_c7", "p24_a7_t3_c1"])
+def test_graph_replay_post_time_reaches_every_post(xg, cfg):
+    """a graph replay posts the whole run in one launch; xg_plan_run shares that launch
+    time out over the steps in proportion to xg_stepplan.posts (the request posts of the GPU's
+    ranks in each step).  Then every post costs the same share, a step without posts gets none
+    (no Timer would read it), and for the methods whose post bracket holds all of a rank's posts
+    the GPU's ranks' post_request_time sum to the launch time exactly."""
+    meta, _, _ = load_golden(cfg)
+    whole = {1, 2, 4, 13, 14, 17, 18}            # post bracket around every request post
+    for m in meta["method_list"]:
+        s = xg.Schedule(m, meta["P"], meta["A"], meta["d"], meta["c"], meta["aggregators"], ntimes=meta["ntimes"],
+                        proc_node=meta["proc_node"], barrier_type=meta["barrier"])
+        for G in (1, 2, 4):
+            for g in range(G):
+                v = s.devplan(G, g)
+                tot = sum(v.posts)
+                lo, hi = s.block_range(G, g)
+                if not tot or hi <= lo:
+                    continue
+                T = 2.5e-5                                    # the replay's launch time
+                post = [T * x / tot for x in v.posts]         # exec.hip, graph branch of xg_plan_run
+                assert abs(sum(post) - T) < 1e-15 and all(p == 0 for p, x in zip(post, v.posts) if not x)
+                done = [0.0] * v.nsteps
+                got = sum(s.rank_timer(r, done, post, G).post_request_time for r in range(lo, hi))
+                assert got <= T * (1 + 1e-9), (cfg, m, G, g, got)
+                if m in whole:
+                    assert abs(got - T) < 1e-12, (cfg, m, G, g, got)
