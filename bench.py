@@ -690,9 +690,9 @@ def spawn_ranks(a):
     if "--no-cpu-baseline" not in argv:
         argv.append("--no-cpu-baseline")
     procs, outs = [], []
-    # ranks sharing one GPU (XG_SHARE_GPU=1, runtime/ctx.hip): 2 hardware queues each, whatever the
+    # ranks sharing one GPU (XG_SHARE_GPU=1, runtime/ctx.hip): 1 hardware queue each, whatever the
     # environment says (the one-GPU boxes export HIP's default 4: 8 ranks x 4 queues time-slice)
-    share = {"GPU_MAX_HW_QUEUES": "2"} if os.environ.get("XG_SHARE_GPU") == "1" else {}
+    share = {"GPU_MAX_HW_QUEUES": "1"} if os.environ.get("XG_SHARE_GPU") == "1" else {}
     for r in range(a.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
                    LOCAL_WORLD_SIZE=str(a.gpus), XG_RDZV_KEY=key, XG_BENCH_PARENT=str(os.getpid()), **share)

@@ -120,10 +120,10 @@ int xg_spawn_ranks(int ngpus, char **argv)
     double t_fail = 0;
     if (ngpus <= 1 || getenv("RANK") || getenv("WORLD_SIZE") || getenv("PMI_RANK") || getenv("PMI_SIZE")) return -1;
     snprintf(key, sizeof key, "spawn%ld_%ld", (long)getpid(), (long)time(NULL));
-    /* every rank on one device (XG_SHARE_GPU=1, runtime/ctx.hip): 2 hardware queues per process
+    /* every rank on one device (XG_SHARE_GPU=1, runtime/ctx.hip): 1 hardware queue per process
      * whatever the environment says (the one-GPU boxes export HIP's default 4), or the command
      * processor time-slices the ranks' queues (profiles/r05/share_gpu_queues/) */
-    if (getenv("XG_SHARE_GPU") && !strcmp(getenv("XG_SHARE_GPU"), "1")) setenv("GPU_MAX_HW_QUEUES", "2", 1);
+    if (getenv("XG_SHARE_GPU") && !strcmp(getenv("XG_SHARE_GPU"), "1")) setenv("GPU_MAX_HW_QUEUES", "1", 1);
     pid = (pid_t *)calloc(ngpus, sizeof(pid_t));
     st = (int *)calloc(ngpus, sizeof(int));
     for (r = 0; r < ngpus; ++r) {

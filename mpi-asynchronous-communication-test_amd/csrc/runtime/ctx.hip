@@ -19,12 +19,12 @@ extern "C" double xg_now(void)
 // one host ("Duplicate GPU detected"), so every rank names a host of its own (NCCL_HOSTID):
 // the ranks then pair over RCCL's network transport (sockets on loopback) instead of xGMI.
 // The calls, groups, pairing and collectives are the real multi-rank ones; the transport and
-// its rates are not the node's.  (More than ~16 hardware queues on the device -- 8 ranks x HIP's
-// default 4 -- and the command processor time-slices them: a README run of m9 took 0.79 s at 8
-// ranks against 9 ms with 2 queues per process, profiles/r05/share_gpu_queues/.  HIP reads
-// GPU_MAX_HW_QUEUES when it loads, so the launchers -- bench.py, xg_spawn_ranks, the tests --
-// set it to 2 for the processes they start on a shared device.)  Called before the first RCCL
-// call of the process.
+// its rates are not the node's.  (More than ~16 hardware queues on the device and the command
+// processor time-slices them: a README run of m9 took 0.79 s at 8 ranks x HIP's default 4 queues
+// against 9 ms at 2 (profiles/r05/share_gpu_queues/), and the 8-rank tests ran 4-7x slower once
+// the pytest process itself held 4 queues beside 8 x 2.  HIP reads GPU_MAX_HW_QUEUES when it
+// loads, so the launchers -- bench.py, xg_spawn_ranks, the tests -- give every process they start
+// on a shared device ONE queue.)  Called before the first RCCL call of the process.
 static void share_gpu_env(int rank)
 {
     const char *v = getenv("XG_SHARE_GPU");
