@@ -215,21 +215,24 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
  * (profiles/r03/pack_forms/), so it is the default; bench.py times direct, one-sided and
  * two-sided per method at N > 1 and keeps the fastest.  Any other form value means
  * XG_PACK_FORM_DEFAULT.  The alltoallw translate this replaces: mpi_test.c:233-302. */
-/*   XG_RELAY           no packing; a step whose cross-GPU traffic is a (partial) permutation of the
- *                      GPUs -- every GPU sends to at most one peer and receives from at most one, each
- *                      such list moving >= XG_RELAY_MIN_BYTES (pairwise m9 / m10: one XOR partner per
- *                      round) -- is sent over every link instead of one: each message is cut into G
- *                      16-B aligned pieces; pieces 0 and 1 go straight to the destination (piece 0 in
- *                      the step's first RCCL group, piece 1 in its second), piece 2 + i through relay
- *                      GPU R[i] (the G - 2 GPUs other than source and destination, ascending): received
- *                      into the relay's STAGE_RECV in the first group and forwarded to the destination
- *                      in the second.  Per link and group that is 1/G of the list instead of all of it
- *                      on one link: ~G/2 x less time per round at the link rate (link-load
- *                      table).  Other steps: direct.  No copy kernel touches a relayed byte. */
+/*   XG_RELAY           no packing; two-phase (Valiant) routing of the steps it pays for: each
+ *                      cross-GPU message of such a step is cut into G 16-B aligned pieces; pieces
+ *                      0 and 1 go straight to the destination (piece 0 in the step's first RCCL
+ *                      group, piece 1 in its second), piece 2 + i through relay GPU R[i] (the G - 2
+ *                      GPUs other than source and destination, ascending): received into the
+ *                      relay's STAGE_RECV in the first group, forwarded in the second.  Every link
+ *                      (a -> h) then carries egress(a) / G in group 0 and every link (h -> b)
+ *                      ingress(b) / G in group 1, whatever the traffic matrix.  A step is relayed
+ *                      when (max egress + max ingress) / G <= XG_RELAY_GAIN x its busiest GPU pair's
+ *                      bytes and every cross-GPU message is >= XG_RELAY_MIN_BYTES: pairwise m9 / m10
+ *                      (one XOR partner per round, 16 -> 4 MiB of link time per round at configs[3]),
+ *                      configs[4]'s half-sync m11.  Other steps: direct.  No copy kernel touches a
+ *                      relayed byte (link-load table). */
 enum { XG_PACK_TWO_SIDED = 0, XG_PACK_ONE_SIDED = 1, XG_RELAY = 2 };
 #define XG_PACK_FORM_DEFAULT XG_PACK_TWO_SIDED
 #define XG_RUN_CALL_BYTES (1 << 20)
 #define XG_RELAY_MIN_BYTES (1 << 20)
+#define XG_RELAY_GAIN 0.8
 xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
                                   int form);
 /* All three return NULL (nothing leaked) when the host runs out of memory while building: every

@@ -2024,29 +2024,42 @@ static void os_free(oneside *o)
     o->fail = fail;
 }
 
-/* ---- relay form (XG_RELAY, xg_sched.h).  A step is relayed when its cross-GPU messages form a
- * (partial) permutation of the GPUs -- every GPU sends to <= 1 peer and receives from <= 1 -- and
- * every such list moves >= XG_RELAY_MIN_BYTES: pairwise m9 / m10 (mpi_test.c:510-597, :421-508;
- * partner rank ^ i, :531-545) at configs[3] put every GPU's round on ONE of its 7 links.  Every GPU
- * decides from the same message list, so all agree. */
-static int relay_step(const xg_sched *s, const int *order, int b, int e, int G, int *to, int *from, int64_t *bytes)
+/* ---- relay form (XG_RELAY, xg_sched.h): two-phase (Valiant) routing of one step.  Every
+ * cross-GPU message is cut into G pieces: pieces 0 and 1 go straight to the destination (one per
+ * RCCL group), piece 2 + i through relay GPU R[i].  Then EVERY link (a -> h) carries egress(a) / G
+ * in the first group and every link (h -> b) ingress(b) / G in the second, whatever the step's
+ * traffic matrix: the step costs (max egress + max ingress) / G of link time instead of its
+ * busiest GPU pair's bytes.  A step is relayed when that is at most XG_RELAY_GAIN of the direct
+ * cost and every cross-GPU message is >= XG_RELAY_MIN_BYTES (smaller pieces are latency, not
+ * bandwidth).  Pairwise m9 / m10 (mpi_test.c:510-597, :421-508; partner rank ^ i, :531-545) at
+ * configs[3] put every GPU's 16 MiB round on ONE of its 7 links: 16 -> 4 MiB of link time per
+ * round.  Every GPU decides from the same message list, so all agree. */
+static int relay_step(const xg_sched *s, const int *order, int b, int e, int G, int64_t *egress, int64_t *ingress,
+                      int64_t *pair)
 {
     int k, g, any = 0;
+    int64_t direct = 0, emax = 0, imax = 0;
     if (G < 3) return 0;
-    for (g = 0; g < G; ++g) { to[g] = from[g] = -1; bytes[g] = 0; }
+    memset(egress, 0, sizeof(int64_t) * (size_t)G);
+    memset(ingress, 0, sizeof(int64_t) * (size_t)G);
+    memset(pair, 0, sizeof(int64_t) * (size_t)G * G);
     for (k = b; k < e; ++k) {
         const xg_msg *m = &s->msgs[order[k]];
         const int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
         if (!moves(m) || is_stage(m) || gs == gd) continue;
-        if ((to[gs] >= 0 && to[gs] != gd) || (from[gd] >= 0 && from[gd] != gs)) return 0;
-        to[gs] = gd;
-        from[gd] = gs;
-        bytes[gs] += m->len;
+        if (m->len < XG_RELAY_MIN_BYTES) return 0;
+        egress[gs] += m->len;
+        ingress[gd] += m->len;
+        pair[(size_t)gs * G + gd] += m->len;
         any = 1;
     }
-    for (g = 0; g < G; ++g)
-        if (to[g] >= 0 && bytes[g] < XG_RELAY_MIN_BYTES) return 0;
-    return any;
+    if (!any) return 0;
+    for (g = 0; g < G * G; ++g) direct = pair[g] > direct ? pair[g] : direct;
+    for (g = 0; g < G; ++g) {
+        emax = egress[g] > emax ? egress[g] : emax;
+        imax = ingress[g] > imax ? ingress[g] : imax;
+    }
+    return (double)(emax + imax) / G <= XG_RELAY_GAIN * (double)direct;
 }
 
 /* piece k of a relayed message of len bytes: [relay_cut(k), relay_cut(k + 1)), 16-B aligned cuts */
@@ -2127,14 +2140,14 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
     int *bucket_n = (int *)calloc((size_t)G * 2, sizeof(int));
     int64_t *bucket_b = (int64_t *)calloc((size_t)G * 2, sizeof(int64_t));
     oneside *os_out = (oneside *)calloc((size_t)G, sizeof(oneside)), *os_in = (oneside *)calloc((size_t)G, sizeof(oneside));
-    int *rl_to = (int *)calloc((size_t)G, sizeof(int)), *rl_from = (int *)calloc((size_t)G, sizeof(int));
-    int64_t *rl_b = (int64_t *)calloc((size_t)G, sizeof(int64_t));
+    int64_t *rl_e = (int64_t *)calloc((size_t)G, sizeof(int64_t)), *rl_i = (int64_t *)calloc((size_t)G, sizeof(int64_t));
+    int64_t *rl_p = (int64_t *)calloc((size_t)G * G, sizeof(int64_t));
     plan_bases pb;
     memset(&pre, 0, sizeof pre); memset(&post, 0, sizeof post); memset(&pp, 0, sizeof pp);
     memset(&pb, 0, sizeof pb);
     if (form != XG_PACK_TWO_SIDED && form != XG_PACK_ONE_SIDED && form != XG_RELAY) form = XG_PACK_FORM_DEFAULT;
     if (form == XG_RELAY) pack_max_seg = 0;         /* relay form: every other step is direct */
-    if (!dp || !cnt || !order || !pos || !bucket_n || !bucket_b || !os_out || !os_in || !rl_to || !rl_from || !rl_b ||
+    if (!dp || !cnt || !order || !pos || !bucket_n || !bucket_b || !os_out || !os_in || !rl_e || !rl_i || !rl_p ||
         plan_bases_init(&pb, s, G, g) ||
         !(dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan)))) {
         oom = 1;
@@ -2238,8 +2251,8 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
         /* the grouped exchange: per peer, sends then receives, message order */
         sp->p2p_begin = pp.n;
         sp->post_begin = post.n;
-        if (form == XG_RELAY && relay_step(s, order, b, e, G, rl_to, rl_from, rl_b)) {
-            /* a permutation step: every list over all G - 1 links of its source (two groups) */
+        if (form == XG_RELAY && relay_step(s, order, b, e, G, rl_e, rl_i, rl_p)) {
+            /* every message over all G - 1 links of its source, then of its destination (two groups) */
             relay_calls(s, &pb, order, b, e, G, g, &pp, &rbase);
             for (p = 0; p < G; ++p)
                 if (p != g) {
@@ -2371,7 +2384,7 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
     oom |= !dp->copies || !dp->p2p;
 done:
     free(pre.v); free(post.v); free(pp.v); free(cnt); free(order); free(pos); free(bucket_n); free(bucket_b);
-    free(os_out); free(os_in); free(rl_to); free(rl_from); free(rl_b);
+    free(os_out); free(os_in); free(rl_e); free(rl_i); free(rl_p);
     plan_bases_free(&pb);
     if (oom) {
         xg_devplan_free(dp);

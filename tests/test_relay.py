@@ -133,16 +133,42 @@ def test_relay_at_configs3_full_size(xg, m):
     assert max(v.region_bytes[3] for v in relay) == 12 << 20
 
 
-@pytest.mark.parametrize("m", [1, 2, 5, 7, 11])
-def test_relay_leaves_non_permutation_steps_direct(xg, m):
-    """steps where a GPU talks to several peers (unordered, alltoallw, half-sync) are the direct
-    form's, call for call; so are lists below XG_RELAY_MIN_BYTES (P16 A8 -d 64 KiB)"""
-    for P, A, d in ((16, 8, 1 << 20), (16, 8, 64 << 10)):
-        s = xg.Schedule(m, P, A, d, 3, xg.aggregator_list(P, A), ntimes=1)
-        for g in range(8):
-            r, dr = s.devplan(8, g, RELAY[0], 0, RELAY[1]), s.devplan(8, g, DIRECT[0], 0, DIRECT[1])
-            for st in range(r.nsteps):
-                if FENCE not in [c[0] for c in r.calls(st)]:
-                    assert r.calls(st) == dr.calls(st), (m, P, A, d, g, st)
-    s = xg.Schedule(9, 16, 8, 64 << 10, 3, xg.aggregator_list(16, 8), ntimes=1)
-    assert not any(o[5] for g in range(8) for o in s.devplan(8, g, RELAY[0], 0, RELAY[1]).p2p)
+def _relay_model(s, G, st_msgs):
+    """the relay decision restated: (max egress + max ingress) / G <= 0.8 x the busiest GPU pair,
+    every cross-GPU message >= 1 MiB (XG_RELAY_GAIN, XG_RELAY_MIN_BYTES)"""
+    eg, ig, pair = [0] * G, [0] * G, {}
+    for src, dst, ln in st_msgs:
+        a, b = s.gpu_of(G, src), s.gpu_of(G, dst)
+        if a == b or ln <= 0:
+            continue
+        if ln < 1 << 20:
+            return False
+        eg[a] += ln
+        ig[b] += ln
+        pair[(a, b)] = pair.get((a, b), 0) + ln
+    return bool(pair) and G >= 3 and (max(eg) + max(ig)) / G <= 0.8 * max(pair.values())
+
+
+@pytest.mark.parametrize("m", [1, 2, 5, 7, 9, 11, 12])
+@pytest.mark.parametrize("P, A, d", [(16, 8, 1 << 20), (16, 8, 64 << 10), (24, 6, 2 << 20)])
+def test_relay_decision_follows_the_link_model(xg, m, P, A, d):
+    """a step is relayed exactly when the two-phase link model beats the direct form's busiest GPU
+    pair by 20 % and its messages are >= 1 MiB; every other step is the direct form's, call for
+    call (unordered / alltoallw steps -- every GPU to every GPU -- stay direct: no gain there)"""
+    G = 8
+    s = xg.Schedule(m, P, A, d, 3, xg.aggregator_list(P, A), ntimes=1)
+    by_step = {}
+    for src, _ss, dst, _ds, ln, st, flags in s.messages():
+        if not flags & 4:
+            by_step.setdefault(st, []).append((src, dst, ln))
+    relay = [s.devplan(G, g, RELAY[0], 0, RELAY[1]) for g in range(G)]
+    direct = [s.devplan(G, g, DIRECT[0], 0, DIRECT[1]) for g in range(G)]
+    for st in range(relay[0].nsteps):
+        want = _relay_model(s, G, by_step.get(st, []))
+        for g in range(G):
+            got = FENCE in [c[0] for c in relay[g].calls(st)]
+            assert got == want, (m, P, A, d, st, g)
+            if not got:
+                assert relay[g].calls(st) == direct[g].calls(st), (m, st, g)
+    if d < 1 << 20:
+        assert not any(o[5] for v in relay for o in v.p2p)
