@@ -476,7 +476,8 @@ BASELINE_CELLS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
                    ("configs[3]", 256, 32, 4 << 20, 200000000, (1, 2, 9, 10)),
                    ("configs[3] at -d 64 KiB", 256, 32, 64 << 10, 200000000, (1, 2, 9, 10))] +
                   [("configs[4] -c %d at -d 4 KiB" % c, 256, 64, 4 << 10, c, (7, 11, 12)) for c in (1, 8)] +
-                  [("configs[4] -c %d" % c, 256, 64, 64 << 20, c, (7, 11, 12)) for c in range(1, 9)])
+                  # the sweep's ends first: a budget that runs out mid-sweep still leaves -c 1 and 8
+                  [("configs[4] -c %d" % c, 256, 64, 64 << 20, c, (7, 11, 12)) for c in (1, 8, 2, 3, 4, 5, 6, 7)])
 
 
 def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_CELLS):

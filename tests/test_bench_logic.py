@@ -212,7 +212,7 @@ def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
     want = ["configs[2] m5", "configs[2] m8"] + ["configs[3] m%d" % m for m in (1, 2, 9, 10)] + \
            ["configs[3] at -d 64 KiB m%d" % m for m in (1, 2, 9, 10)] + \
            ["configs[4] -c %d at -d 4 KiB m%d" % (c, m) for c in (1, 8) for m in (7, 11, 12)] + \
-           ["configs[4] -c %d m%d" % (c, m) for c in range(1, 9) for m in (7, 11, 12)]
+           ["configs[4] -c %d m%d" % (c, m) for c in (1, 8, 2, 3, 4, 5, 6, 7) for m in (7, 11, 12)]
     assert list(cells) == want
     # every reference cell run on the host has a GPU cell of the same key (side_by_side)
     import bench
