@@ -11,6 +11,8 @@ gcc -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-re
     "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/hazard.c" "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/solo.c" \
     "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/calls.c" "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/pieces.c"
 cd "$REPO/tests"
-LD_PRELOAD="$(gcc -print-file-name=libasan.so) $(gcc -print-file-name=libubsan.so)" ASAN_OPTIONS=detect_leaks=0 \
-    XG_LIBDIR="$OUT" python -m pytest test_host_sched.py test_devplan.py test_oracle.py test_engine_hazards.py test_hbm_fit.py test_solo_tables.py test_rccl_calls.py test_baseline_golden.py test_timed_steps.py -q -s -m "not gpu" -p no:cacheprovider
+# the sanitizer runtimes go first in LD_PRELOAD (ASan must be the first DSO); whatever the
+# environment already preloads stays after them
+LD_PRELOAD="$(gcc -print-file-name=libasan.so) $(gcc -print-file-name=libubsan.so)${LD_PRELOAD:+ $LD_PRELOAD}" ASAN_OPTIONS=detect_leaks=0 \
+    XG_LIBDIR="$OUT" python -m pytest test_host_sched.py test_devplan.py test_oracle.py test_engine_hazards.py test_hbm_fit.py test_solo_tables.py test_rccl_calls.py test_relay.py test_baseline_golden.py test_timed_steps.py -q -s -m "not gpu" -p no:cacheprovider
 rm -rf "$OUT"
