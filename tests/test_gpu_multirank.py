@@ -212,3 +212,28 @@ def test_bench_line_from_a_real_two_rank_job(tmp_path):
     assert x["peak"] > 0 and x["ceiling_error"] is None and x["sweep_error"] is None and len(x["sweep"]) == 8
     assert x["links"]["rounds"] == 1 and x["links"]["GBps"][0][1] > 0 and x["links"]["GBps"][1][0] > 0
     assert set(line["phase_wall_s"]) >= {"timed steps", "xGMI per-link sweep"}
+
+
+def test_bench_line_under_torchrun_launch_form(tmp_path):
+    """the driver's own N > 1 command form -- python -m torch.distributed.run --nnodes=1
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P bench.py --gpus 2 ... -- with both
+    ranks on this GPU: rank 0 runs the reference's CPU baseline before it touches the GPU and writes
+    the RCCL id, rank 1 waits for it (its watchdog allowing for rank 0's CPU phase), and rank 0 prints
+    the one line (the launcher imports torch in its agent process only; no rank does)"""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = _env(tmp_path)
+    job = _spawn([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                  "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                  "--gpus", "2", "--steps", "3", "--warmup", "1", "--baseline-configs", "off", "--cpu-reps", "2"],
+                 env, str(tmp_path), "torchrun", tmp_path)
+    (out, err), = _wait_all([job], 140)
+    assert job[0].returncode == 0, err[-3000:]
+    lines = [x for x in out.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0 and "not xGMI" in line["transport"]
+    assert line["cpu_baseline"]["kind"] in ("reference", "port") and line["xgmi"]["links"]["rounds"] == 1
+    assert "cpu baseline" in line["phase_wall_s"]
