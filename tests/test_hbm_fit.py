@@ -2,7 +2,8 @@
 
 configs[4] (P256 A64 -d 64 MiB, -c 1..8, m7/m11/m12) is the largest: on 8 GPUs each
 GPU holds 32 ranks' send segments (128 GiB) and 8 aggregators' receive slots
-(128 GiB); the per-peer staging buffers must not push that past one MI355X's 288 GB.
+(128 GiB); the per-peer staging buffers -- and the relay form's forwarding staging (<= 1.5 GiB
+at m11 -c 8) -- must not push that past one MI355X's 288 GB.
 """
 import pytest
 
@@ -20,13 +21,13 @@ def test_per_gpu_regions_fit_288gb(xg, case):
     for m in methods:
         for c in cs:
             s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
-            for pack in (0, 4 << 20):
+            for pack, form in ((0, -1), (4 << 20, -1), (0, 2)):      # direct, packed, relay
                 tot = 0
                 for g in range(8):
-                    v = s.devplan(8, g, pack)
+                    v = s.devplan(8, g, pack, 0, form)
                     need = sum(v.region_bytes)
                     # plan tables: <= 24 B per 32 KiB piece, 32 B per RCCL op
                     need += 24 * (sum(x[4] for x in v.copies) // 32768 + len(v.copies)) + 32 * len(v.p2p)
-                    assert need < HBM, (m, c, pack, g, need)
+                    assert need < HBM, (m, c, pack, form, g, need)
                     tot += v.region_bytes[0] + v.region_bytes[1]
                 assert tot == 2 * P * A * d          # every segment and slot lives on exactly one GPU
