@@ -134,12 +134,15 @@ def test_baseline_shapes_as_eight_rank_job(tmp_path):
 @pytest.mark.parametrize("cfg", ["cfg1_p32_a14_d1m", "cfg2_p64_a16_d256k"])
 def test_bench_workloads_as_two_and_four_rank_jobs(tmp_path, cfg):
     """the bench's own N = 2 / 4 workloads (configs[1]) and configs[2]'s shape, both packed forms
-    too, against the reference's checksums"""
+    too (and the relay form at configs[1], 4 ranks), against the reference's checksums"""
     from conftest import load_baseline
-    methods = load_baseline(cfg)[0]["method_list"]
+    meta = load_baseline(cfg)[0]
+    methods = meta["method_list"]
     for G in (2, 4):
-        rows = _job(tmp_path, G, [{"golden": "baseline/" + cfg, "forms": [DIRECT, ONE_SIDED, TWO_SIDED]}])
-        _assert_exact(rows, 3 * len(methods))
+        # configs[1]'s 1 MiB segments: at 4 ranks the relay form reroutes m9 / m10's XOR rounds
+        forms = [DIRECT, ONE_SIDED, TWO_SIDED] + ([RELAY] if G > 2 and meta["d"] >= 1 << 20 else [])
+        rows = _job(tmp_path, G, [{"golden": "baseline/" + cfg, "forms": forms}])
+        _assert_exact(rows, len(forms) * len(methods))
 
 
 @pytest.mark.parametrize("G", [4, 8])
