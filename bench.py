@@ -315,10 +315,14 @@ def cpu_baseline(a, methods):
 # configs[2] at its stated size, configs[3]'s shape at -d 64 KiB, configs[4]'s at -d 4 KiB for -c 1
 # and 8 (64 MiB would be 1 TiB per direction in host RAM); the same keys as the GPU cells at the
 # same -d in baseline_configs_8gpu, so the two sit side by side
+_C3 = [("configs[3] at -d 64 KiB m%d" % m, 256, 32, 64 << 10, 200000000, m) for m in (1, 9, 2, 10)]
+_C4 = [("configs[4] -c %d at -d 4 KiB m%d" % (c, m), 256, 64, 4 << 10, c, m) for c, m in
+       ((1, 7), (8, 12), (1, 11), (8, 7), (1, 12), (8, 11))]
+# configs[2] first, then configs[3] and [4] cell by cell in turn: each 256-process mpiexec costs
+# ~1 min of start-up on a 16-CPU box (profiles/r05/torchrun8_shared_gpu/), so a budget that runs
+# out still leaves each configuration measured
 CPU_CELLS = ([("configs[2] m%d" % m, 64, 16, 256 << 10, 200000000, m) for m in (5, 8)] +
-             [("configs[3] at -d 64 KiB m%d" % m, 256, 32, 64 << 10, 200000000, m) for m in (1, 2, 9, 10)] +
-             [("configs[4] -c %d at -d 4 KiB m%d" % (c, m), 256, 64, 4 << 10, c, m) for c in (1, 8)
-              for m in (7, 11, 12)])
+             [x for pair in zip(_C3 + [None] * 2, _C4) for x in pair if x])
 
 
 def cpu_configs_on(a, world):
