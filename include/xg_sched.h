@@ -208,7 +208,7 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
  *                      slots; only the runs not contiguous on the other side are staged, by
  *                      the sender (or the receiver) -- each byte copied on one side at most.
  *                      Of the two orders the one with fewer copied bytes + XG_RUN_CALL_BYTES
- *                      per call; ties: destination order (sched.c, oneside).
+ *                      per call; ties: destination order (devplan.c, oneside).
  * One-sided halves the copied bytes but posts more calls (configs[2] on 8 GPUs: 2 per peer and
  * direction instead of 1).  On one MI355X, where a virtual 8-GPU job moves every pair as an
  * RCCL self send/recv and those serialize at ~3 us per call, two-sided is the faster form

@@ -1,0 +1,644 @@
+/*
+ * devplan.c -- the per-GPU device plan of a compiled schedule (xg_devplan_build_form): per step,
+ * the GPU's local copies, packs into per-peer staging, its RCCL calls in the direct, packed
+ * one-sided / two-sided or relay form, and unpacks.  Plain C99, no HIP.  See include/xg_sched.h;
+ * the calls each step posts and their pairing proof are calls.c.
+ */
+#include "sched_int.h"
+
+#include <limits.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ device plan */
+/* Growable arrays of the device-plan builder.  The builder runs on every rank of a job and
+ * must not stop one rank alone: when the host runs out of memory, a push lands in `sink` and
+ * `fail` is set; xg_devplan_build_form then frees what it built and returns NULL, which the
+ * caller turns into an error every rank agrees on (methods.c peers_agree). */
+typedef struct { xg_copy *v; int n, cap, fail; xg_copy sink; } cvec;
+typedef struct { xg_p2p *v; int n, cap, fail; xg_p2p sink; } pvec;
+static xg_copy *cpush(cvec *c)
+{
+    if (c->n == c->cap) {
+        const int cap = c->cap ? 2 * c->cap : 256;
+        xg_copy *v = c->fail ? NULL : (xg_copy *)realloc(c->v, sizeof(xg_copy) * cap);
+        if (!v) { c->fail = 1; memset(&c->sink, 0, sizeof c->sink); return &c->sink; }
+        c->v = v; c->cap = cap;
+    }
+    memset(&c->v[c->n], 0, sizeof(xg_copy));
+    return &c->v[c->n++];
+}
+static xg_p2p *ppush(pvec *c)
+{
+    if (c->n == c->cap) {
+        const int cap = c->cap ? 2 * c->cap : 256;
+        xg_p2p *v = c->fail ? NULL : (xg_p2p *)realloc(c->v, sizeof(xg_p2p) * cap);
+        if (!v) { c->fail = 1; memset(&c->sink, 0, sizeof c->sink); return &c->sink; }
+        c->v = v; c->cap = cap;
+    }
+    memset(&c->v[c->n], 0, sizeof(xg_p2p));
+    return &c->v[c->n++];
+}
+
+void xg_devplan_free(xg_devplan *p)
+{
+    if (!p) return;
+    free(p->copies); free(p->p2p); free(p->steps); free(p);
+}
+
+/* same decision on both ends of a (step, src gpu, dst gpu) transfer list: >= 2 segments, mean
+ * below pack_max_seg, and at least pack_min bytes (below that one RCCL call per segment costs
+ * less than the pack and unpack launches) */
+static int use_pack(int n, int64_t total, int64_t pack_max_seg, int64_t pack_min)
+{
+    return pack_max_seg > 0 && n >= 2 && total / n < pack_max_seg && total >= pack_min;
+}
+
+/* region base of every rank hosted by the GPU the plan is for */
+typedef struct { int64_t *base[XG_NBUF]; } plan_bases;
+
+/* -> 0, or -1 when the host is out of memory (pb is then freeable) */
+static int plan_bases_init(plan_bases *pb, const xg_sched *s, int G, int g)
+{
+    int lo, hi, r, k, fail = 0;
+    int64_t scr = 0;
+    (void)g;
+    for (k = 0; k < XG_NBUF; ++k) fail |= !(pb->base[k] = (int64_t *)calloc(s->P + 1, sizeof(int64_t)));
+    if (fail) return -1;
+    for (r = 0; r < s->P; ++r) {
+        pb->base[XG_BUF_SEND][r] = xg_send_offset(s, G, r);
+        pb->base[XG_BUF_RECV][r] = xg_recv_offset(s, G, r);
+    }
+    for (k = 0; k < G; ++k) {
+        xg_block_range(s->P, G, k, &lo, &hi);
+        for (scr = 0, r = lo; r < hi; ++r) { pb->base[XG_BUF_SCRATCH][r] = scr; scr += s->scr_size[r]; }
+    }
+    return 0;
+}
+
+static void plan_bases_free(plan_bases *pb)
+{
+    int k;
+    for (k = 0; k < XG_NBUF; ++k) free(pb->base[k]);
+}
+
+static int64_t src_off(const plan_bases *pb, const xg_msg *m) { return pb->base[m->sbuf][m->src] + m->soff; }
+static int64_t dst_off(const plan_bases *pb, const xg_msg *m) { return pb->base[m->dbuf][m->dst] + m->doff; }
+
+/* a message that moves device bytes (not a size message, not empty) */
+static int moves(const xg_msg *m) { return m->len > 0 && !(m->flags & XG_MSG_CTRL); }
+
+/* a rank-local memcpy through a TAM aggregation buffer */
+static int is_stage(const xg_msg *m)
+{
+    return (m->flags & XG_MSG_COPY) && (m->sbuf == XG_BUF_SCRATCH || m->dbuf == XG_BUF_SCRATCH);
+}
+
+static void local_copy(xg_copy *c, const plan_bases *pb, const xg_msg *m)
+{
+    c->src_buf = m->sbuf; c->src_off = src_off(pb, m);
+    c->dst_buf = m->dbuf; c->dst_off = dst_off(pb, m);
+    c->len = m->len;
+}
+
+xg_devplan *xg_devplan_build(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg)
+{
+    return xg_devplan_build_form(s, ngpus, g, pack_max_seg, 0, XG_PACK_FORM_DEFAULT);
+}
+
+xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min)
+{
+    return xg_devplan_build_form(s, ngpus, g, pack_max_seg, pack_min, XG_PACK_FORM_DEFAULT);
+}
+
+/* One-sided form of one packed (step, src GPU -> dst GPU) transfer list (XG_PACK_ONE_SIDED).
+ * The messages are put in destination order (by_src = 0) or source order (by_src = 1) and
+ * merged into RUNS, each contiguous on that side: one RCCL call per run.  A run that is
+ * contiguous on the other side as well moves straight between the regions; any other one is
+ * gathered into staging by the sender (destination order) or scattered out of it by the
+ * receiver (source order) -- so every byte is copied on ONE side at most, where the two-sided
+ * form packs and unpacks all of them.  This is the transpose the alltoallw datatypes of m5/m8
+ * describe (mpi_test.c:233-302): e.g. all-to-many at P64 A16 on 8 GPUs, per peer the 16
+ * segments of 8 senders for 2 aggregators -- 2 runs of 2 MiB, one per aggregator's receive
+ * slots, gathered on the sending GPU; nothing is unpacked.  Of the two orders the one with
+ * fewer copied bytes + XG_RUN_CALL_BYTES per call wins (ties: destination order).  Both GPUs
+ * of the pair derive it from the same message list, so their calls pair one to one. */
+typedef struct {
+    int n, nrun, by_src, fail;   /* fail: out of host memory (the plan is discarded) */
+    int *idx;                 /* message indices, run order */
+    int *run_b;               /* run r = idx[run_b[r] .. run_b[r + 1]) */
+    unsigned char *staged;    /* run r goes through staging */
+} oneside;
+
+static const xg_msg *os_msg(const xg_sched *s, const oneside *o, int i) { return &s->msgs[o->idx[i]]; }
+
+typedef struct { int64_t off; int32_t buf, idx; } os_key;
+static int os_cmp(const void *a, const void *b)
+{
+    const os_key *x = (const os_key *)a, *y = (const os_key *)b;
+    if (x->buf != y->buf) return x->buf < y->buf ? -1 : 1;
+    if (x->off != y->off) return x->off < y->off ? -1 : 1;
+    return x->idx < y->idx ? -1 : x->idx > y->idx;      /* equal addresses: message order */
+}
+
+/* runs of `o` in the order by_src; returns the cost (copied bytes + calls) */
+static int64_t os_layout(const xg_sched *s, const plan_bases *pb, oneside *o, int by_src)
+{
+    int i, r;
+    int64_t cost = 0;
+    os_key *key = (os_key *)malloc(sizeof(os_key) * ((size_t)o->n + 1));
+    o->by_src = by_src;
+    if (!key) {
+        o->fail = 1;
+        o->nrun = 0;
+        return 0;
+    }
+    for (i = 0; i < o->n; ++i) {
+        const xg_msg *m = os_msg(s, o, i);
+        key[i].buf = by_src ? m->sbuf : m->dbuf;
+        key[i].off = by_src ? src_off(pb, m) : dst_off(pb, m);
+        key[i].idx = o->idx[i];
+    }
+    qsort(key, (size_t)o->n, sizeof(os_key), os_cmp);
+    for (i = 0; i < o->n; ++i) o->idx[i] = key[i].idx;
+    free(key);
+    o->nrun = 0;
+    for (i = 0; i < o->n; ++i) {
+        const xg_msg *m = os_msg(s, o, i);
+        if (i > 0) {
+            const xg_msg *q = os_msg(s, o, i - 1);
+            const int contiguous = by_src ? (m->sbuf == q->sbuf && src_off(pb, m) == src_off(pb, q) + q->len)
+                                          : (m->dbuf == q->dbuf && dst_off(pb, m) == dst_off(pb, q) + q->len);
+            if (contiguous) continue;
+        }
+        o->run_b[o->nrun++] = i;
+    }
+    o->run_b[o->nrun] = o->n;
+    for (r = 0; r < o->nrun; ++r) {
+        int64_t bytes = 0;
+        int other = 1;      /* contiguous on the other side too */
+        for (i = o->run_b[r]; i < o->run_b[r + 1]; ++i) {
+            const xg_msg *m = os_msg(s, o, i);
+            bytes += m->len;
+            if (i > o->run_b[r]) {
+                const xg_msg *q = os_msg(s, o, i - 1);
+                other &= by_src ? (m->dbuf == q->dbuf && dst_off(pb, m) == dst_off(pb, q) + q->len)
+                                : (m->sbuf == q->sbuf && src_off(pb, m) == src_off(pb, q) + q->len);
+            }
+        }
+        o->staged[r] = !other;
+        cost += (other ? 0 : bytes) + XG_RUN_CALL_BYTES;
+    }
+    return cost;
+}
+
+/* the one-sided form of the messages of step [b, e) from GPU gs to GPU gd */
+static void os_build(const xg_sched *s, const plan_bases *pb, const int *order, int b, int e, int G, int gs,
+                     int gd, oneside *o)
+{
+    int k;
+    int64_t cost_d, cost_s;
+    o->n = 0;
+    for (k = b; k < e; ++k) {
+        const xg_msg *m = &s->msgs[order[k]];
+        if (moves(m) && xg_gpu_of(s->P, G, m->src) == gs && xg_gpu_of(s->P, G, m->dst) == gd) o->n++;
+    }
+    o->idx = (int *)malloc(sizeof(int) * ((size_t)o->n + 1));
+    o->run_b = (int *)malloc(sizeof(int) * ((size_t)o->n + 2));
+    o->staged = (unsigned char *)malloc((size_t)o->n + 1);
+    if (!o->idx || !o->run_b || !o->staged) {
+        free(o->idx); free(o->run_b); free(o->staged);
+        o->idx = o->run_b = NULL;
+        o->staged = NULL;
+        o->n = o->nrun = 0;
+        o->fail = 1;
+        return;
+    }
+    o->n = 0;
+    for (k = b; k < e; ++k) {
+        const xg_msg *m = &s->msgs[order[k]];
+        if (moves(m) && xg_gpu_of(s->P, G, m->src) == gs && xg_gpu_of(s->P, G, m->dst) == gd) o->idx[o->n++] = order[k];
+    }
+    cost_s = os_layout(s, pb, o, 1);
+    cost_d = os_layout(s, pb, o, 0);
+    if (cost_s < cost_d) os_layout(s, pb, o, 1);
+}
+
+/* frees the arrays; keeps `fail` for the caller to see */
+static void os_free(oneside *o)
+{
+    const int fail = o->fail;
+    free(o->idx); free(o->run_b); free(o->staged);
+    memset(o, 0, sizeof *o);
+    o->fail = fail;
+}
+
+/* ---- relay form (XG_RELAY, xg_sched.h): two-phase (Valiant) routing of one step.  Every
+ * cross-GPU message is cut into G pieces: pieces 0 and 1 go straight to the destination (one per
+ * RCCL group), piece 2 + i through relay GPU R[i].  Then EVERY link (a -> h) carries egress(a) / G
+ * in the first group and every link (h -> b) ingress(b) / G in the second, whatever the step's
+ * traffic matrix: the step costs (max egress + max ingress) / G of link time instead of its
+ * busiest GPU pair's bytes.  A step is relayed when that is at most XG_RELAY_GAIN of the direct
+ * cost and every cross-GPU message is >= XG_RELAY_MIN_BYTES (smaller pieces are latency, not
+ * bandwidth).  Pairwise m9 / m10 (mpi_test.c:510-597, :421-508; partner rank ^ i, :531-545) at
+ * configs[3] put every GPU's 16 MiB round on ONE of its 7 links: 16 -> 4 MiB of link time per
+ * round.  Every GPU decides from the same message list, so all agree. */
+static int relay_step(const xg_sched *s, const int *order, int b, int e, int G, int64_t *egress, int64_t *ingress,
+                      int64_t *pair)
+{
+    int k, g, any = 0;
+    int64_t direct = 0, emax = 0, imax = 0;
+    if (G < 3) return 0;
+    memset(egress, 0, sizeof(int64_t) * (size_t)G);
+    memset(ingress, 0, sizeof(int64_t) * (size_t)G);
+    memset(pair, 0, sizeof(int64_t) * (size_t)G * G);
+    for (k = b; k < e; ++k) {
+        const xg_msg *m = &s->msgs[order[k]];
+        const int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
+        if (!moves(m) || is_stage(m) || gs == gd) continue;
+        if (m->len < XG_RELAY_MIN_BYTES) return 0;
+        egress[gs] += m->len;
+        ingress[gd] += m->len;
+        pair[(size_t)gs * G + gd] += m->len;
+        any = 1;
+    }
+    if (!any) return 0;
+    for (g = 0; g < G * G; ++g) direct = pair[g] > direct ? pair[g] : direct;
+    for (g = 0; g < G; ++g) {
+        emax = egress[g] > emax ? egress[g] : emax;
+        imax = ingress[g] > imax ? ingress[g] : imax;
+    }
+    return (double)(emax + imax) / G <= XG_RELAY_GAIN * (double)direct;
+}
+
+/* piece k of a relayed message of len bytes: [relay_cut(k), relay_cut(k + 1)), 16-B aligned cuts */
+static int64_t relay_cut(int64_t len, int k, int G) { return k >= G ? len : ((len * k / G) & ~(int64_t)15); }
+
+/* relay i (0 .. G-3) of a message from GPU gs to GPU gd: the GPUs other than gs, gd, ascending */
+static int relay_gpu(int i, int gs, int gd)
+{
+    const int lo = gs < gd ? gs : gd, hi = gs < gd ? gd : gs;
+    int h = i;
+    if (h >= lo) ++h;
+    if (h >= hi) ++h;
+    return h;
+}
+
+static void relay_push(pvec *pp, int peer, int is_send, int buf, int64_t off, int64_t len, int group)
+{
+    xg_p2p *o;
+    if (len <= 0) return;            /* a 0-byte piece (len < 16 G): no call on either side */
+    o = ppush(pp);
+    o->peer = peer; o->is_send = is_send; o->buf = buf; o->off = off; o->len = len; o->group = group;
+}
+
+/* GPU g's calls of one relayed step: group 0 = pieces 0 straight to the destination and pieces
+ * 2 + i to relay R[i] (into its STAGE_RECV at *rbase on); group 1 = pieces 1 straight, and what g
+ * holds as a relay forwarded to the destination.  Every list is in message order, so the k-th
+ * send of any GPU to any other pairs with the k-th receive there, group by group. */
+static void relay_calls(const xg_sched *s, const plan_bases *pb, const int *order, int b, int e, int G, int g,
+                        pvec *pp, int64_t *rbase)
+{
+    int grp, k, i;
+    int64_t roff = *rbase;
+    for (grp = 0; grp < 2; ++grp) {
+        roff = *rbase;
+        for (k = b; k < e; ++k) {
+            const xg_msg *m = &s->msgs[order[k]];
+            const int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
+            const int ri = g != gs && g != gd ? g - (g > gs) - (g > gd) : -1;   /* g's relay index */
+            int64_t so, dof;
+            if (!moves(m) || is_stage(m) || gs == gd) continue;
+            so = src_off(pb, m);
+            dof = dst_off(pb, m);
+            if (g == gs) {
+                relay_push(pp, gd, 1, m->sbuf, so + relay_cut(m->len, grp, G),
+                           relay_cut(m->len, grp + 1, G) - relay_cut(m->len, grp, G), grp);
+                for (i = 0; grp == 0 && i < G - 2; ++i)
+                    relay_push(pp, relay_gpu(i, gs, gd), 1, m->sbuf, so + relay_cut(m->len, 2 + i, G),
+                               relay_cut(m->len, 3 + i, G) - relay_cut(m->len, 2 + i, G), 0);
+            }
+            if (ri >= 0) {
+                const int64_t len = relay_cut(m->len, 3 + ri, G) - relay_cut(m->len, 2 + ri, G);
+                if (grp == 0) relay_push(pp, gs, 0, XG_BUF_STAGE_RECV, roff, len, 0);
+                else relay_push(pp, gd, 1, XG_BUF_STAGE_RECV, roff, len, 1);
+                roff += len > 0 ? len : 0;
+            }
+            if (g == gd) {
+                relay_push(pp, gs, 0, m->dbuf, dof + relay_cut(m->len, grp, G),
+                           relay_cut(m->len, grp + 1, G) - relay_cut(m->len, grp, G), grp);
+                for (i = 0; grp == 1 && i < G - 2; ++i)
+                    relay_push(pp, relay_gpu(i, gs, gd), 0, m->dbuf, dof + relay_cut(m->len, 2 + i, G),
+                               relay_cut(m->len, 3 + i, G) - relay_cut(m->len, 2 + i, G), 1);
+            }
+        }
+    }
+    *rbase = roff;
+}
+
+xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
+                                  int form)
+{
+    xg_devplan *dp = (xg_devplan *)calloc(1, sizeof *dp);
+    int nst = s->nsteps, i, st, G = ngpus, oom = 0;
+    int *cnt = (int *)calloc(nst + 1, sizeof(int)), *order = (int *)malloc(sizeof(int) * (s->nmsg + 1));
+    int *pos = (int *)malloc(sizeof(int) * (nst + 1));
+    cvec pre, post;
+    pvec pp;
+    int64_t stage_s_max = 0, stage_r_max = 0;
+    int *bucket_n = (int *)calloc((size_t)G * 2, sizeof(int));
+    int64_t *bucket_b = (int64_t *)calloc((size_t)G * 2, sizeof(int64_t));
+    oneside *os_out = (oneside *)calloc((size_t)G, sizeof(oneside)), *os_in = (oneside *)calloc((size_t)G, sizeof(oneside));
+    int64_t *rl_e = (int64_t *)calloc((size_t)G, sizeof(int64_t)), *rl_i = (int64_t *)calloc((size_t)G, sizeof(int64_t));
+    int64_t *rl_p = (int64_t *)calloc((size_t)G * G, sizeof(int64_t));
+    plan_bases pb;
+    memset(&pre, 0, sizeof pre); memset(&post, 0, sizeof post); memset(&pp, 0, sizeof pp);
+    memset(&pb, 0, sizeof pb);
+    if (form != XG_PACK_TWO_SIDED && form != XG_PACK_ONE_SIDED && form != XG_RELAY) form = XG_PACK_FORM_DEFAULT;
+    if (form == XG_RELAY) pack_max_seg = 0;         /* relay form: every other step is direct */
+    if (!dp || !cnt || !order || !pos || !bucket_n || !bucket_b || !os_out || !os_in || !rl_e || !rl_i || !rl_p ||
+        plan_bases_init(&pb, s, G, g) ||
+        !(dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan)))) {
+        oom = 1;
+        goto done;
+    }
+    dp->gpu = g; dp->ngpus = G; dp->nsteps = nst;
+    {   /* per step, the request posts of this GPU's ranks (graph replays share their launch time
+         * out by them: xg_plan_run) */
+        int32_t *posts = (int32_t *)calloc((size_t)nst + 1, sizeof(int32_t));
+        if (!posts) { oom = 1; goto done; }
+        xgi_step_posts_of(s, G, g, posts, nst);
+        for (st = 0; st < nst; ++st) dp->steps[st].posts = posts[st];
+        free(posts);
+    }
+    /* in-loop MPI_Barrier -> device-side barrier after the step it completes at (G > 1) */
+    for (i = 0; i < s->nbarrier; ++i)
+        if (G > 1 && s->barrier_epoch[i] >= 0 && s->barrier_epoch[i] < nst) dp->steps[s->barrier_epoch[i]].sync_after = 1;
+    /* counting sort of messages by step, stable in message order */
+    for (i = 0; i < s->nmsg; ++i) cnt[s->msgs[i].step + 1]++;
+    for (st = 0; st < nst; ++st) cnt[st + 1] += cnt[st];
+    memcpy(pos, cnt, sizeof(int) * (nst + 1));
+    for (i = 0; i < s->nmsg; ++i) order[pos[s->msgs[i].step]++] = i;
+    dp->region_bytes[XG_BUF_SEND] = xg_region_bytes(s, G, g, XG_BUF_SEND);
+    dp->region_bytes[XG_BUF_RECV] = xg_region_bytes(s, G, g, XG_BUF_RECV);
+    dp->region_bytes[XG_BUF_SCRATCH] = xg_region_bytes(s, G, g, XG_BUF_SCRATCH);
+    for (st = 0; st < nst; ++st) {
+        int b = cnt[st], e = cnt[st + 1], k, p;
+        int64_t sbase = 0, rbase = 0;
+        xg_stepplan *sp = &dp->steps[st];
+        /* per-peer volume (out: [p], in: [G+p]) for the pack decision */
+        memset(bucket_n, 0, sizeof(int) * 2 * G);
+        memset(bucket_b, 0, sizeof(int64_t) * 2 * G);
+        sp->pre_begin = pre.n;
+        /* rank-local memcpy's through SCRATCH first, in a launch of their own: the
+         * local messages and packs below may read what they write in this step */
+        for (k = b; k < e; ++k) {
+            const xg_msg *m = &s->msgs[order[k]];
+            if (!moves(m) || !is_stage(m) || xg_gpu_of(s->P, G, m->src) != g) continue;
+            local_copy(cpush(&pre), &pb, m);
+            dp->local_bytes += m->len;
+        }
+        sp->stage_count = pre.n - sp->pre_begin;
+        for (k = b; k < e; ++k) {
+            const xg_msg *m = &s->msgs[order[k]];
+            int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
+            if (!moves(m) || is_stage(m)) continue;
+            if (gs == g && gd == g) {
+                local_copy(cpush(&pre), &pb, m);
+                dp->local_bytes += m->len;
+            } else if (gs == g) {
+                bucket_n[gd]++; bucket_b[gd] += m->len;
+            } else if (gd == g) {
+                bucket_n[G + gs]++; bucket_b[G + gs] += m->len;
+            }
+        }
+        /* the one-sided layout of every packed list of this GPU's, both directions */
+        if (form == XG_PACK_ONE_SIDED)
+            for (p = 0; p < G; ++p) {
+                if (p == g) continue;
+                if (bucket_n[p] && use_pack(bucket_n[p], bucket_b[p], pack_max_seg, pack_min))
+                    os_build(s, &pb, order, b, e, G, g, p, &os_out[p]);
+                if (bucket_n[G + p] && use_pack(bucket_n[G + p], bucket_b[G + p], pack_max_seg, pack_min))
+                    os_build(s, &pb, order, b, e, G, p, g, &os_in[p]);
+                oom |= os_out[p].fail | os_in[p].fail;
+            }
+        /* packs (into staging) join the pre-exchange copy launch */
+        for (p = 0; p < G; ++p) {
+            int64_t off = 0;
+            if (p == g || !bucket_n[p] || !use_pack(bucket_n[p], bucket_b[p], pack_max_seg, pack_min)) continue;
+            if (form == XG_PACK_ONE_SIDED) {
+                const oneside *o = &os_out[p];
+                int r;
+                for (r = 0; r < o->nrun; ++r) {
+                    if (o->by_src || !o->staged[r]) continue;     /* sent as it lies */
+                    for (k = o->run_b[r]; k < o->run_b[r + 1]; ++k) {
+                        const xg_msg *m = os_msg(s, o, k);
+                        xg_copy *c = cpush(&pre);
+                        c->src_buf = m->sbuf; c->src_off = src_off(&pb, m);
+                        c->dst_buf = XG_BUF_STAGE_SEND; c->dst_off = sbase + off;
+                        c->len = m->len;
+                        off += m->len;
+                    }
+                }
+                sbase += off;
+                continue;
+            }
+            for (k = b; k < e; ++k) {
+                const xg_msg *m = &s->msgs[order[k]];
+                if (!moves(m) || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
+                {
+                    xg_copy *c = cpush(&pre);
+                    c->src_buf = m->sbuf; c->src_off = src_off(&pb, m);
+                    c->dst_buf = XG_BUF_STAGE_SEND; c->dst_off = sbase + off;
+                    c->len = m->len;
+                    off += m->len;
+                }
+            }
+            sbase += off;
+        }
+        sp->pre_count = pre.n - sp->pre_begin;
+        /* the grouped exchange: per peer, sends then receives, message order */
+        sp->p2p_begin = pp.n;
+        sp->post_begin = post.n;
+        if (form == XG_RELAY && relay_step(s, order, b, e, G, rl_e, rl_i, rl_p)) {
+            /* every message over all G - 1 links of its source, then of its destination (two groups) */
+            relay_calls(s, &pb, order, b, e, G, g, &pp, &rbase);
+            for (p = 0; p < G; ++p)
+                if (p != g) {
+                    dp->remote_send_bytes += bucket_b[p];
+                    dp->remote_recv_bytes += bucket_b[G + p];
+                }
+        } else {
+            int64_t soff = 0;
+            for (p = 0; p < G; ++p) {
+                int pk;
+                if (p == g) continue;
+                if (bucket_n[p]) {
+                    pk = use_pack(bucket_n[p], bucket_b[p], pack_max_seg, pack_min);
+                    if (pk && form == XG_PACK_ONE_SIDED) {
+                        const oneside *o = &os_out[p];
+                        int r;
+                        for (r = 0; r < o->nrun; ++r) {
+                            xg_p2p *q = ppush(&pp);
+                            int64_t len = 0;
+                            for (k = o->run_b[r]; k < o->run_b[r + 1]; ++k) len += os_msg(s, o, k)->len;
+                            q->peer = p; q->is_send = 1; q->len = len;
+                            if (!o->by_src && o->staged[r]) {
+                                q->buf = XG_BUF_STAGE_SEND; q->off = soff;
+                                soff += len;
+                            } else {
+                                const xg_msg *m = os_msg(s, o, o->run_b[r]);
+                                q->buf = m->sbuf; q->off = src_off(&pb, m);
+                            }
+                        }
+                    } else if (pk) {
+                        xg_p2p *o = ppush(&pp);
+                        o->peer = p; o->is_send = 1; o->buf = XG_BUF_STAGE_SEND; o->off = soff; o->len = bucket_b[p];
+                        soff += bucket_b[p];
+                    } else {
+                        for (k = b; k < e; ++k) {
+                            const xg_msg *m = &s->msgs[order[k]];
+                            if (!moves(m) || xg_gpu_of(s->P, G, m->src) != g || xg_gpu_of(s->P, G, m->dst) != p) continue;
+                            {
+                                xg_p2p *o = ppush(&pp);
+                                o->peer = p; o->is_send = 1; o->buf = m->sbuf;
+                                o->off = src_off(&pb, m); o->len = m->len;
+                            }
+                        }
+                    }
+                    dp->remote_send_bytes += bucket_b[p];
+                }
+                if (bucket_n[G + p]) {
+                    pk = use_pack(bucket_n[G + p], bucket_b[G + p], pack_max_seg, pack_min);
+                    if (pk && form == XG_PACK_ONE_SIDED) {
+                        const oneside *o = &os_in[p];
+                        int r;
+                        for (r = 0; r < o->nrun; ++r) {
+                            xg_p2p *q = ppush(&pp);
+                            int64_t len = 0;
+                            for (k = o->run_b[r]; k < o->run_b[r + 1]; ++k) len += os_msg(s, o, k)->len;
+                            q->peer = p; q->is_send = 0; q->len = len;
+                            if (o->by_src && o->staged[r]) {
+                                int64_t off = 0;
+                                q->buf = XG_BUF_STAGE_RECV; q->off = rbase;
+                                for (k = o->run_b[r]; k < o->run_b[r + 1]; ++k) {
+                                    const xg_msg *m = os_msg(s, o, k);
+                                    xg_copy *c = cpush(&post);
+                                    c->src_buf = XG_BUF_STAGE_RECV; c->src_off = rbase + off;
+                                    c->dst_buf = m->dbuf; c->dst_off = dst_off(&pb, m);
+                                    c->len = m->len;
+                                    off += m->len;
+                                }
+                                rbase += len;
+                            } else {
+                                const xg_msg *m = os_msg(s, o, o->run_b[r]);
+                                q->buf = m->dbuf; q->off = dst_off(&pb, m);
+                            }
+                        }
+                    } else if (pk) {
+                        xg_p2p *o = ppush(&pp);
+                        int64_t off = 0;
+                        o->peer = p; o->is_send = 0; o->buf = XG_BUF_STAGE_RECV; o->off = rbase; o->len = bucket_b[G + p];
+                        for (k = b; k < e; ++k) {
+                            const xg_msg *m = &s->msgs[order[k]];
+                            if (!moves(m) || xg_gpu_of(s->P, G, m->src) != p || xg_gpu_of(s->P, G, m->dst) != g) continue;
+                            {
+                                xg_copy *c = cpush(&post);
+                                c->src_buf = XG_BUF_STAGE_RECV; c->src_off = rbase + off;
+                                c->dst_buf = m->dbuf; c->dst_off = dst_off(&pb, m);
+                                c->len = m->len;
+                                off += m->len;
+                            }
+                        }
+                        rbase += bucket_b[G + p];
+                    } else {
+                        for (k = b; k < e; ++k) {
+                            const xg_msg *m = &s->msgs[order[k]];
+                            if (!moves(m) || xg_gpu_of(s->P, G, m->src) != p || xg_gpu_of(s->P, G, m->dst) != g) continue;
+                            {
+                                xg_p2p *o = ppush(&pp);
+                                o->peer = p; o->is_send = 0; o->buf = m->dbuf;
+                                o->off = dst_off(&pb, m); o->len = m->len;
+                            }
+                        }
+                    }
+                    dp->remote_recv_bytes += bucket_b[G + p];
+                }
+            }
+            if (soff != sbase && !oom) { fprintf(stderr, "xg_devplan_build: staging mismatch\n"); abort(); }
+        }
+        sp->p2p_count = pp.n - sp->p2p_begin;
+        sp->post_count = post.n - sp->post_begin;
+        if (sbase > stage_s_max) stage_s_max = sbase;
+        if (rbase > stage_r_max) stage_r_max = rbase;
+        for (p = 0; p < G; ++p) {
+            os_free(&os_out[p]);
+            os_free(&os_in[p]);
+        }
+        if (oom) goto done;
+    }
+    /* post copies are stored after the pre copies in one array */
+    oom |= pre.fail | post.fail | pp.fail;
+    dp->ncopy = pre.n + post.n;
+    if (!oom && (dp->copies = (xg_copy *)malloc(sizeof(xg_copy) * (dp->ncopy + 1)))) {
+        if (pre.n) memcpy(dp->copies, pre.v, sizeof(xg_copy) * pre.n);
+        if (post.n) memcpy(dp->copies + pre.n, post.v, sizeof(xg_copy) * post.n);
+        for (st = 0; st < nst; ++st) dp->steps[st].post_begin += pre.n;
+        dp->np2p = pp.n;
+        dp->p2p = pp.v ? pp.v : (xg_p2p *)malloc(sizeof(xg_p2p));
+        if (dp->p2p == pp.v) pp.v = NULL;           /* owned by the plan now */
+        dp->region_bytes[XG_BUF_STAGE_SEND] = stage_s_max;
+        dp->region_bytes[XG_BUF_STAGE_RECV] = stage_r_max;
+    }
+    oom |= !dp->copies || !dp->p2p;
+done:
+    free(pre.v); free(post.v); free(pp.v); free(cnt); free(order); free(pos); free(bucket_n); free(bucket_b);
+    free(os_out); free(os_in); free(rl_e); free(rl_i); free(rl_p);
+    plan_bases_free(&pb);
+    if (oom) {
+        xg_devplan_free(dp);
+        return NULL;
+    }
+    return dp;
+}
+
+/* ------------------------------------------------------------------ fill / verify descriptors */
+int xg_fill_runs(const xg_sched *s, int ngpus, int g, xg_segrun *out)
+{
+    int lo, hi, r, n = 0;
+    xg_block_range(s->P, ngpus, g, &lo, &hi);
+    for (r = lo; r < hi; ++r) {
+        int ns = xgi_nsend_segs(s, r);
+        if (!ns) continue;
+        if (out) {   /* prepare_*_data: segment i of rank r carries seed i (:106-110, :195-199) */
+            out[n].rank = r; out[n].seed0 = 0; out[n].nsegs = ns; out[n].pad = 0;
+            out[n].off = xg_send_offset(s, ngpus, r);
+        }
+        n++;
+    }
+    return n;
+}
+
+int xg_verify_slots(const xg_sched *s, int ngpus, int g, xg_slot *out)
+{
+    int lo, hi, r, i, n = 0;
+    xg_block_range(s->P, ngpus, g, &lo, &hi);
+    for (r = lo; r < hi; ++r) {
+        int nslots = xgi_nrecv_slots(s, r), myindex = 0;
+        int64_t base;
+        if (!nslots) continue;
+        base = xg_recv_offset(s, ngpus, r);
+        for (i = 0; i < s->A; ++i)
+            if (s->rank_list[i] == r) myindex = i;
+        for (i = 0; i < nslots; ++i, ++n) {
+            if (!out) continue;
+            /* check_buffer call sites: a2m (src=i, seed=myindex) :215; m2a (src=rank_list[i], seed=rank) :139 */
+            out[n].src = s->dir == XG_A2M ? i : s->rank_list[i];
+            out[n].seed = s->dir == XG_A2M ? myindex : r;
+            out[n].dst = r; out[n].pad = 0;
+            out[n].off = base + (int64_t)i * s->d;
+        }
+    }
+    return n;
+}

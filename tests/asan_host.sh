@@ -7,7 +7,8 @@ REPO=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$(mktemp -d /tmp/xg_asan.XXXXXX)
 gcc -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all \
     -Wall -Wextra -fPIC -std=c99 -D_POSIX_C_SOURCE=200809L -I"$REPO/include" -shared -o "$OUT/libxghost.so" \
-    "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/sched.c" "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/report.c" \
+    "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/programs.c" "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/sched.c" "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/devplan.c" \
+    "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/report.c" \
     "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/hazard.c" "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/solo.c" \
     "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/calls.c" "$REPO/mpi-asynchronous-communication-test_amd/csrc/host/pieces.c"
 cd "$REPO/tests"

@@ -17,7 +17,7 @@ import pytest
 from conftest import REPO
 
 HOST = os.path.join(REPO, "mpi-asynchronous-communication-test_amd", "csrc", "host")
-HOST_SRCS = ["sched.c", "report.c", "hazard.c", "solo.c", "calls.c", "pieces.c"]
+HOST_SRCS = ["programs.c", "sched.c", "devplan.c", "report.c", "hazard.c", "solo.c", "calls.c", "pieces.c"]
 SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all"]
 
 pytestmark = pytest.mark.skipif(not shutil.which("gcc"), reason="gcc not found")

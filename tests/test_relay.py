@@ -1,4 +1,4 @@
-"""The relay form (XG_RELAY, sched.c relay_calls) on the CPU: a step whose cross-GPU messages form a
+"""The relay form (XG_RELAY, devplan.c relay_calls) on the CPU: a step whose cross-GPU messages form a
 permutation of the GPUs -- pairwise m9 / m10's XOR rounds (mpi_test.c:510-597, :421-508; partner
 rank ^ i at :531-545) -- sends every message over all G - 1 links of its source in two RCCL groups
 instead of over one link.  Every byte still lands where the reference puts it (race-checked CPU
