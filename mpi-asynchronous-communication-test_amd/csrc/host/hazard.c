@@ -106,6 +106,10 @@ int xg_engine_hazards(const xg_span *xfer, const int *step_begin, int nsteps, in
         if (flags[nsteps - 1] < 1) flags[nsteps - 1] = 1;
         return 0;
     }
+    cap = 64;
+    pend = (ivl *)malloc(sizeof(ivl) * cap);
+    tmp = (ivl *)malloc(sizeof(ivl) * cap);
+    if (!pend || !tmp) abort();
     for (s = 0; s < nsteps; ++s) {
         const int b = step_begin[s], e = step_begin[s + 1];
         int hazard = 0, nnew = 0, n, m;

@@ -26,6 +26,13 @@ void *xgi_xmalloc(size_t n)
     return p;
 }
 
+void *xgi_xcalloc(size_t n, size_t size)
+{
+    void *p = calloc(n ? n : 1, size ? size : 1);
+    if (!p) { fprintf(stderr, "xg_sched: out of host memory (%zu x %zu bytes)\n", n, size); abort(); }
+    return p;
+}
+
 static op_t *push(prog_t *p)
 {
     if (p->nops == p->cap) {

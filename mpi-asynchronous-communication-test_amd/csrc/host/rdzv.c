@@ -82,24 +82,33 @@ int xg_env_int(const char *a, const char *b, int dflt)
 /* environment of child r: this process's, with the rank variables replaced (the last
  * CHILD_VARS entries are its own: free_child_env releases them) */
 #define CHILD_VARS 5
+
+/* the spawner has nothing to fall back on without host memory: say so and stop */
+static void *xzalloc(size_t n, size_t size)
+{
+    void *p = calloc(n ? n : 1, size);
+    if (!p) { fprintf(stderr, "xg_spawn_ranks: out of host memory\n"); exit(1); }
+    return p;
+}
+
 static char **child_env(int r, int n, const char *key)
 {
     size_t m = 0, i, k = 0;
     char **env;
     static const char *drop[] = {"RANK=", "LOCAL_RANK=", "WORLD_SIZE=", "LOCAL_WORLD_SIZE=", "XG_RDZV_KEY=", NULL};
     while (environ[m]) m++;
-    env = (char **)calloc(m + 6, sizeof(char *));
+    env = (char **)xzalloc(m + 6, sizeof(char *));
     for (i = 0; i < m; ++i) {
         int j, skip = 0;
         for (j = 0; drop[j]; ++j)
             if (!strncmp(environ[i], drop[j], strlen(drop[j]))) skip = 1;
         if (!skip) env[k++] = environ[i];
     }
-    env[k] = (char *)malloc(32); snprintf(env[k++], 32, "RANK=%d", r);
-    env[k] = (char *)malloc(32); snprintf(env[k++], 32, "LOCAL_RANK=%d", r);
-    env[k] = (char *)malloc(32); snprintf(env[k++], 32, "WORLD_SIZE=%d", n);
-    env[k] = (char *)malloc(32); snprintf(env[k++], 32, "LOCAL_WORLD_SIZE=%d", n);
-    env[k] = (char *)malloc(160); snprintf(env[k++], 160, "XG_RDZV_KEY=%s", key);
+    env[k] = (char *)xzalloc(32, 1); snprintf(env[k++], 32, "RANK=%d", r);
+    env[k] = (char *)xzalloc(32, 1); snprintf(env[k++], 32, "LOCAL_RANK=%d", r);
+    env[k] = (char *)xzalloc(32, 1); snprintf(env[k++], 32, "WORLD_SIZE=%d", n);
+    env[k] = (char *)xzalloc(32, 1); snprintf(env[k++], 32, "LOCAL_WORLD_SIZE=%d", n);
+    env[k] = (char *)xzalloc(160, 1); snprintf(env[k++], 160, "XG_RDZV_KEY=%s", key);
     env[k] = NULL;
     return env;
 }
@@ -124,8 +133,8 @@ int xg_spawn_ranks(int ngpus, char **argv)
      * whatever the environment says (the one-GPU boxes export HIP's default 4), or the command
      * processor time-slices the ranks' queues (profiles/r05/share_gpu_queues/) */
     if (getenv("XG_SHARE_GPU") && !strcmp(getenv("XG_SHARE_GPU"), "1")) setenv("GPU_MAX_HW_QUEUES", "1", 1);
-    pid = (pid_t *)calloc(ngpus, sizeof(pid_t));
-    st = (int *)calloc(ngpus, sizeof(int));
+    pid = (pid_t *)xzalloc(ngpus, sizeof(pid_t));
+    st = (int *)xzalloc(ngpus, sizeof(int));
     for (r = 0; r < ngpus; ++r) {
         char **env = child_env(r, ngpus, key);
         if (posix_spawn(&pid[r], "/proc/self/exe", NULL, NULL, argv, env)) {

@@ -213,7 +213,7 @@ static int compile_steps(xg_sched *s, char *err, size_t errlen)
     int *pc = (int *)xgi_xmalloc(sizeof(int) * P), *epoch = (int *)xgi_xmalloc(sizeof(int) * P);
     int32_t **pe = (int32_t **)xgi_xmalloc(sizeof(int32_t *) * P);     /* post epoch */
     int nb = s->progs[0].nbarrier;
-    int *arrived = (int *)calloc(nb + 1, sizeof(int)), *arr_epoch = (int *)xgi_xmalloc(sizeof(int) * (nb + 1));
+    int *arrived = (int *)xgi_xcalloc(nb + 1, sizeof(int)), *arr_epoch = (int *)xgi_xmalloc(sizeof(int) * (nb + 1));
     int *lw = (int *)xgi_xmalloc(sizeof(int) * NLB * P), *lrd = (int *)xgi_xmalloc(sizeof(int) * NLB * P);
     for (r = 0; r < NLB * P; ++r) lw[r] = lrd[r] = INT_MIN / 2;
     for (r = 1; r < P; ++r)
@@ -362,18 +362,18 @@ xg_sched *xg_sched_build_iter(int method, int procs, int cb_nodes, int64_t data_
     if (comm_size < 1) { snprintf(err, errlen, "comm_size must be >= 1 (the reference divides by it)"); return NULL; }
     for (i = 0; i < cb_nodes; ++i)
         if (rank_list[i] < 0 || rank_list[i] >= procs) { snprintf(err, errlen, "aggregator %d out of range", rank_list[i]); return NULL; }
-    s = (xg_sched *)calloc(1, sizeof *s);
+    s = (xg_sched *)xgi_xcalloc(1, sizeof *s);
     s->method = method; s->P = procs; s->A = cb_nodes; s->d = data_size; s->c = comm_size;
     s->ntimes = ntimes; s->eager = eager_limit; s->dir = xg_method_direction(method);
     s->proc_node = proc_node; s->barrier_type = barrier_type; s->iter = iter;
     s->rank_list = (int *)xgi_xmalloc(sizeof(int) * cb_nodes);
     memcpy(s->rank_list, rank_list, sizeof(int) * cb_nodes);
-    s->isagg = (int *)calloc(procs, sizeof(int));
+    s->isagg = (int *)xgi_xcalloc(procs, sizeof(int));
     s->agg_prefix = (int *)xgi_xmalloc(sizeof(int) * (procs + 1));
     for (i = 0; i < cb_nodes; ++i) s->isagg[rank_list[i]] = 1;
     s->agg_prefix[0] = 0;
     for (r = 0; r < procs; ++r) s->agg_prefix[r + 1] = s->agg_prefix[r] + s->isagg[r];
-    s->progs = (prog_t *)calloc(procs, sizeof(prog_t));
+    s->progs = (prog_t *)xgi_xcalloc(procs, sizeof(prog_t));
     lastidx = (int *)xgi_xmalloc(sizeof(int) * procs);
     for (r = 0; r < procs; ++r) lastidx[r] = -1;
     for (i = 0; i < cb_nodes; ++i) lastidx[rank_list[i]] = i;
@@ -391,12 +391,12 @@ xg_sched *xg_sched_build_iter(int method, int procs, int cb_nodes, int64_t data_
     }
     free(lastidx);
     scratch_layout(s);
-    s->post_msg = (int32_t **)calloc(procs, sizeof(int32_t *));
-    s->post_eager = (uint8_t **)calloc(procs, sizeof(uint8_t *));
+    s->post_msg = (int32_t **)xgi_xcalloc(procs, sizeof(int32_t *));
+    s->post_eager = (uint8_t **)xgi_xcalloc(procs, sizeof(uint8_t *));
     for (r = 0; r < procs; ++r) {
         prog_t *p = &s->progs[r];
         s->post_msg[r] = (int32_t *)xgi_xmalloc(sizeof(int32_t) * (p->nposts + 1));
-        s->post_eager[r] = (uint8_t *)calloc(p->nposts + 1, 1);
+        s->post_eager[r] = (uint8_t *)xgi_xcalloc(p->nposts + 1, 1);
         for (i = 0; i < p->nops; ++i)
             if (p->ops[i].kind == OP_SEND && p->ops[i].eager_ok && p->ops[i].cnt * p->ops[i].esz <= eager_limit)
                 s->post_eager[r][p->ops[i].post] = 1;
@@ -477,7 +477,7 @@ static void count_posts(xg_sched *s, int ngpus)
     int r, i;
     if (s->post_count && s->pc_ngpus == ngpus) return;
     free(s->post_count);
-    s->post_count = (int32_t *)calloc((size_t)ngpus * (s->nsteps + 1), sizeof(int32_t));
+    s->post_count = (int32_t *)xgi_xcalloc((size_t)ngpus * (s->nsteps + 1), sizeof(int32_t));
     s->pc_ngpus = ngpus;
     for (r = 0; r < s->P; ++r) {
         const prog_t *p = &s->progs[r];

@@ -82,7 +82,8 @@ typedef struct {
     const int *lastidx;     /* [P] last i with rl[i] == rank, -1 if none */
 } ctx_t;
 
-XGI void *xgi_xmalloc(size_t n);
+XGI void *xgi_xmalloc(size_t n);              /* abort on out of host memory */
+XGI void *xgi_xcalloc(size_t n, size_t size);
 /* the rank's whole program: MPI_Barrier, total_start, the method body, total_end */
 XGI void xgi_program(ctx_t *x);
 /* segments a rank sends / slots it receives (its share of SEND / RECV) */
