@@ -472,6 +472,33 @@ def link_sweep(ctx, world, nbytes=16 << 20, reps=5, error=RuntimeError):
     return res, None
 
 
+def busiest_link_bytes(xg, s, world, pack, form):
+    """the plan's link time in bytes: per step and per RCCL group of it, the most loaded directed GPU
+    link's bytes (the calls each GPU posts, xg_devplan_step_calls), summed over the run -- what the
+    exchange costs at one link rate however fast the rest of the node is (profiles/link_load.py)"""
+    views = [s.devplan(world, g, pack, 0, form) for g in range(world)]
+    tot = 0
+    for st in range(views[0].nsteps):
+        per = {}                                  # (group, src GPU, dst GPU) -> bytes
+        for g, v in enumerate(views):
+            grp = 0
+            for kind, peer, _buf, _off, ln in v.calls(st):
+                if kind == xg.CALL_FENCE:
+                    grp += 1
+                elif kind == xg.CALL_SEND and peer != g:
+                    per[(grp, g, peer)] = per.get((grp, g, peer), 0) + ln
+        for q in {k[0] for k in per}:
+            tot += max(b for k, b in per.items() if k[0] == q)
+    return tot
+
+
+def link_rate(out):
+    """the median per-link rate (GB/s, one direction) of the per-link sweep, or None"""
+    links = ((out.get("xgmi") or {}).get("links")) or {}
+    vals = sorted(v for row in links.get("GBps") or [] for v in row if v)
+    return vals[len(vals) // 2] if vals else None
+
+
 # ---------------------------------------------------------------- BASELINE.json's 8-GPU configurations
 # (name, P, A, d, -c, methods): configs[2], configs[3], configs[4] at their stated sizes, and
 # configs[3] / [4] at the reduced -d the reference runs at on the host (CPU_CELLS: the same keys),
@@ -484,10 +511,12 @@ BASELINE_CELLS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
                   [("configs[4] -c %d" % c, 256, 64, 64 << 20, c, (7, 11, 12)) for c in (1, 8, 2, 3, 4, 5, 6, 7)])
 
 
-def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_CELLS):
+def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_CELLS, link_gbps=None):
     """Every method of BASELINE.json's 8-GPU configurations on this job: per (config, method) one
     verified run (every slot checked on its GPU, bad slots MAX-reduced), one timed run (device
     time, MAX over GPUs), delivered and cross-GPU (xGMI) GB/s and the reference's max total time.
+    Beside each: the plan's link bound -- its busiest-link bytes (busiest_link_bytes) at the per-link
+    sweep's median rate (`link_gbps`) -- and the fraction of it the run reached.
     Where the relay form (XG_RELAY) changes the plan -- configs[3]'s pairwise m9 / m10, whose
     XOR rounds put each GPU on one link -- it is verified and timed too, and the faster form is
     the cell's figure ("forms", "chosen").  Collective throughout: every rank takes the same cells
@@ -528,10 +557,18 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
         finally:
             run.close()
         cross = sum(s.devplan(world, g).remote_send_bytes for g in range(world))
-        return {"P": P, "A": A, "d": d, "c": c, "ms_per_run": round(t_run * 1e3, 4),
-                "GBps_delivered": round(P * A * d / t_run / 1e9, 2),
-                "GBps_cross_gpu": round(cross / t_run / 1e9, 2), "cross_gpu_bytes": int(cross),
-                "max_total_time_s": tmax, "verified": nbad == 0, "bad_slots_max_gpu": int(nbad)}, None
+        # (rank 0 prints the line; the other ranks skip the host-side plan walk)
+        busiest = busiest_link_bytes(xg, s, world, form[0], form[1]) if rank == 0 else 0
+        fig = {"P": P, "A": A, "d": d, "c": c, "ms_per_run": round(t_run * 1e3, 4),
+               "GBps_delivered": round(P * A * d / t_run / 1e9, 2),
+               "GBps_cross_gpu": round(cross / t_run / 1e9, 2), "cross_gpu_bytes": int(cross),
+               "busiest_link_bytes": int(busiest) if rank == 0 else None,
+               "max_total_time_s": tmax, "verified": nbad == 0, "bad_slots_max_gpu": int(nbad)}
+        if link_gbps and busiest:
+            bound_ms = busiest / (link_gbps * 1e9) * 1e3
+            fig["link_bound_ms"] = round(bound_ms, 4)
+            fig["link_bound_frac"] = round(bound_ms / (t_run * 1e3), 4) if t_run > 0 else None
+        return fig, None
 
     try:
         for name, P, A, d, c, methods in cells:
@@ -1137,7 +1174,8 @@ def main():
         extra = out["baseline_configs_8gpu"] = {"budget_s": a.baseline_budget}
         with LineGuard(out, rank, a.baseline_budget + 45.0, lambda msg: extra.__setitem__("error", msg)):
             try:
-                baseline_configs_phase(xg, ctx, world, rank, a.baseline_budget, extra)
+                extra["link_GBps"] = link_rate(out)
+                baseline_configs_phase(xg, ctx, world, rank, a.baseline_budget, extra, link_gbps=extra["link_GBps"])
             except xg.XGError as e:
                 extra["error"] = str(e)
     if rank == 0:

@@ -224,6 +224,15 @@ def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
             assert v["verified"] and v["ms_per_run"] > 0 and v["GBps_cross_gpu"] > 0, (k, v)
     assert cells["configs[4] -c 1 m7"]["cross_gpu_bytes"] == 256 * 64 * (64 << 20) // 2   # half the pairs cross
     assert "error" not in ex and ex["spent_s"] >= 0
+    # each cell's link bound: its busiest-link bytes at the per-link sweep's median rate
+    assert ex["link_GBps"] == bench.link_rate(out) and ex["link_GBps"] > 0
+    for k, v in cells.items():
+        if isinstance(v, dict):
+            assert v["busiest_link_bytes"] > 0, (k, v)
+            want_ms = v["busiest_link_bytes"] / (ex["link_GBps"] * 1e9) * 1e3
+            assert abs(v["link_bound_ms"] - want_ms) <= 1e-4 + 1e-6 * want_ms, (k, v)
+            # (from the unrounded run time: ms_per_run carries 4 decimals)
+            assert v["link_bound_frac"] == pytest.approx(v["link_bound_ms"] / v["ms_per_run"], rel=0.02), (k, v)
 
 
 def test_bench_baseline_configs_phase_keeps_to_its_budget(tmp_path):
@@ -387,3 +396,20 @@ def test_bench_baseline_configs_time_the_relay_form_where_it_applies(tmp_path):
         assert set(c["forms"]) == {"direct", "relay"} and c["chosen"] in c["forms"] and c["verified"], c
     for m in (1, 2):
         assert "forms" not in cells["configs[3] m%d" % m]
+
+
+def test_busiest_link_bytes_of_the_pairwise_plans(xg):
+    """bench.busiest_link_bytes (the link bound beside every BASELINE cell) on configs[3]'s pairwise
+    m9 at 8 GPUs: 224 XOR rounds of 16 MiB on one link each direct, a quarter of that relayed
+    (the figures of profiles/r05/link_load.txt and tests/test_relay.py); m1's single all-to-all step
+    spreads its bytes over every link; the median link rate comes from the per-link sweep"""
+    import bench
+    P, A, d = 256, 32, 4 << 20
+    rl = xg.aggregator_list(P, A)
+    s9 = xg.Schedule(9, P, A, d, 200000000, rl, ntimes=1)
+    assert bench.busiest_link_bytes(xg, s9, 8, 0, -1) == 3584 << 20
+    assert bench.busiest_link_bytes(xg, s9, 8, 0, xg.RELAY) == 896 << 20
+    s1 = xg.Schedule(1, P, A, d, 200000000, rl, ntimes=1)
+    assert bench.busiest_link_bytes(xg, s1, 8, 0, -1) == 512 << 20
+    assert bench.link_rate({"xgmi": {"links": {"GBps": [[None, 40.0, 50.0], [45.0, None, 60.0], [55.0, 52.0, None]]}}}) == 52.0
+    assert bench.link_rate({"xgmi": None}) is None
