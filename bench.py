@@ -879,6 +879,15 @@ def xgmi_phase(xg, ctx, runs, world, nmethods, steps, elapsed, out):
     xgmi["sweep"], xgmi["sweep_error"] = p2p_sweep(ctx, world, xg.XGError)
     phase("xGMI per-link sweep")
     xgmi["links"], xgmi["links_error"] = link_sweep(ctx, world, error=xg.XGError)
+    # the timed region's link bound: the chosen plans' busiest-link bytes per step at the median
+    # measured link rate, and the share of it the timed steps reached (rank 0 prints the line)
+    rate = link_rate(out)
+    if rate and ctx.rank == 0:
+        busiest = sum(busiest_link_bytes(xg, r.sched, world, r.pack_max_seg, r.pack_form) for r in runs)
+        bound_ms = busiest / (rate * 1e9) * 1e3
+        xgmi["link_bound"] = {"busiest_link_bytes_per_step": int(busiest), "link_GBps": rate,
+                              "ms_per_step": round(bound_ms, 4),
+                              "frac": round(bound_ms / (elapsed / steps * 1e3), 4)}
 
 
 def main():

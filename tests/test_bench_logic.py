@@ -53,6 +53,10 @@ def test_bench_multi_gpu_rank0_line(world, tmp_path):
         assert set(tune) == {f + "_ms" for f in forms} | {"chosen", "margin"}, tune
         assert tune["chosen"] in forms and tune[tune["chosen"] + "_ms"] == min(tune[f + "_ms"] for f in forms)
         assert tune["margin"] is not None and tune["margin"] >= 0
+    # the timed steps against their link bound (busiest-link bytes per step at the median link rate)
+    lb = out["xgmi"]["link_bound"]
+    assert lb["busiest_link_bytes_per_step"] > 0 and lb["link_GBps"] > 0 and lb["ms_per_step"] > 0
+    assert lb["frac"] == pytest.approx(lb["ms_per_step"] / out["ms_per_step"], rel=0.02)
     # the self-diagnosing fields: RCCL's version, each phase's wall time, the per-link sweep
     assert out["rccl_version"] == 22703 and "not xGMI" not in out["transport"]
     pw = out["phase_wall_s"]
