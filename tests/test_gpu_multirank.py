@@ -150,8 +150,10 @@ def test_relay_form_as_multi_rank_job(tmp_path, G):
     """the relay form (XG_RELAY) between real ranks: pairwise m9 / m10 (each XOR round relayed over
     every other GPU in two RCCL groups) and m12 / m1 (their permutation steps relayed, the rest
     direct) at P16 A8 -d 1 MiB, and at 8 ranks configs[3]'s P256 A32 at -d 1 MiB (lists of 4 MiB per
-    round) -- every slot byte-checked on the device, sampled slots against the oracle's closed form"""
-    cases = [{"shape": [16, 8, 1 << 20, 3], "methods": [9, 10, 12, 1], "forms": [DIRECT, RELAY]}]
+    round) -- every slot byte-checked on the device, sampled slots against the oracle's closed form;
+    an -d of (1 << 20) + 3 puts every piece of a relayed message at an odd address"""
+    cases = [{"shape": [16, 8, 1 << 20, 3], "methods": [9, 10, 12, 1], "forms": [DIRECT, RELAY]},
+             {"shape": [16, 8, (1 << 20) + 3, 3], "methods": [9, 10, 12], "forms": [DIRECT, RELAY]}]
     if G == 8:
         cases.append({"shape": [256, 32, 1 << 20, 200000000], "methods": [9, 10], "forms": [DIRECT, RELAY]})
     rows = _job(tmp_path, G, cases, timeout=140)
