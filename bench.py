@@ -511,15 +511,22 @@ BASELINE_CELLS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
                   [("configs[4] -c %d" % c, 256, 64, 64 << 20, c, (7, 11, 12)) for c in (1, 8, 2, 3, 4, 5, 6, 7)])
 
 
+# the cross-GPU plan forms a BASELINE cell is timed in (pack_max_seg, pack_form), direct first: the
+# others only where they change the plan
+CELL_FORMS = (("direct", (0, -1)), ("packed_one_sided", (4 << 20, 1)), ("packed_two_sided", (4 << 20, 0)),
+              ("relay", (0, 2)))
+
+
 def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_CELLS, link_gbps=None):
     """Every method of BASELINE.json's 8-GPU configurations on this job: per (config, method) one
     verified run (every slot checked on its GPU, bad slots MAX-reduced), one timed run (device
     time, MAX over GPUs), delivered and cross-GPU (xGMI) GB/s and the reference's max total time.
     Beside each: the plan's link bound -- its busiest-link bytes (busiest_link_bytes) at the per-link
     sweep's median rate (`link_gbps`) -- and the fraction of it the run reached.
-    Where the relay form (XG_RELAY) changes the plan -- configs[3]'s pairwise m9 / m10, whose
-    XOR rounds put each GPU on one link -- it is verified and timed too, and the faster form is
-    the cell's figure ("forms", "chosen").  Collective throughout: every rank takes the same cells
+    Every cross-GPU form that changes the cell's plan -- packed one-sided / two-sided (lists of
+    segments <= 4 MiB) and the relay form (XG_RELAY: configs[3]'s pairwise m9 / m10, whose XOR rounds
+    put each GPU on one link; configs[4]'s m11 / m12) -- is verified and timed beside the direct
+    form, and the fastest is the cell's figure ("forms", "chosen").  Collective throughout: every rank takes the same cells
     in the same order, and every decision (budget spent, a plan or allocation that failed on some
     GPU) is MAX-reduced first, so all ranks skip alike.  Fills result["cells"] as it goes (a
     watchdog may print it half done)."""
@@ -527,7 +534,7 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
     result["cells"] = cells_out = {}
     regions = {}                      # (P, A, d) -> Regions shared by that configuration's cells
     no_room = set()                   # (P, A, d) whose regions could not be allocated on some GPU
-    default, relay = (4 << 20, -1), (0, xg.RELAY)
+    needs = {}                        # (P, A, d, c) -> region bytes of every method and form on this GPU
 
     def measure(s, P, A, d, c, form, reg):
         """one verified + one timed run of a plan form -> (figures, None) or (None, why)"""
@@ -582,17 +589,24 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                 if (P, A, d) in no_room:
                     cells_out[key] = "skipped: this configuration's regions did not fit"
                     continue
-                err, no_alloc, relayed = "", False, 0.0
+                err, no_alloc, differs = "", False, [0.0] * (len(CELL_FORMS) - 1)
                 try:
                     s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
-                    # does the relay form change this plan (a permutation step with lists >= 1 MiB)?
-                    relayed = 1.0 if world > 2 and any(o[5] for o in s.devplan(world, rank, relay[0], 0, relay[1]).p2p) else 0.0
-                    need = [0] * xg.NBUF
-                    for mm in methods:          # one allocation per configuration, sized for all its methods
-                        sm = xg.Schedule(mm, P, A, d, c, rl, ntimes=1)
-                        for f in (default, relay):
-                            v = sm.devplan(world, rank, f[0], 0, f[1])
-                            need = [max(x, y) for x, y in zip(need, v.region_bytes)]
+                    # which forms change this GPU's plan (packing: lists of small segments; relay: a
+                    # permutation step with lists >= 1 MiB); MAX-reduced below, so all GPUs agree
+                    v0 = s.devplan(world, rank, 0, 0, -1)
+                    for i, (_fname, f) in enumerate(CELL_FORMS[1:]):
+                        v = s.devplan(world, rank, f[0], 0, f[1])
+                        differs[i] = 1.0 if (v.copies, v.p2p) != (v0.copies, v0.p2p) else 0.0
+                    if (P, A, d, c) not in needs:   # one allocation per configuration: all its methods, all forms
+                        need = [0] * xg.NBUF
+                        for mm in methods:
+                            sm = xg.Schedule(mm, P, A, d, c, rl, ntimes=1)
+                            for _fname, f in CELL_FORMS:
+                                v = sm.devplan(world, rank, f[0], 0, f[1])
+                                need = [max(x, y) for x, y in zip(need, v.region_bytes)]
+                        needs[(P, A, d, c)] = need
+                    need = needs[(P, A, d, c)]
                     rk = (P, A, d)
                     if rk not in regions or not regions[rk].fits(need):
                         # a new configuration, or one whose -c needs more staging than the cells
@@ -607,15 +621,14 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                         no_alloc = False
                 except xg.XGError as e:
                     err = str(e)
-                failed, unplaced, relayed = ctx.allreduce_max([1.0 if err else 0.0, 1.0 if no_alloc else 0.0, relayed])
+                failed, unplaced, *differs = ctx.allreduce_max([1.0 if err else 0.0, 1.0 if no_alloc else 0.0] + differs)
                 if failed:
                     cells_out[key] = "failed: %s" % (err or "on another GPU")
                     if unplaced:      # some GPU never got this configuration's regions: the rest would fail alike
                         no_room.add((P, A, d))
                     continue
-                forms = {"direct": default}
-                if relayed:
-                    forms["relay"] = relay
+                forms = dict(CELL_FORMS[:1])
+                forms.update((fname, f) for (fname, f), dif in zip(CELL_FORMS[1:], differs) if dif)
                 figs = {}
                 for fname, form in forms.items():
                     figs[fname], why = measure(s, P, A, d, c, form, regions[(P, A, d)])
@@ -631,6 +644,9 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                     cell["chosen"] = best
                     cell["forms"] = {k: (v["ms_per_run"] if isinstance(v, dict) and v["verified"] else str(v))
                                      for k, v in figs.items()}
+                    times = sorted(v["ms_per_run"] for v in ok.values())
+                    # how far ahead the chosen form is: (runner-up - chosen) / chosen
+                    cell["margin"] = round((times[1] - times[0]) / times[0], 4) if len(times) > 1 and times[0] > 0 else None
                 cells_out[key] = cell
     finally:
         for r in regions.values():

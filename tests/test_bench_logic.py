@@ -27,9 +27,17 @@ sys.exit(rc)
 '''
 
 
+def _key(prefix, tmp_path, *extra):
+    """a rendezvous key unique to this test's directory (tmp_path.name alone is cut to 30 characters
+    and numbered per xdist worker, so two tests running at once could share one RCCL id file)"""
+    import hashlib
+    h = hashlib.sha1(str(tmp_path).encode()).hexdigest()[:10]
+    return "_".join([prefix, tmp_path.name, h] + [str(x) for x in extra])
+
+
 def _run(world, rank, argv, tmp_path):
     env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
-               XG_RDZV_KEY="logic_%s_%d" % (tmp_path.name, world))
+               XG_RDZV_KEY=_key("logic", tmp_path, world))
     code = DRIVER.format(repo=REPO, argv=argv)
     return subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
 
@@ -84,7 +92,7 @@ def test_bench_multi_gpu_rank0_line(world, tmp_path):
 
 def test_bench_multi_gpu_other_rank(tmp_path):
     """a non-zero rank waits for rank 0's RCCL id, runs everything, prints nothing"""
-    key = "logic_%s_%d" % (tmp_path.name, 4)
+    key = _key("logic", tmp_path, 4)
     with open("/tmp/xg_bench_rdzv_%s.bin" % key, "wb") as f:
         f.write(b"\x02" * 128)
     try:
@@ -146,7 +154,7 @@ def _run_job(world, argv, tmp_path, extra_env):
     procs = []
     for rank in range(world):
         env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
-                   XG_RDZV_KEY="fault_%s_%d" % (tmp_path.name, world), XG_FAKE_BARRIER_DIR=str(tmp_path),
+                   XG_RDZV_KEY=_key("fault", tmp_path, world), XG_FAKE_BARRIER_DIR=str(tmp_path),
                    **extra_env)
         procs.append(subprocess.Popen([sys.executable, "-c", DRIVER.format(repo=REPO, argv=argv)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
@@ -222,7 +230,10 @@ def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
     # every reference cell run on the host has a GPU cell of the same key (side_by_side)
     import bench
     assert {k for k, *_ in bench.CPU_CELLS} <= set(want)
-    assert cells["configs[3] m9"].startswith("failed") and cells["configs[3] at -d 64 KiB m9"].startswith("failed")
+    def failed(v):       # one form: its failure; several: every form's failure under "forms"
+        return str(v).startswith("failed") or (isinstance(v, dict) and "verified" not in v and
+                                                all(str(x).startswith("failed") for x in v["forms"].values()))
+    assert failed(cells["configs[3] m9"]) and failed(cells["configs[3] at -d 64 KiB m9"])
     assert "injected" in str(out["rccl_log_tail"]) or out.get("rccl_log_tail") is None
     for k, v in cells.items():
         if k not in ("configs[3] m9", "configs[3] at -d 64 KiB m9"):
@@ -232,7 +243,7 @@ def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
     # each cell's link bound: its busiest-link bytes at the per-link sweep's median rate
     assert ex["link_GBps"] == bench.link_rate(out) and ex["link_GBps"] > 0
     for k, v in cells.items():
-        if isinstance(v, dict):
+        if isinstance(v, dict) and "verified" in v:
             assert v["busiest_link_bytes"] > 0, (k, v)
             want_ms = v["busiest_link_bytes"] / (ex["link_GBps"] * 1e9) * 1e3
             assert abs(v["link_bound_ms"] - want_ms) <= 1e-4 + 1e-6 * want_ms, (k, v)
@@ -286,13 +297,13 @@ def test_watchdog_on_rank0_prints_a_line_naming_the_phase(tmp_path):
     """rank 0 of a 2-GPU job whose rank 1 never comes waits in the communicator init: the watchdog
     prints a line with value null and the phase it stopped in, then exits 124"""
     env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="2", XG_FAKE_BARRIER_DIR=str(tmp_path),
-               XG_RDZV_KEY="wd0_%s" % tmp_path.name)
+               XG_RDZV_KEY=_key("wd0", tmp_path))
     code = DRIVER.format(repo=REPO, argv=["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
                                           "--watchdog", "3"])
     try:
         p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     finally:
-        rdzv = "/tmp/xg_bench_rdzv_wd0_%s.bin" % tmp_path.name
+        rdzv = "/tmp/xg_bench_rdzv_%s.bin" % _key("wd0", tmp_path)
         if os.path.exists(rdzv):
             os.unlink(rdzv)
     assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
@@ -399,9 +410,23 @@ def test_bench_baseline_configs_time_the_relay_form_where_it_applies(tmp_path):
     cells = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])["baseline_configs_8gpu"]["cells"]
     for m in (9, 10):
         c = cells["configs[3] m%d" % m]
-        assert set(c["forms"]) == {"direct", "relay"} and c["chosen"] in c["forms"] and c["verified"], c
+        assert {"direct", "relay"} <= set(c["forms"]) and c["chosen"] in c["forms"] and c["verified"], c
+        assert c["forms"][c["chosen"]] == min(c["forms"].values()) and c["margin"] >= 0, c
     for m in (1, 2):
-        assert "forms" not in cells["configs[3] m%d" % m]
+        assert "relay" not in cells["configs[3] m%d" % m].get("forms", {})
+    # configs[4]'s 64 MiB segments are never packed: direct, and relay where it reroutes (m11 / m12)
+    for k, c in cells.items():
+        if k.startswith("configs[4] -c") and "at -d" not in k and isinstance(c, dict):
+            assert set(c.get("forms", {"direct": 0})) <= {"direct", "relay"}, (k, c)
+
+
+def test_bench_cell_forms_are_the_librarys():
+    """bench.CELL_FORMS names the library's forms (xg.py mirrors xg_sched.h)"""
+    import bench
+    import __graft_entry__ as G
+    xg = G.load_package().xg
+    assert dict(bench.CELL_FORMS) == {"direct": (0, -1), "packed_one_sided": (4 << 20, xg.PACK_ONE_SIDED),
+                                      "packed_two_sided": (4 << 20, xg.PACK_TWO_SIDED), "relay": (0, xg.RELAY)}
 
 
 def test_busiest_link_bytes_of_the_pairwise_plans(xg):

@@ -6,6 +6,7 @@ per-peer FIFO does).  Every golden configuration x method, every BASELINE config
 G = 2..8, direct and packed; bench.py's own call sequence (tuning passes included) on G
 processes; and the matcher's refusals."""
 import json
+import hashlib
 import os
 import subprocess
 import sys
@@ -166,7 +167,7 @@ def test_bench_ranks_issue_the_same_collectives(tmp_path, world):
     processes; REAL host plans): every rank issues the same sequence of barriers, MAX
     reductions, RCCL ceiling runs and plan runs, tuning passes included -- the plans it runs
     are refused up front unless their calls pair (check_pairing in MethodRun)."""
-    key = "calls_%s_%d" % (tmp_path.name, world)
+    key = "calls_%s_%s_%d" % (tmp_path.name, hashlib.sha1(str(tmp_path).encode()).hexdigest()[:10], world)
     argv = ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--watchdog", "200"]
     code = DRIVER.format(repo=REPO, argv=argv)
     procs = []
@@ -223,7 +224,7 @@ def test_self_calls_carry_the_local_part(xg, cfg):
 def test_bench_ranks_with_different_arguments_refuse_alike(tmp_path):
     """ranks started with different arguments would plan different RCCL calls and hang: every
     rank compares a digest of its arguments (one MAX reduction) and all stop with the reason"""
-    key = "calls_args_%s" % tmp_path.name
+    key = "calls_args_%s_%s" % (tmp_path.name, hashlib.sha1(str(tmp_path).encode()).hexdigest()[:10])
     procs = []
     for r, steps in ((0, "2"), (1, "3")):
         argv = ["--gpus", "2", "--steps", steps, "--warmup", "1", "--no-cpu-baseline", "--watchdog", "120"]
