@@ -24,19 +24,22 @@ pytestmark = pytest.mark.skipif(not shutil.which("gcc"), reason="gcc not found")
 
 
 def _build(out, mains):
+    """start the sanitized build of one executable -> (Popen, out)"""
     cmd = ["gcc", "-O1", "-g", *SAN, "-std=c99", "-D_POSIX_C_SOURCE=200809L", "-Wall", "-Wextra", "-Werror",
            "-I", os.path.join(REPO, "include"), "-I", HOST, "-o", out,
            *[os.path.join(HOST, m) for m in mains], os.path.join(REPO, "tests", "host_dev.c"),
            *[os.path.join(HOST, s) for s in HOST_SRCS], "-lm"]
-    subprocess.run(cmd, check=True)
-    return out
+    return subprocess.Popen(cmd), out
 
 
 @pytest.fixture(scope="module")
 def exes(tmp_path_factory):
     d = tmp_path_factory.mktemp("host_dev_bin")
-    return {"test": _build(str(d / "test"), ["main.c", "rdzv.c", "methods.c"]),
-            "pt2pt": _build(str(d / "pt2pt_test"), ["pt2pt.c", "rdzv.c"])}
+    builds = {"test": _build(str(d / "test"), ["main.c", "rdzv.c", "methods.c"]),
+              "pt2pt": _build(str(d / "pt2pt_test"), ["pt2pt.c", "rdzv.c"])}     # both at once
+    for name, (p, _out) in builds.items():
+        assert p.wait(timeout=600) == 0, "build of %s failed" % name
+    return {name: out for name, (_p, out) in builds.items()}
 
 
 def _env(tmp_path, **kw):
