@@ -2,7 +2,7 @@
 """How far is the relay form (XG_RELAY) from the best possible two-hop routing?  CPU only.
 
 For every step of the BASELINE 8-GPU plans whose messages cross GPUs, the GPU-pair traffic matrix
-D[a][b] (bytes) is routed three ways and the step's link time summed over the run:
+D[a][b] (bytes) is routed four ways and the step's link time summed over the run:
 
   direct   busiest GPU pair (one link carries each pair's bytes)
   relay    the relay form where it applies: (max egress + max ingress) / G, kept only when lower
@@ -11,6 +11,9 @@ D[a][b] (bytes) is routed three ways and the step's link time summed over the ru
            split over G paths -- straight in group 0, straight in group 1, or via relay h (a -> h
            in group 0, h -> b in group 1) -- minimising max group-0 link + max group-1 link
            (scipy linprog / HiGHS)
+  FW       a non-uniform split anyone could compute per step without an LP solver: Frank-Wolfe on
+           a soft-max of the two groups' busiest links (300 iterations, numpy) -- what a weighted
+           relay form would send; kept per step only where it beats the relay form
 
 A permutation step (m9 / m10, most of m11) is provably at its two-hop optimum under the relay
 form: with d bytes straight and r through each of the G - 2 relays, every link of the source
@@ -65,11 +68,51 @@ def lp_two_hop(D):
     return res.fun
 
 
+def fw_two_hop(D, iters=300, sharp=40.0):
+    """Frank-Wolfe on softmax(group-0 link loads) + softmax(group-1 link loads): per pair, move a
+    2 / (t + 3) share of its bytes onto its cheapest path under the current gradient; -> the best
+    T0 + T1 seen (MiB)"""
+    pairs = [(a, b) for a in range(G) for b in range(G) if a != b and D[a][b] > 0]
+    dem = np.array([D[a][b] for a, b in pairs], float)
+    y = np.zeros((len(pairs), G))
+    for i, (a, b) in enumerate(pairs):
+        y[i, a] = y[i, b] = dem[i] / 2                 # straight, half in each group
+
+    def loads(y):
+        l0, l1 = np.zeros((G, G)), np.zeros((G, G))
+        for i, (a, b) in enumerate(pairs):
+            for h in range(G):
+                if h != a:
+                    l0[a, h] += y[i, h]
+                if h != b:
+                    l1[h, b] += y[i, h]
+        return l0, l1
+
+    best = None
+    for t in range(iters + 1):
+        l0, l1 = loads(y)
+        cost = l0.max() + l1.max()
+        best = cost if best is None else min(best, cost)
+        if t == iters:
+            break
+        beta = sharp / cost
+        g0 = np.exp(beta * (l0 - l0.max()))
+        g1 = np.exp(beta * (l1 - l1.max()))
+        g0, g1 = g0 / g0.sum(), g1 / g1.sum()
+        s = np.zeros_like(y)
+        for i, (a, b) in enumerate(pairs):
+            c = [(g0[a, h] if h != a else 0.0) + (g1[h, b] if h != b else 0.0) for h in range(G)]
+            s[i, int(np.argmin(c))] = dem[i]
+        y = y + 2.0 / (t + 3) * (s - y)
+    return best
+
+
 def main():
     import __graft_entry__ as GE
     xg = GE.load_package().xg
     print("two-hop routing of the BASELINE 8-GPU plans, link time summed over the run (MiB on the busiest link)")
-    print("%-16s %-4s %10s %10s %10s %12s" % ("config", "m", "direct", "relay", "LP", "relay / LP"))
+    print("%-16s %-4s %10s %10s %10s %10s %12s %12s" % ("config", "m", "direct", "relay", "FW", "LP", "relay / LP",
+                                                        "min(relay, FW) / direct"))
     for name, P, A, d, c, methods in CONFIGS:
         rl = xg.aggregator_list(P, A)
         for m in methods:
@@ -80,7 +123,7 @@ def main():
                 if flags & 4 or a == b or ln <= 0:
                     continue
                 by.setdefault(st, [[0.0] * G for _ in range(G)])[a][b] += ln / 2 ** 20
-            direct = relay = best = 0.0
+            direct = relay = best = fwr = 0.0
             memo = {}
             for D in by.values():
                 key = tuple(map(tuple, D))
@@ -88,12 +131,15 @@ def main():
                     dd = max(max(r) for r in D)
                     eg = max(sum(r) for r in D)
                     ig = max(sum(D[a][b] for a in range(G)) for b in range(G))
-                    memo[key] = (dd, min(dd, (eg + ig) / G), lp_two_hop(D))
-                dd, rr, ll = memo[key]
+                    rr = min(dd, (eg + ig) / G)
+                    memo[key] = (dd, rr, lp_two_hop(D), min(rr, fw_two_hop(D)))
+                dd, rr, ll, ff = memo[key]
                 direct += dd
                 relay += rr
                 best += ll
-            print("%-16s %-4d %10.0f %10.0f %10.0f %12.3f" % (name, m, direct, relay, best, relay / best))
+                fwr += ff
+            print("%-16s %-4d %10.0f %10.0f %10.0f %10.0f %12.3f %12.3f"
+                  % (name, m, direct, relay, fwr, best, relay / best, fwr / direct))
             sys.stdout.flush()
 
 
