@@ -162,9 +162,13 @@ def main():
                     finally:
                         run.close()
                     if rank == 0:
+                        # steps of this rank's plan with a second RCCL group (the relay form's forwards)
+                        v = s.devplan(world, rank, pack, 0, form)
+                        relayed = sum(1 for st in range(v.nsteps)
+                                      if any(k == xg.CALL_FENCE for k, *_ in v.calls(st)))
                         print(json.dumps({"case": label, "method": method, "it": it, "form": [pack, form],
                                           "slots": int(sum(red[:world])), "want": nslots(it, direction),
-                                          "wrong": int(red[world]),
+                                          "wrong": int(red[world]), "relayed_steps": relayed,
                                           "max_total_time_s": red[world + 1], "wall_s": round(time.time() - t0, 3)}),
                               flush=True)
     ctx.barrier()

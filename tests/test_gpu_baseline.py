@@ -10,7 +10,8 @@
 2. test_config3_full_size_virtual8 / test_config4_d8m_virtual8: every byte of the 8-GPU plans
    of configs[3] (P256 A32 -d 4 MiB, m1 / m2 / m9 / m10) and configs[4] (P256 A64, m7 / m11 /
    m12, -c 1..8, at -d 8 MiB: 256 GiB for the 8 GPUs' regions) moved on the device as an 8-GPU
-   job, verified slot by slot (collision-free fingerprint).
+   job, verified slot by slot (collision-free fingerprint) -- configs[4]'s m11 / m12 in the relay
+   form too (profiles/r06/relay_c4.log).
 3. test_config4_stated_size_gpu0_share: configs[4] at its stated -d 64 MiB, GPU 0's share of the
    8-GPU job (256 GiB of regions) run alone, every -c.
 Reference: mpi_test.c:1748-1950 (m1 / m2), :421-597 (m9 / m10), :942-1114 (m11 / m12 / m7).
@@ -160,21 +161,37 @@ def test_config3_full_size_virtual8(xg, world8, method):
             r.close()
 
 
+def _relayed_steps(xg, s, G, form):
+    """steps of GPU 0's plan in `form` that post a second RCCL group (the relay form's forwards)"""
+    v = s.devplan(G, 0, form[0], 0, form[1])
+    return sum(1 for st in range(v.nsteps) if any(k == xg.CALL_FENCE for k, *_ in v.calls(st)))
+
+
 def test_config4_d8m_virtual8(xg, world8):
     """configs[4] (P256 A64, m7 / m11 / m12) at -d 8 MiB -- 16 GiB of SEND + 16 GiB of RECV per
     GPU, 256 GiB for the job -- as an 8-GPU job at every -c in 1..8 (device copies in RCCL's
-    pairing), and through RCCL itself at -c 1 and -c 8; regions allocated once per GPU"""
+    pairing), and through RCCL itself at -c 1 and -c 8; regions allocated once per GPU.  m11 / m12
+    also in the relay form (XG_RELAY), the form the N = 8 BASELINE phase times beside direct on
+    exactly these plans (profiles/r05/link_load.txt): every -c through copies, -c 1 and 8 through
+    RCCL.  m7's plan is the same in both forms (no step gains), so it runs direct only."""
     P, A, d, it = 256, 64, 8 << 20, 1
     rl = xg.aggregator_list(P, A)
     scheds = {(m, c): xg.Schedule(m, P, A, d, c, rl, ntimes=1, iteration=it) for m in (7, 11, 12)
               for c in range(1, 9)}
-    pack = ((4 << 20, -1),)           # the default: 8 MiB segments are never packed
-    regions = _shared_regions(xg, world8, [scheds[(m, 1)] for m in (7, 11, 12)], pack)
+    pack = (4 << 20, -1)              # the default: 8 MiB segments are never packed
+    relay = (0, 2)
+    regions = _shared_regions(xg, world8, list(scheds.values()), (pack, relay))
     try:
         for (m, c), s in scheds.items():
-            for rccl in ((False, True) if c in (1, 8) else (False,)):
-                res = _run_job(xg, world8, s, it, 1, pack[0][0], pack[0][1], rccl, regions)
-                _check_strong(s, res, d, it, ("m%d" % m, c, rccl), sample=5)
+            forms = [pack] + ([relay] if m != 7 else [])
+            if m != 7:       # the relay form must reroute these plans, or this test checks nothing new
+                assert _relayed_steps(xg, s, 8, relay) > 0 and _relayed_steps(xg, s, 8, pack) == 0, (m, c)
+            else:
+                assert _relayed_steps(xg, s, 8, relay) == 0
+            for form in forms:
+                for rccl in ((False, True) if c in (1, 8) else (False,)):
+                    res = _run_job(xg, world8, s, it, 1, form[0], form[1], rccl, regions)
+                    _check_strong(s, res, d, it, ("m%d" % m, c, form, rccl), sample=5)
     finally:
         for r in regions:
             r.close()

@@ -160,6 +160,22 @@ def test_relay_form_as_multi_rank_job(tmp_path, G):
     _assert_exact(rows, sum(len(c["methods"]) * 2 for c in cases))
 
 
+@pytest.mark.parametrize("c", [1, 8])
+def test_relay_form_config4_as_eight_rank_job(tmp_path, c):
+    """configs[4]'s own plans (P256 A64) in the relay form between 8 real ranks, at -d 1 MiB (the
+    smallest -d the relay form engages at: XG_RELAY_MIN_BYTES) and -c 1 / 8: m11 / m12, whose steps
+    the relay form rewrites (252 of 256 and 256 of 256 at the stated size, profiles/r05/link_load.txt),
+    and m7, which it leaves direct.  The N = 8 BASELINE phase times exactly these plans; every slot
+    is byte-checked on the device and sampled slots equal the oracle's closed form.
+    Reference: many_to_all_half_sync / all_to_many_half_sync2 (mpi_test.c:942-997, :999-1053)."""
+    cases = [{"shape": [256, 64, 1 << 20, c], "methods": [11, 12, 7], "forms": [DIRECT, RELAY]}]
+    rows = _job(tmp_path, 8, cases, timeout=140)
+    _assert_exact(rows, 6)
+    relayed = {r["method"]: r["relayed_steps"] for r in rows if r["form"] == RELAY}
+    assert relayed[11] > 0 and relayed[12] > 0 and relayed[7] == 0, relayed
+    assert all(r["relayed_steps"] == 0 for r in rows if r["form"] == DIRECT)
+
+
 def _cli(args, tmp_path, G, timeout=120, exe="test"):
     env = _env(tmp_path, XG_GPUS=G, XG_RDZV_DIR=tmp_path)
     (tmp_path / "cwd").mkdir(exist_ok=True)
