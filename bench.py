@@ -34,6 +34,7 @@ import json
 import os
 import re
 import shutil
+import statistics
 import subprocess
 import threading
 import sys
@@ -72,23 +73,23 @@ def parse():
                     help="after the line's own measurements, run BASELINE.json's 8-GPU configurations "
                          "(configs[2], [3], [4] at their stated sizes) on this job and add them to the line "
                          "(auto: only when the job has 8 GPUs)")
-    ap.add_argument("--baseline-budget", type=float, default=90.0,
+    ap.add_argument("--baseline-budget", type=float, default=130.0,
                     help="seconds the BASELINE-configs phase may take; cells past it are skipped (all ranks "
-                         "alike), and a phase still running 45 s later prints the line without the rest")
-    ap.add_argument("--xgmi-budget", type=float, default=120.0,
+                         "alike), and a phase still running GUARD_GRACE s later prints the line without the rest")
+    ap.add_argument("--xgmi-budget", type=float, default=40.0,
                     help="N > 1: seconds the xGMI ceiling + sweep phase may take before the line is printed "
                          "without the rest of it")
-    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 420)),
+    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 150)),
                     help="rank process: seconds from the communicator init to the measured value before a rank "
                          "that is still running reports the phase it is stuck in and exits 124 (0: off) -- a lost "
                          "peer leaves RCCL waiting forever; the phases after the value have guards of their own")
-    ap.add_argument("--cpu-budget", type=float, default=120.0,
+    ap.add_argument("--cpu-budget", type=float, default=40.0,
                     help="seconds the reference's configs[1] run under mpiexec may take in all")
     ap.add_argument("--cpu-configs", choices=("auto", "on", "off"), default="auto",
                     help="run the reference under mpiexec at BASELINE.json's 8-GPU configurations (configs[2] at "
-                         "full size, configs[3] at -d 64 KiB, configs[4] at -d 4 KiB for -c 1 and 8) before the "
-                         "GPUs start (auto: when the job has 8 GPUs)")
-    ap.add_argument("--cpu-configs-budget", type=float, default=150.0,
+                         "full size, configs[3] and [4] at -d 4 KiB) before the GPUs start (auto: when the job "
+                         "has 8 GPUs)")
+    ap.add_argument("--cpu-configs-budget", type=float, default=170.0,
                     help="seconds those reference cells may take in all; a cell past it is recorded as skipped")
     return ap.parse_args()
 
@@ -160,7 +161,9 @@ def start_watchdog(seconds, rank):
     return w
 
 
-GUARD_GRACE = 45.0      # a LineGuard fires this long after its phase's own budget
+GUARD_GRACE = 20.0      # a LineGuard fires this long after its phase's own budget
+CPU_GRACE = 10.0        # rank 0's reference cells stop at their budget (run_reference kills the mpiexec
+                        # session); the other ranks allow this much more for the last kill + the id file
 
 
 def pre_value_allowance(a, rank, world, parent):
@@ -169,7 +172,7 @@ def pre_value_allowance(a, rank, world, parent):
     them, so every rank allows their budgets"""
     if parent or a.no_cpu_baseline or world == 1:
         return 0.0
-    return a.cpu_budget + (a.cpu_configs_budget + GUARD_GRACE if cpu_configs_on(a, world) else 0.0)
+    return a.cpu_budget + (a.cpu_configs_budget + CPU_GRACE if cpu_configs_on(a, world) else 0.0)
 
 
 def wall_bound(a, world, parent=False):
@@ -254,19 +257,40 @@ def host_cpus():
     return n, how
 
 
-def run_reference(args, timeout):
+def reference_cpus():
+    """CPUs to pin the reference's MPI processes to: with a cgroup CPU quota below the affinity mask
+    (a one-GPU box: 16 CPUs of quota spread over 256 in the mask) the first `quota` CPUs of the mask,
+    else None (no pinning).  Busy-polling MPICH ranks spread over the whole mask burn the quota in
+    parallel and are then throttled for the rest of every period together, so a message waits for
+    the next period; pinned, they time-slice on as many CPUs as they are paid for."""
+    n, _how = host_cpus()
+    if not hasattr(os, "sched_getaffinity"):
+        return None
+    mask = sorted(os.sched_getaffinity(0))
+    return mask[:n] if n < len(mask) else None
+
+
+def run_reference(args, timeout, cpus=None):
     """one mpiexec of the reference ./test (oracle/_ref/test) in a session of its own, so a run past
     `timeout` ends with every one of its processes (its exact process group) -- busy-polling MPI
-    ranks left behind would share the host with everything after.  -> (max total time or None,
-    wall seconds, error text)"""
+    ranks left behind would share the host with everything after.  cpus: the CPU set its processes
+    inherit (reference_cpus).  -> (max total time or None, wall seconds, error text)"""
     import signal
     ref = os.path.join(REPO, "oracle", "_ref", "test")
     mpiexec = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
     if not (os.path.exists(ref) and os.path.exists(mpiexec)):
         return None, 0.0, "no reference build (oracle/_ref/test) or mpiexec on this host"
     t0 = time.time()
-    p = subprocess.Popen([mpiexec, "-launcher", "fork"] + args[:2] + [ref] + args[2:], stdout=subprocess.PIPE,
-                         stderr=subprocess.PIPE, text=True, cwd="/tmp", start_new_session=True)
+    old = None
+    if cpus:                       # the child inherits this thread's affinity at fork
+        old = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, cpus)
+    try:
+        p = subprocess.Popen([mpiexec, "-launcher", "fork"] + args[:2] + [ref] + args[2:], stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE, text=True, cwd="/tmp", start_new_session=True)
+    finally:
+        if old is not None:
+            os.sched_setaffinity(0, old)
     try:
         out, err = p.communicate(timeout=max(1.0, timeout))
     except subprocess.TimeoutExpired:
@@ -279,19 +303,25 @@ def run_reference(args, timeout):
     return float(mt[0]), time.time() - t0, ""
 
 
+def pinned_text(cpus):
+    return ("pinned to the %d CPUs %d-%d of the affinity mask (the cgroup quota's worth)" % (len(cpus), cpus[0], cpus[-1])
+            if cpus else "not pinned")
+
+
 def cpu_baseline(a, methods):
     """The reference ./test (oracle/_ref/test, built from /root/reference by oracle/Makefile)
     under MPICH on this box's host cores, same P/A/d/methods, bounded -k, --cpu-budget s in all."""
     if not os.path.exists(os.path.join(REPO, "oracle", "_ref", "test")):
         return cpu_baseline_port(a, methods)
     tot_bytes, tot_time, per = 0.0, 0.0, {}
+    cpus = reference_cpus()
     t0 = time.time()
     for m in methods:
         args = ["-n", str(a.procs), "-a", str(a.aggs), "-p", "1", "-d", str(a.size), "-m", str(m), "-i", "1",
                 "-k", str(a.cpu_reps)]
         if a.comm_size != 200000000:
             args += ["-c", str(a.comm_size)]
-        mt, _wall, err = run_reference(args, a.cpu_budget - (time.time() - t0))
+        mt, _wall, err = run_reference(args, a.cpu_budget - (time.time() - t0), cpus)
         if err.startswith("over budget"):
             return {"value": None, "unit": "GB/s", "cores": a.procs, "kind": "reference",
                     "sample": "method %d %s (--cpu-budget %.0f s)" % (m, err, a.cpu_budget)}
@@ -304,25 +334,43 @@ def cpu_baseline(a, methods):
     return {"value": round(tot_bytes / tot_time / 1e9, 4), "unit": "GB/s", "cores": min(a.procs, ncpu),
             "kind": "reference",
             "sample": "reference ./test via MPICH 3.3.2 ch3:nemesis, mpiexec -n %d (one process per logical "
-                      "rank) on %d usable host CPUs (%s)%s, -a %d -d %d -k %d, methods %s, aggregate = "
+                      "rank) on %d usable host CPUs (%s; %s)%s, -a %d -d %d -k %d, methods %s, aggregate = "
                       "sum(P*A*d*k) / sum(max total time); %.1f s wall"
-                      % (a.procs, ncpu, how, ", oversubscribed: MPICH busy-polls" if a.procs > ncpu else "",
+                      % (a.procs, ncpu, how, pinned_text(cpus),
+                         ", oversubscribed: MPICH busy-polls" if a.procs > ncpu else "",
                          a.aggs, a.size, a.cpu_reps, ",".join(map(str, methods)), time.time() - t0),
             "max_total_time_s": per}
 
 
 # (cell key, P, A, d, -c, method): BASELINE.json's 8-GPU configurations at sizes the host runs --
-# configs[2] at its stated size, configs[3]'s shape at -d 64 KiB, configs[4]'s at -d 4 KiB for -c 1
-# and 8 (64 MiB would be 1 TiB per direction in host RAM); the same keys as the GPU cells at the
-# same -d in baseline_configs_8gpu, so the two sit side by side
-_C3 = [("configs[3] at -d 64 KiB m%d" % m, 256, 32, 64 << 10, 200000000, m) for m in (1, 9, 2, 10)]
-_C4 = [("configs[4] -c %d at -d 4 KiB m%d" % (c, m), 256, 64, 4 << 10, c, m) for c, m in
-       ((1, 7), (8, 12), (1, 11), (8, 7), (1, 12), (8, 11))]
-# configs[2] first, then configs[3] and [4] cell by cell in turn: each 256-process mpiexec costs
-# ~1 min of start-up on a 16-CPU box (profiles/r05/torchrun8_shared_gpu/), so a budget that runs
-# out still leaves each configuration measured
-CPU_CELLS = ([("configs[2] m%d" % m, 64, 16, 256 << 10, 200000000, m) for m in (5, 8)] +
-             [x for pair in zip(_C3 + [None] * 2, _C4) for x in pair if x])
+# configs[2] at its stated size, configs[3]'s and configs[4]'s P256 shapes at -d 4 KiB (64 MiB would be
+# 1 TiB per direction in host RAM); the same keys as the GPU cells at the same -d in
+# baseline_configs_8gpu, so the two sit side by side.  A P256 cell on a 16-CPU host costs ~6 s of MPI
+# start-up and tear-down whatever its -d, and its exchange is latency-bound (256 busy-polling ranks
+# time-slicing: the pairwise m9 / m10 post 256 Sendrecv rounds each), so -d 4 KiB is the size at
+# which a cell costs what its schedule costs.  Order: every direction and schedule once --
+# alltoallw, a2m, m2a, half-sync a2m / m2a, pairwise, then the rest -- before any -c repeats, so a
+# budget that runs out still leaves every kind of schedule measured.
+def _c3(m):
+    return ("configs[3] at -d 4 KiB m%d" % m, 256, 32, 4 << 10, 200000000, m)
+
+
+def _c4(c, m):
+    return ("configs[4] -c %d at -d 4 KiB m%d" % (c, m), 256, 64, 4 << 10, c, m)
+
+
+def _c2(m):
+    return ("configs[2] m%d" % m, 64, 16, 256 << 10, 200000000, m)
+
+
+CPU_CELLS = [_c2(5), _c3(1), _c3(2), _c4(8, 7), _c4(8, 11), _c3(9), _c2(8), _c4(8, 12), _c3(10),
+             _c4(1, 7), _c4(1, 11), _c4(1, 12)]
+
+
+def cell_cap(a):
+    """seconds one reference cell may take: a share of the budget, so one slow cell (a pairwise
+    schedule on few CPUs) cannot leave the cells after it unmeasured"""
+    return round(max(20.0, 0.3 * a.cpu_configs_budget), 1)
 
 
 def cpu_configs_on(a, world):
@@ -335,8 +383,11 @@ def cpu_baseline_configs(a, cells=CPU_CELLS):
     that would start past it, or runs past it, is recorded as skipped.  Run before any process
     touches a GPU (the parent of an N-GPU job, or rank 0 under a launcher)."""
     ncpu, how = host_cpus()
+    cpus = reference_cpus()
+    cap = cell_cap(a)
     t0 = time.time()
-    res = {"budget_s": a.cpu_configs_budget, "cores": ncpu, "cores_how": how, "kind": "reference",
+    res = {"budget_s": a.cpu_configs_budget, "cell_cap_s": cap, "cores": ncpu, "cores_how": how,
+           "pinning": pinned_text(cpus), "kind": "reference",
            "launch": "mpiexec -launcher fork -n P oracle/_ref/test -a A -p 1 -d D -m M -i 1 -k 1 [-c C] "
                      "(MPICH 3.3.2 ch3:nemesis, busy-polling ranks)", "cells": {}}
     for key, P, A, d, c, m in cells:
@@ -347,7 +398,7 @@ def cpu_baseline_configs(a, cells=CPU_CELLS):
         args = ["-n", str(P), "-a", str(A), "-p", "1", "-d", str(d), "-m", str(m), "-i", "1", "-k", "1"]
         if c != 200000000:
             args += ["-c", str(c)]
-        mt, wall, err = run_reference(args, left)
+        mt, wall, err = run_reference(args, min(left, cap), cpus)
         if mt is None:
             res["cells"][key] = ("skipped: " if err.startswith("over budget") else "failed: ") + err
             continue
@@ -472,12 +523,14 @@ def link_sweep(ctx, world, nbytes=16 << 20, reps=5, error=RuntimeError):
     return res, None
 
 
-def busiest_link_bytes(xg, s, world, pack, form):
-    """the plan's link time in bytes: per step and per RCCL group of it, the most loaded directed GPU
-    link's bytes (the calls each GPU posts, xg_devplan_step_calls), summed over the run -- what the
-    exchange costs at one link rate however fast the rest of the node is (profiles/link_load.py)"""
+def link_bytes(xg, s, world, pack, form):
+    """the plan's link traffic from the calls each GPU posts in this form (xg_devplan_step_calls) ->
+    (busiest, total): busiest = per step and per RCCL group of it, the most loaded directed GPU link's
+    bytes, summed over the run -- what the exchange costs at one link rate however fast the rest of
+    the node is (profiles/link_load.py); total = every cross-GPU send's bytes (a relayed byte crosses
+    two links and counts twice: the traffic the links carried, beside the logical payload)"""
     views = [s.devplan(world, g, pack, 0, form) for g in range(world)]
-    tot = 0
+    busiest = total = 0
     for st in range(views[0].nsteps):
         per = {}                                  # (group, src GPU, dst GPU) -> bytes
         for g, v in enumerate(views):
@@ -487,9 +540,72 @@ def busiest_link_bytes(xg, s, world, pack, form):
                     grp += 1
                 elif kind == xg.CALL_SEND and peer != g:
                     per[(grp, g, peer)] = per.get((grp, g, peer), 0) + ln
+                    total += ln
         for q in {k[0] for k in per}:
-            tot += max(b for k, b in per.items() if k[0] == q)
-    return tot
+            busiest += max(b for k, b in per.items() if k[0] == q)
+    return busiest, total
+
+
+CALL_COST_BYTES = (1 << 20, 16 << 20)
+
+
+def call_cost(ctx, world, reps=10, error=RuntimeError):
+    """RCCL's cost per call inside a group on this node's links: all pairs at once, every transfer of
+    `bytes` posted as 1 call and as `world` calls (xg_p2p_split_bench) -- a relayed message is cut into
+    G pieces, so a relayed step posts about G x the calls of direct.  MAX time
+    over the GPUs.  -> (result, error or None): every rank stops at the same case on an error."""
+    res = {"reps": reps, "rows": []}
+    for nbytes in CALL_COST_BYTES:
+        t = {}
+        for calls in (1, world):
+            msg = None
+            try:
+                _g, sec = ctx.p2p_split_bench(nbytes, calls, reps)
+            except error as e:
+                sec, msg = 0.0, str(e)
+            t_max, err = ctx.allreduce_max([sec, 1.0 if msg else 0.0])
+            if err:
+                return res, "%d B x %d calls: %s" % (nbytes, calls, msg or "failed on another GPU")
+            t[calls] = t_max
+            res["rows"].append({"bytes": nbytes, "calls_per_peer": calls, "us_per_rep": round(t_max * 1e6, 2)})
+        # per extra send + receive pair: every rank posts (calls - 1) x (world - 1) more of each
+        res.setdefault("us_per_extra_call", {})[str(nbytes)] = round(
+            (t[world] - t[1]) * 1e6 / max(1, (world - 1) * (world - 1)), 3)
+    return res, None
+
+
+def busiest_link_bytes(xg, s, world, pack, form):
+    """link_bytes' busiest-link figure"""
+    return link_bytes(xg, s, world, pack, form)[0]
+
+
+FORM_REPS = 3           # timed runs per plan form wherever forms are compared (median / min / max)
+CHOICE_RULE = ("%d timed runs per form; direct is kept unless a form's median beats direct's by more than the "
+               "spread (max - min) of either; ms_per_run = the chosen form's median" % FORM_REPS)
+
+
+def choose_form(samples, default="direct"):
+    """The form choice of a BASELINE cell or of a method of the N > 1 line.  samples: {form: [seconds
+    of each timed run]} of the forms that verified.  `default` (direct: no staging, no second group)
+    is kept unless another form's MEDIAN beats it by more than the spread (max - min) of either form's
+    runs; among the forms that do, the lowest median wins.  Without the default, the lowest median.
+    -> (chosen, {form: {"median_ms", "min_ms", "max_ms"}}, margin): margin = (the best other median -
+    the chosen median) / the chosen median -- negative when a faster median was within the spread."""
+    st = {f: (statistics.median(v), min(v), max(v)) for f, v in samples.items() if v}
+    if not st:
+        return None, {}, None
+    if default in st:
+        dm, dlo, dhi = st[default]
+        win = [f for f, (m, lo, hi) in st.items() if f != default and dm - m > max(dhi - dlo, hi - lo)]
+        chosen = min(win, key=lambda f: st[f][0]) if win else default
+    else:
+        chosen = min(st, key=lambda f: st[f][0])
+    stats = {f: {"median_ms": round(m * 1e3, 4), "min_ms": round(lo * 1e3, 4), "max_ms": round(hi * 1e3, 4)}
+             for f, (m, lo, hi) in st.items()}
+    others = [st[f][0] for f in st if f != chosen]
+    cm = st[chosen][0]
+    margin = round((min(others) - cm) / cm, 4) if others and cm > 0 else None
+    return chosen, stats, margin
 
 
 def link_rate(out):
@@ -501,11 +617,11 @@ def link_rate(out):
 
 # ---------------------------------------------------------------- BASELINE.json's 8-GPU configurations
 # (name, P, A, d, -c, methods): configs[2], configs[3], configs[4] at their stated sizes, and
-# configs[3] / [4] at the reduced -d the reference runs at on the host (CPU_CELLS: the same keys),
+# configs[3] / [4] at the reduced -d (4 KiB) the reference runs at on the host (CPU_CELLS: the same keys),
 # ahead of configs[4]'s stated-size cells, which take most of the phase's budget
 BASELINE_CELLS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
                    ("configs[3]", 256, 32, 4 << 20, 200000000, (1, 2, 9, 10)),
-                   ("configs[3] at -d 64 KiB", 256, 32, 64 << 10, 200000000, (1, 2, 9, 10))] +
+                   ("configs[3] at -d 4 KiB", 256, 32, 4 << 10, 200000000, (1, 2, 9, 10))] +
                   [("configs[4] -c %d at -d 4 KiB" % c, 256, 64, 4 << 10, c, (7, 11, 12)) for c in (1, 8)] +
                   # the sweep's ends first: a budget that runs out mid-sweep still leaves -c 1 and 8
                   [("configs[4] -c %d" % c, 256, 64, 64 << 20, c, (7, 11, 12)) for c in (1, 8, 2, 3, 4, 5, 6, 7)])
@@ -519,14 +635,16 @@ CELL_FORMS = (("direct", (0, -1)), ("packed_one_sided", (4 << 20, 1)), ("packed_
 
 def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_CELLS, link_gbps=None):
     """Every method of BASELINE.json's 8-GPU configurations on this job: per (config, method) one
-    verified run (every slot checked on its GPU, bad slots MAX-reduced), one timed run (device
-    time, MAX over GPUs), delivered and cross-GPU (xGMI) GB/s and the reference's max total time.
+    verified run (every slot checked on its GPU, bad slots MAX-reduced), FORM_REPS timed runs (device
+    time, MAX over GPUs; the median is the figure), delivered, cross-GPU (logical payload) and on-link
+    (what the form's calls put on the links) GB/s and the reference's max total time.
     Beside each: the plan's link bound -- its busiest-link bytes (busiest_link_bytes) at the per-link
     sweep's median rate (`link_gbps`) -- and the fraction of it the run reached.
     Every cross-GPU form that changes the cell's plan -- packed one-sided / two-sided (lists of
     segments <= 4 MiB) and the relay form (XG_RELAY: configs[3]'s pairwise m9 / m10, whose XOR rounds
     put each GPU on one link; configs[4]'s m11 / m12) -- is verified and timed beside the direct
-    form, and the fastest is the cell's figure ("forms", "chosen").  Collective throughout: every rank takes the same cells
+    form; choose_form keeps direct unless another form's median beats it by more than the spread
+    ("forms": each form's median / min / max, "chosen", "margin").  Collective throughout: every rank takes the same cells
     in the same order, and every decision (budget spent, a plan or allocation that failed on some
     GPU) is MAX-reduced first, so all ranks skip alike.  Fills result["cells"] as it goes (a
     watchdog may print it half done)."""
@@ -537,7 +655,8 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
     needs = {}                        # (P, A, d, c) -> region bytes of every method and form on this GPU
 
     def measure(s, P, A, d, c, form, reg):
-        """one verified + one timed run of a plan form -> (figures, None) or (None, why)"""
+        """one verified run of a plan form, then FORM_REPS timed runs (device time, MAX over GPUs) ->
+        (figures, per-run seconds, None) or (None, None, why)"""
         run, err = None, ""
         try:
             run = xg.MethodRun(ctx, s, it=0, mode=0, regions=reg, pack_max_seg=form[0], pack_form=form[1])
@@ -546,7 +665,8 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
         if ctx.allreduce_max([1.0 if err else 0.0])[0]:
             if run is not None:
                 run.close()
-            return None, "failed: %s" % (err or "on another GPU")
+            return None, None, "failed: %s" % (err or "on another GPU")
+        runs_s = []
         try:
             ctx.barrier()
             done, post, _wall = run.run_timed()
@@ -554,28 +674,33 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
             tmax = max(s.rank_timer(q, done, post, world).total_time for q in range(lo, hi)) if hi > lo else 0.0
             _chk, bad, _first = run.verify()
             tmax, nbad = ctx.allreduce_max([tmax, float(sum(1 for b in bad if b))])
-            ctx.barrier()
-            ctx.device_sync()
-            t1 = time.perf_counter()
-            run.enqueue()
-            ctx.device_sync()
-            run.check()
-            t_run = ctx.allreduce_max([time.perf_counter() - t1])[0]
+            for _ in range(FORM_REPS if nbad == 0 else 0):
+                ctx.barrier()
+                ctx.device_sync()
+                t1 = time.perf_counter()
+                run.enqueue()
+                ctx.device_sync()
+                run.check()
+                runs_s.append(ctx.allreduce_max([time.perf_counter() - t1])[0])
         finally:
             run.close()
+        t_run = statistics.median(runs_s) if runs_s else 0.0
         cross = sum(s.devplan(world, g).remote_send_bytes for g in range(world))
         # (rank 0 prints the line; the other ranks skip the host-side plan walk)
-        busiest = busiest_link_bytes(xg, s, world, form[0], form[1]) if rank == 0 else 0
+        busiest, on_links = link_bytes(xg, s, world, form[0], form[1]) if rank == 0 else (0, 0)
         fig = {"P": P, "A": A, "d": d, "c": c, "ms_per_run": round(t_run * 1e3, 4),
-               "GBps_delivered": round(P * A * d / t_run / 1e9, 2),
-               "GBps_cross_gpu": round(cross / t_run / 1e9, 2), "cross_gpu_bytes": int(cross),
+               "runs_ms": [round(x * 1e3, 4) for x in runs_s],
+               "GBps_delivered": round(P * A * d / t_run / 1e9, 2) if t_run > 0 else None,
+               "GBps_cross_gpu": round(cross / t_run / 1e9, 2) if t_run > 0 else None, "cross_gpu_bytes": int(cross),
+               "link_bytes": int(on_links) if rank == 0 else None,
+               "GBps_link": round(on_links / t_run / 1e9, 2) if rank == 0 and t_run > 0 else None,
                "busiest_link_bytes": int(busiest) if rank == 0 else None,
                "max_total_time_s": tmax, "verified": nbad == 0, "bad_slots_max_gpu": int(nbad)}
-        if link_gbps and busiest:
+        if link_gbps and busiest and t_run > 0:
             bound_ms = busiest / (link_gbps * 1e9) * 1e3
             fig["link_bound_ms"] = round(bound_ms, 4)
-            fig["link_bound_frac"] = round(bound_ms / (t_run * 1e3), 4) if t_run > 0 else None
-        return fig, None
+            fig["link_bound_frac"] = round(bound_ms / (t_run * 1e3), 4)
+        return fig, runs_s, None
 
     try:
         for name, P, A, d, c, methods in cells:
@@ -629,24 +754,24 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                     continue
                 forms = dict(CELL_FORMS[:1])
                 forms.update((fname, f) for (fname, f), dif in zip(CELL_FORMS[1:], differs) if dif)
-                figs = {}
+                figs, samples = {}, {}
                 for fname, form in forms.items():
-                    figs[fname], why = measure(s, P, A, d, c, form, regions[(P, A, d)])
+                    figs[fname], runs_s, why = measure(s, P, A, d, c, form, regions[(P, A, d)])
                     if why:
                         figs[fname] = why
-                ok = {k: v for k, v in figs.items() if isinstance(v, dict) and v["verified"]}
-                if not ok:
+                    elif figs[fname]["verified"]:
+                        samples[fname] = runs_s
+                if not samples:
                     cells_out[key] = figs["direct"] if len(figs) == 1 else {"forms": figs}
                     continue
-                best = min(ok, key=lambda k: ok[k]["ms_per_run"])
-                cell = dict(ok[best])
+                # direct stays the cell's form unless another beats its median by more than the spread
+                best, stats, margin = choose_form(samples)
+                cell = dict(figs[best])
                 if len(figs) > 1:
                     cell["chosen"] = best
-                    cell["forms"] = {k: (v["ms_per_run"] if isinstance(v, dict) and v["verified"] else str(v))
-                                     for k, v in figs.items()}
-                    times = sorted(v["ms_per_run"] for v in ok.values())
-                    # how far ahead the chosen form is: (runner-up - chosen) / chosen
-                    cell["margin"] = round((times[1] - times[0]) / times[0], 4) if len(times) > 1 and times[0] > 0 else None
+                    cell["forms"] = {k: (stats[k] if k in stats else str(v)) for k, v in figs.items()}
+                    cell["margin"] = margin
+                    cell["choice_rule"] = CHOICE_RULE
                 cells_out[key] = cell
     finally:
         for r in regions.values():
@@ -895,13 +1020,17 @@ def xgmi_phase(xg, ctx, runs, world, nmethods, steps, elapsed, out):
     xgmi["sweep"], xgmi["sweep_error"] = p2p_sweep(ctx, world, xg.XGError)
     phase("xGMI per-link sweep")
     xgmi["links"], xgmi["links_error"] = link_sweep(ctx, world, error=xg.XGError)
+    phase("xGMI per-call cost")
+    xgmi["per_call"], xgmi["per_call_error"] = call_cost(ctx, world, error=xg.XGError)
     # the timed region's link bound: the chosen plans' busiest-link bytes per step at the median
     # measured link rate, and the share of it the timed steps reached (rank 0 prints the line)
     rate = link_rate(out)
     if rate and ctx.rank == 0:
-        busiest = sum(busiest_link_bytes(xg, r.sched, world, r.pack_max_seg, r.pack_form) for r in runs)
+        lb = [link_bytes(xg, r.sched, world, r.pack_max_seg, r.pack_form) for r in runs]
+        busiest = sum(b for b, _ in lb)
         bound_ms = busiest / (rate * 1e9) * 1e3
         xgmi["link_bound"] = {"busiest_link_bytes_per_step": int(busiest), "link_GBps": rate,
+                              "link_bytes_per_step": int(sum(x for _, x in lb)),
                               "ms_per_step": round(bound_ms, 4),
                               "frac": round(bound_ms / (elapsed / steps * 1e3), 4)}
 
@@ -989,17 +1118,26 @@ def main():
 
     # N > 1: per method, pick by measurement whether cross-GPU segments go to RCCL
     # one op per segment (direct), in runs contiguous at one end with the rest staged on
-    # the other (packed one-sided), or packed into one staging buffer per peer (pack +
-    # unpack launches, two-sided).  Every GPU sees the same MAX times -> same choice.
+    # the other (packed one-sided), packed into one staging buffer per peer (pack +
+    # unpack launches, two-sided), or -- where it reroutes some step of the method (three or
+    # more GPUs, messages >= 1 MiB) -- cut over every link in two groups (relay).  Every form
+    # is timed FORM_REPS times and choose_form keeps direct unless another form's median beats
+    # it by more than the spread.  Every GPU sees the same MAX times -> the same choice.
     tune_on = a.tune_pack == 1 or (a.tune_pack < 0 and world > 1 and a.pack_max_seg == 4 << 20)
     names = {(0, -1): "direct", (4 << 20, xg.PACK_ONE_SIDED): "packed_one_sided",
-             (4 << 20, xg.PACK_TWO_SIDED): "packed_two_sided"}
-    cands = list(names) if tune_on else [(a.pack_max_seg, -1)]
+             (4 << 20, xg.PACK_TWO_SIDED): "packed_two_sided", (0, xg.RELAY): "relay"}
+    base = [k for k in names if k != (0, xg.RELAY)] if tune_on else [(a.pack_max_seg, -1)]
     failed = {}         # method -> why each of its plan forms was refused (every form failed)
     for m in methods:
         phase("method %d: verify + plan choice" % m)
         s = xg.Schedule(m, a.procs, a.aggs, a.size, a.comm_size, rl, ntimes=1)
-        best, why = None, {}
+        cands = list(base)
+        if tune_on and world >= 3:
+            # the relay form only where it changes some GPU's plan (MAX over the GPUs: all agree)
+            v0, vr = s.devplan(world, rank, 0, 0, -1), s.devplan(world, rank, 0, 0, xg.RELAY)
+            if ctx.allreduce_max([1.0 if (vr.copies, vr.p2p) != (v0.copies, v0.p2p) else 0.0])[0]:
+                cands.append((0, xg.RELAY))
+        passed, samples, why = {}, {}, {}
         for pk, form in cands:
             fname = names.get((pk, form), "plan")
             # a form that cannot be planned, loaded or verified on SOME GPU is left out on every
@@ -1034,27 +1172,26 @@ def main():
                 done, post, _wall = r.run_timed()
                 tw.append(max(s.rank_timer(q, done, post, world).total_time for q in range(lo, hi)) if hi > lo else 0.0)
             tmax = ctx.allreduce_max([sorted(tw)[1]])[0]
-            t = timed_reps(r, 5) if len(cands) > 1 else 0.0
             if len(cands) > 1:
-                tune.setdefault(str(m), {})[fname + "_ms"] = round(t * 1e3, 4)
-            if best is None or t < best[0]:
-                if best is not None:
-                    best[1].close()
-                best = (t, r, tmax, (pk, form))
-            else:
-                r.close()
+                samples[fname] = [timed_reps(r, 2) for _ in range(FORM_REPS)]
+            passed[fname] = (r, tmax, (pk, form))
         if len(cands) > 1:
             tune.setdefault(str(m), {}).update(why)
-        if best is None:
+        if not passed:
             failed[str(m)] = why
             continue
+        chosen = next(iter(passed))
         if len(cands) > 1:
-            tune[str(m)]["chosen"] = names[best[3]]
-            times = sorted(v for k, v in tune[str(m)].items() if k.endswith("_ms"))
-            # how far ahead the chosen form is: (runner-up - chosen) / chosen
-            tune[str(m)]["margin"] = round((times[1] - times[0]) / times[0], 4) if len(times) > 1 and times[0] > 0 else None
-        max_total[str(m)] = best[2]
-        runs.append(best[1])
+            chosen, stats, margin = choose_form(samples)
+            tm = tune[str(m)]
+            for f, st in stats.items():
+                tm[f + "_ms"] = st["median_ms"]
+            tm.update(stats={f: stats[f] for f in stats}, chosen=chosen, margin=margin, choice_rule=CHOICE_RULE)
+        for f, (r, _t, _k) in passed.items():
+            if f != chosen:
+                r.close()
+        max_total[str(m)] = passed[chosen][1]
+        runs.append(passed[chosen][0])
     if failed:
         # a method none of whose forms delivered: no throughput can be quoted for the
         # workload -- say which and why in the line, then fail
@@ -1190,14 +1327,14 @@ def main():
             xgmi_phase(xg, ctx, runs, world, len(methods), a.steps, elapsed, out)
     if a.baseline_configs == "on" or (a.baseline_configs == "auto" and world == 8):
         # BASELINE.json's 8-GPU configurations on this job, after everything above is measured.
-        # The line must come out whatever happens in there: a rank still in the phase 45 s past its
-        # budget (a peer lost inside RCCL waits forever) prints the line with what was done (rank 0)
+        # The line must come out whatever happens in there: a rank still in the phase GUARD_GRACE s past
+        # its budget (a peer lost inside RCCL waits forever) prints the line with what was done (rank 0)
         # and ends its process.
         for r in runs:
             r.close()
         runs = []
         extra = out["baseline_configs_8gpu"] = {"budget_s": a.baseline_budget}
-        with LineGuard(out, rank, a.baseline_budget + 45.0, lambda msg: extra.__setitem__("error", msg)):
+        with LineGuard(out, rank, a.baseline_budget + GUARD_GRACE, lambda msg: extra.__setitem__("error", msg)):
             try:
                 extra["link_GBps"] = link_rate(out)
                 baseline_configs_phase(xg, ctx, world, rank, a.baseline_budget, extra, link_gbps=extra["link_GBps"])

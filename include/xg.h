@@ -77,7 +77,8 @@ double xg_now(void);                                           /* host seconds (
  * posting or waiting for the device -- for a watchdog to print when a run does not return. */
 const char *xg_debug_where(void);
 /* ROCm runtime libraries (libamdhip64, librccl, libhsa-runtime64) mapped into this process from
- * outside the ROCm install (/opt/rocm*, $ROCM_PATH): e.g. torch's wheel bundles its own under the
+ * outside the ROCm install libxg.so was built against (its library directory, recorded at build
+ * time) and /opt/rocm*, $ROCM_PATH: e.g. torch's wheel bundles its own under the
  * same sonames, and a process that loaded them first binds libxg.so to another HIP runtime and
  * RCCL than it was built against (profiles/r04/torch_runtime/).  Returns how many; their paths,
  * comma-separated, in buf (may be NULL).  xg_get_unique_id and xg_init refuse (XG_EARG) when
@@ -184,8 +185,16 @@ int xg_ktime_launch(xg_ctx *ctx, int k, double *ms, int64_t *bytes);
  * 2: one direction rank 1 -> rank 0.  *gbps = bytes sent by this rank per
  * second (mode 2: bytes moved 1 -> 0), *sec = seconds per repetition. */
 int xg_p2p_bench(xg_ctx *ctx, int64_t bytes, int mode, int reps, double *gbps, double *sec);
+/* xg_p2p_bench mode 0 with every (rank, peer) transfer of `bytes` posted as `calls` (1..4096)
+ * consecutive ncclSend / ncclRecv of 16-B aligned cuts of it, in one group: against calls = 1,
+ * RCCL's cost per extra call to the same peer -- what the relay form (XG_RELAY, xg_sched.h),
+ * which cuts every relayed message into G pieces, pays per step beside its link-time gain.
+ * With XG_SELF_COMM on a one-rank context: rank 0 to itself. */
+int xg_p2p_split_bench(xg_ctx *ctx, int64_t bytes, int calls, int reps, double *gbps, double *sec);
 /* One link: `bytes` each way between this rank and `peer` (send + receive in one group), reps
- * times; peer < 0 or peer == this rank: idle (returns 0 rates).  Every rank of a round calls it
+ * times; peer < 0 or peer == this rank: idle (returns 0 rates).  Every rank agrees that all have
+ * their buffers (a MAX all-reduce, idle ranks too) before any call is posted, so an allocation
+ * that fails on one rank fails the round on all (XG_ENOMEM) instead of stranding its partner.  Every rank of a round calls it
  * with its partner of that round (a 1-factorisation of the ranks), so all links of the round run
  * at once and each is measured under the others' load (the per-peer sweep of the N > 1 bench
  * line: link asymmetry shows as the spread).  *gbps = bytes this rank sent per second. */

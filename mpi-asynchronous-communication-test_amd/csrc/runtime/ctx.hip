@@ -76,6 +76,9 @@ static int foreign_cb(struct dl_phdr_info *info, size_t, void *arg)
 extern "C" int xg_foreign_runtime(char *buf, size_t len)
 {
     Foreign f;
+#ifdef XG_ROCM_LIBDIR
+    f.roots.push_back(real(XG_ROCM_LIBDIR));        // the build's own ROCm (a distro or conda install too)
+#endif
     f.roots.push_back(real("/opt/rocm"));
     if (getenv("ROCM_PATH")) f.roots.push_back(real(getenv("ROCM_PATH")));
     if (DIR *d = opendir("/opt")) {                  // versioned installs (/opt/rocm-7.2.0)
@@ -239,6 +242,9 @@ static int init_ctx(xg_ctx *c, const void *uid)
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, xgk::copy_kernel_w<xgk::kWaveKiB>, xgk::kThreads,
                                                             0));
         c->wave_grid = c->cus * (per_cu < 1 ? 1 : per_cu);
+        // piece KiB of a wave-copy launch: 0 = by its bytes (wave_kib_for), 2 / 4 / 8 forced (A/B)
+        env = getenv("XG_WAVE_KIB");
+        c->wave_kib = env && (atoi(env) == 2 || atoi(env) == 4 || atoi(env) == 8) ? atoi(env) : 0;
     }
     env = getenv("XG_STEP_CHAIN");           // "0": a step mark after every step launch
     c->step_chain = !(env && !strcmp(env, "0"));

@@ -84,9 +84,14 @@ int launch_dispatches(const xg_plan *p, int b, int n, int64_t bytes)
 static int launch_one(xg_plan *p, int b, int n, int v, hipStream_t st, unsigned long long *start)
 {
     const xgk::DCopy *pc = p->d_pieces + b;
-    if (v == 1 && p->wave_at[b]) {       // pieces of <= kWaveKiB, 16-B aligned (launch_chunk)
+    if (v == 1 && p->wave_at[b]) {       // pieces of <= wave_at[b] KiB, 16-B aligned (launch_chunk)
         const int w = std::max(1, std::min(p->ctx->wave_grid, (n + 3) / 4));
-        hipLaunchKernelGGL((xgk::copy_kernel_w<xgk::kWaveKiB>), dim3(w), dim3(xgk::kThreads), 0, st, pc, n, start);
+        if (p->wave_at[b] == 2)
+            hipLaunchKernelGGL((xgk::copy_kernel_w<2>), dim3(w), dim3(xgk::kThreads), 0, st, pc, n, start);
+        else if (p->wave_at[b] == 4)
+            hipLaunchKernelGGL((xgk::copy_kernel_w<4>), dim3(w), dim3(xgk::kThreads), 0, st, pc, n, start);
+        else
+            hipLaunchKernelGGL((xgk::copy_kernel_w<xgk::kWaveKiB>), dim3(w), dim3(xgk::kThreads), 0, st, pc, n, start);
     } else if (v == 6) hipLaunchKernelGGL((xgk::copy_kernel_g<4, true>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start);
     else hipLaunchKernelGGL((xgk::copy_kernel_g<4>), dim3(n), dim3(xgk::kThreads), 0, st, pc, start);
     HIPCHK(hipGetLastError());

@@ -439,7 +439,7 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
     // A launch of a cross-GPU step (packs, unpacks, its local part), or of a GPU-local step too
     // large for the step engine, that copies with plain loads and stores, every transfer 16-B
     // aligned, of >= wave_min bytes: copy_kernel_w over pieces of kWaveKiB (wave_at marks its
-    // first piece; profiles/r03/wave_copy/).
+    // first piece with the launch's piece KiB, wave_kib_for; profiles/r03/wave_copy/).
     int64_t chunk = c->chunk;
     std::vector<xgk::DCopy> pieces;
     std::vector<char> wave_at;
@@ -461,8 +461,9 @@ extern "C" int xg_plan_load(xg_ctx *c, xg_regions *r, const xg_devplan *dp, xg_p
         if (bytes <= 0) return;
         if (cross && bytes >= c->wave_min && bytes <= kWaveMax && (bits & 15) == 0 &&
             copy_variant(p, bytes, reread) == 1) {
-            chunk = (int64_t)xgk::kWaveKiB << 10;
-            wave_at[first] = 1;
+            const int kib = c->wave_kib ? c->wave_kib : wave_kib_for(bytes, c->cus);
+            chunk = (int64_t)kib << 10;
+            wave_at[first] = (char)kib;
             return;
         }
         std::vector<int64_t> lens;

@@ -130,6 +130,7 @@ struct xg_ctx {
     int64_t wave_min;          // cross-GPU steps' plain copy launches of >= this many bytes (and <= kWaveMax)
                                // run copy_kernel_w (launch_chunk)
     int wave_grid;             // copy_kernel_w workgroups resident at once (occupancy x CUs)
+    int wave_kib;              // XG_WAVE_KIB: copy_kernel_w piece KiB forced (2 / 4 / 8), 0 = by launch bytes
     int cus;                   // compute units
     int step_chain;            // 1: time runs of one-launch local steps by in-kernel stamps (xg_plan_run)
     int engine_arm;            // 1: xg_plan_run arms single-segment plans (doorbell)
@@ -239,7 +240,8 @@ struct xg_plan {
     std::vector<int> chain_end;
     unsigned long long *d_cstamp;  // nsteps wall-clock stamps of chained steps
     std::vector<int64_t> plen;     // prefix sums of the piece lengths (npieces + 1), host side
-    std::vector<char> wave_at;     // npieces + 1: 1 at the first piece of a copy_kernel_w launch
+    std::vector<char> wave_at;     // npieces + 1: at the first piece of a copy_kernel_w launch, its
+                                   // piece KiB (2 / 4 / 8: the J of copy_kernel_w<J>); else 0
     // hipGraph replay (XG_GRAPH=1): the launches of one xg_plan_enqueue / one timed xg_plan_run,
     // captured at first use and replayed after (a launch-bound multi-step run then costs one
     // graph launch of host time instead of a launch, an event and an RCCL group per step)
@@ -295,6 +297,16 @@ constexpr int64_t kNtStream = 4 << 20;     // ... and, in a streaming plan, laun
 constexpr int64_t kGridCacheMax = 256 << 20;   // grid_pays: a run of <= this many bytes stays in the MALL
 constexpr int64_t kWgCost = 2048;          // a copy workgroup's fixed start, bytes-equivalent (xg_piece_size)
 constexpr int64_t kWaveMax = 32 << 20;     // copy_kernel_w up to this launch size (profiles/r03/wave_local/)
+// Piece KiB of a copy_kernel_w launch of `bytes`: the largest of 8 / 4 / 2 that still gives every
+// CU a 4-wave workgroup (bytes / piece >= 4 x CUs): a 4 MiB launch in 8 KiB pieces is 512 waves =
+// 128 workgroups, half the chip (the local part of a configs[2] step, profiles/r05/share_launches/);
+// in 4 KiB pieces it is 256 workgroups.  Smaller launches take 2 KiB pieces.
+static inline int wave_kib_for(int64_t bytes, int cus)
+{
+    for (int kib = 8; kib > 2; kib /= 2)
+        if (bytes / ((int64_t)kib << 10) >= 4 * (int64_t)cus) return kib;
+    return 2;
+}
 
 // The copy kernel variant of a launch moving `bytes` (launch_copy).  Variant 0 picks
 // non-temporal loads/stores (6) when the bytes cannot come back from the 256 MiB

@@ -489,11 +489,15 @@ ROCM_RUNTIME_LIBS = ("libamdhip64.so", "librccl.so", "libhsa-runtime64.so")
 
 def foreign_rocm_runtime():
     """ROCm runtime libraries mapped into this process from outside the ROCm install libxg.so is
-    built against (/opt/rocm, or $ROCM_PATH).  torch's wheel bundles its own libamdhip64.so.7,
+    built against (lib/rocm_libdir, /opt/rocm*, or $ROCM_PATH).  torch's wheel bundles its own libamdhip64.so.7,
     librccl.so.1 and libhsa-runtime64.so.1 under the same sonames: once `import torch` has
     loaded them, libxg.so binds to those instead -- another runtime and RCCL than it was built
     and tested with (the full GPU suite hung in RCCL that way, profiles/r04/torch_runtime/)."""
     roots = {os.path.realpath(r) for r in ("/opt/rocm", os.environ.get("ROCM_PATH") or "/opt/rocm")}
+    try:        # the library directory of the ROCm libxg.so was linked against (written by the Makefile)
+        roots.add(os.path.realpath(open(os.path.join(HERE, "lib", "rocm_libdir")).read().strip()))
+    except OSError:
+        pass
     try:
         roots |= {os.path.realpath(os.path.join("/opt", n)) for n in os.listdir("/opt") if n.startswith("rocm")}
         maps = open("/proc/self/maps").read().splitlines()
@@ -572,6 +576,7 @@ def device():
         d.xg_set_copy_params.argtypes = [vp, i64, ip]
         d.xg_p2p_bench.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         d.xg_p2p_pair_bench.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        d.xg_p2p_split_bench.argtypes = [vp, i64, ip, ip, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         d.xg_rccl_version.argtypes = [C.POINTER(C.c_int)]
         _dev = d
     return _dev
@@ -648,6 +653,13 @@ class Context:
     def p2p_bench(self, nbytes, mode=0, reps=20):
         g, sec = C.c_double(), C.c_double()
         _check(_dev.xg_p2p_bench(self._c, nbytes, mode, reps, C.byref(g), C.byref(sec)), "xg_p2p_bench")
+        return g.value, sec.value
+
+    def p2p_split_bench(self, nbytes, calls, reps=20):
+        """all pairs, every transfer of `nbytes` posted as `calls` calls -> (GB/s sent, s per rep)"""
+        g, sec = C.c_double(), C.c_double()
+        _check(_dev.xg_p2p_split_bench(self._c, nbytes, calls, reps, C.byref(g), C.byref(sec)),
+               "xg_p2p_split_bench")
         return g.value, sec.value
 
     def p2p_pair_bench(self, nbytes, peer, reps=10):

@@ -130,6 +130,15 @@ def make(real_xg):
                     time.sleep(1)
             return 50.0, nbytes / 50e9
 
+        def p2p_split_bench(self, nbytes, ncalls, reps=20):
+            calls["split_bench"] = calls.get("split_bench", 0) + 1
+            trace.append(["p2p_split_bench", int(nbytes), int(ncalls), int(reps)])
+            if _on_fail_rank(self.rank) and (calls["split_bench"] - 1,) in _faults("XG_FAKE_SPLIT_FAIL"):
+                _rccl_warn("xg_p2p_split_bench: injected RCCL failure on rank %d" % self.rank)
+                raise real_xg.XGError("xg_p2p_split_bench failed with code 2 (injected)")
+            sec = nbytes / 50e9 + 5e-6 * ncalls        # 5 us per call: a visible per-call cost
+            return nbytes * (self.nranks - 1) / sec / 1e9, sec
+
         def p2p_pair_bench(self, nbytes, peer, reps=10):
             calls["pair_bench"] = calls.get("pair_bench", 0) + 1
             trace.append(["p2p_pair_bench", int(nbytes), int(reps)])     # the peer differs by rank (pair_rounds)
@@ -186,6 +195,11 @@ def make(real_xg):
 
         def enqueue(self):
             trace.append(["enqueue"] + self.key)
+            # XG_FAKE_FORM_DELAY=<pack_form>:<ms>,...: a run of that form takes that long (the
+            # form-choice rule's integration tests)
+            for f in os.environ.get("XG_FAKE_FORM_DELAY", "").split(","):
+                if f.strip() and int(f.split(":")[0]) == self.pack_form:
+                    time.sleep(float(f.split(":")[1]) / 1e3)
 
         def check(self):
             pass

@@ -92,3 +92,12 @@ def test_bench_refuses_a_foreign_rocm_runtime(tmp_path):
     assert out.returncode == 1, (out.stdout[-2000:], out.stderr[-2000:])
     line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
     assert line["value"] is None and "outside /opt/rocm" in line["error"], line
+
+
+def test_build_records_its_rocm_library_directory():
+    """a ROCm installed elsewhere (distro packages, a conda env) that libxg.so was built
+    and linked against is not foreign -- the Makefile records its library directory, in libxg.so
+    (XG_ROCM_LIBDIR, xg_foreign_runtime) and in lib/rocm_libdir (xg.py's check before loading)"""
+    libdir = os.path.realpath("/opt/rocm/lib")
+    assert open(os.path.join(PKG, "lib", "rocm_libdir")).read().strip() == libdir
+    assert libdir.encode() in open(os.path.join(PKG, "lib", "libxg.so"), "rb").read()

@@ -56,11 +56,17 @@ def test_bench_multi_gpu_rank0_line(world, tmp_path):
     assert out["xgmi"]["peak"] > 0 and out["xgmi"]["cross_gpu_bytes_per_step"] > 0
     assert out["roofline"] and out["roofline"]["bound"] == "hbm"
     assert set(out["pack_autotune_ms_per_run"]) == {"1", "2", "3", "4"}
-    forms = ("direct", "packed_one_sided", "packed_two_sided")
-    for m, tune in out["pack_autotune_ms_per_run"].items():      # every form timed, the fastest kept
-        assert set(tune) == {f + "_ms" for f in forms} | {"chosen", "margin"}, tune
-        assert tune["chosen"] in forms and tune[tune["chosen"] + "_ms"] == min(tune[f + "_ms"] for f in forms)
-        assert tune["margin"] is not None and tune["margin"] >= 0
+    for m, tune in out["pack_autotune_ms_per_run"].items():      # every form timed FORM_REPS times
+        # the relay form is a candidate where it reroutes a step: >= 3 GPUs, and configs[1]'s m3 / m4
+        forms = ("direct", "packed_one_sided", "packed_two_sided") + (("relay",) if "relay_ms" in tune else ())
+        assert set(tune) == {f + "_ms" for f in forms} | {"chosen", "margin", "stats", "choice_rule"}, tune
+        assert tune["chosen"] in forms and set(tune["stats"]) == set(forms)
+        for f in forms:
+            st = tune["stats"][f]
+            assert st["min_ms"] <= st["median_ms"] == tune[f + "_ms"] <= st["max_ms"]
+        assert tune["margin"] is not None
+    # configs[1]'s methods 1-4 have no step the relay form reroutes, at any G (tests below: where it does)
+    assert not [m for m, tune in out["pack_autotune_ms_per_run"].items() if "relay_ms" in tune]
     # the timed steps against their link bound (busiest-link bytes per step at the median link rate)
     lb = out["xgmi"]["link_bound"]
     assert lb["busiest_link_bytes_per_step"] > 0 and lb["link_GBps"] > 0 and lb["ms_per_step"] > 0
@@ -71,7 +77,7 @@ def test_bench_multi_gpu_rank0_line(world, tmp_path):
     pw = out["phase_wall_s"]
     for ph in ("start", "RCCL communicator init (ncclCommInitRank, %d ranks)" % world, "methods: verify + plan choice",
                "warm-up", "timed steps", "xGMI ceiling (RCCL all-pairs send/recv)", "xGMI p2p sweep",
-               "xGMI per-link sweep"):
+               "xGMI per-link sweep", "xGMI per-call cost"):
         assert ph in pw and pw[ph] >= 0, (ph, pw)
     links = out["xgmi"]["links"]
     assert out["xgmi"]["links_error"] is None and links["rounds"] == world - 1
@@ -82,6 +88,13 @@ def test_bench_multi_gpu_rank0_line(world, tmp_path):
     calls = json.loads([l for l in p.stdout.splitlines() if l.startswith("CALLS ")][0][6:])
     sweep = out["xgmi"]["sweep"]          # the pt2pt_test analogue: 1 -> 0 latency + all pairs, 4 sizes
     assert calls["p2p"] == 1 + len(sweep) == 9
+    # RCCL's cost per call: 1 and `world` calls per peer at 1 and 16 MiB (the fake charges 5 us a call)
+    pc = out["xgmi"]["per_call"]
+    assert out["xgmi"]["per_call_error"] is None and len(pc["rows"]) == 4
+    assert [(r["bytes"], r["calls_per_peer"]) for r in pc["rows"]] == [(b, c) for b in (1 << 20, 16 << 20) for c in (1, world)]
+    for b in ("1048576", "16777216"):
+        assert pc["us_per_extra_call"][b] == pytest.approx(5.0 / (world - 1), rel=0.01)
+    assert lb["link_bytes_per_step"] >= out["xgmi"]["cross_gpu_bytes_per_step"]
     assert [(r["mode"], r["bytes"]) for r in sweep] == [(m, b) for b in (4096, 65536, 1 << 20, 16 << 20)
                                                         for m in ("one_way_1_to_0", "all_pairs")]
     for r in sweep:
@@ -215,6 +228,7 @@ def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
     of configs[2], [3] and [4] (stated sizes) runs on the job, one verified and one timed run each,
     and lands in the line; a plan that fails on one GPU (injected: m9 on GPU 1) is recorded for that
     cell on every rank and the rest go on"""
+    import bench
     argv = ARGV2 + ["--baseline-configs", "on", "--no-ktime"]
     rcs, outs = _run_job(2, argv, tmp_path, {"XG_FAKE_PLAN_FAIL": "9:1"})
     assert rcs == [0, 0], [o[1][-1500:] for o in outs]
@@ -223,21 +237,24 @@ def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
     ex = out["baseline_configs_8gpu"]
     cells = ex["cells"]
     want = ["configs[2] m5", "configs[2] m8"] + ["configs[3] m%d" % m for m in (1, 2, 9, 10)] + \
-           ["configs[3] at -d 64 KiB m%d" % m for m in (1, 2, 9, 10)] + \
+           ["configs[3] at -d 4 KiB m%d" % m for m in (1, 2, 9, 10)] + \
            ["configs[4] -c %d at -d 4 KiB m%d" % (c, m) for c in (1, 8) for m in (7, 11, 12)] + \
            ["configs[4] -c %d m%d" % (c, m) for c in (1, 8, 2, 3, 4, 5, 6, 7) for m in (7, 11, 12)]
     assert list(cells) == want
     # every reference cell run on the host has a GPU cell of the same key (side_by_side)
-    import bench
     assert {k for k, *_ in bench.CPU_CELLS} <= set(want)
     def failed(v):       # one form: its failure; several: every form's failure under "forms"
         return str(v).startswith("failed") or (isinstance(v, dict) and "verified" not in v and
                                                 all(str(x).startswith("failed") for x in v["forms"].values()))
-    assert failed(cells["configs[3] m9"]) and failed(cells["configs[3] at -d 64 KiB m9"])
+    assert failed(cells["configs[3] m9"]) and failed(cells["configs[3] at -d 4 KiB m9"])
     assert "injected" in str(out["rccl_log_tail"]) or out.get("rccl_log_tail") is None
     for k, v in cells.items():
-        if k not in ("configs[3] m9", "configs[3] at -d 64 KiB m9"):
+        if k not in ("configs[3] m9", "configs[3] at -d 4 KiB m9"):
             assert v["verified"] and v["ms_per_run"] > 0 and v["GBps_cross_gpu"] > 0, (k, v)
+            # FORM_REPS timed runs of the chosen form, its median the figure; the bytes its calls put
+            # on the links beside the logical payload (a relayed byte crosses two links)
+            assert len(v["runs_ms"]) == bench.FORM_REPS and v["ms_per_run"] == sorted(v["runs_ms"])[1], (k, v)
+            assert v["link_bytes"] >= v["cross_gpu_bytes"] and v["GBps_link"] >= v["GBps_cross_gpu"], (k, v)
     assert cells["configs[4] -c 1 m7"]["cross_gpu_bytes"] == 256 * 64 * (64 << 20) // 2   # half the pairs cross
     assert "error" not in ex and ex["spent_s"] >= 0
     # each cell's link bound: its busiest-link bytes at the per-link sweep's median rate
@@ -357,10 +374,13 @@ def test_wall_bound_of_the_driver_runs():
     import bench
     sys.argv = ["bench.py"]
     a = bench.parse()
-    assert bench.wall_bound(a, 1) == a.watchdog == 420
+    assert bench.wall_bound(a, 1) == a.watchdog == 150
     b8 = bench.wall_bound(a, 8)
-    assert b8 == a.cpu_budget + a.cpu_configs_budget + 45 + a.watchdog + a.xgmi_budget + a.baseline_budget + 45
-    assert b8 <= 1000, b8
+    assert b8 == a.cpu_budget + a.cpu_configs_budget + bench.CPU_GRACE + a.watchdog + a.xgmi_budget + \
+        a.baseline_budget + bench.GUARD_GRACE
+    # the only driver timeout on record is 600 s (BENCH_r05.json): 30 s of headroom for the launcher
+    assert b8 <= 570, b8
+    assert bench.wall_bound(a, 2) == a.cpu_budget + a.watchdog + a.xgmi_budget <= 570
     # every guard fires after its phase's own budget, never before
     assert bench.GUARD_GRACE > 0 and bench.pre_value_allowance(a, 1, 8, parent=True) == 0
 
@@ -374,6 +394,14 @@ def test_cpu_baseline_configs_budget_and_schema(tmp_path):
     a = bench.parse()
     r = bench.cpu_baseline_configs(a)
     assert list(r["cells"]) == [k for k, *_ in bench.CPU_CELLS] and len(r["cells"]) == 12
+    # every BASELINE 8-GPU method once before any -c repeats: configs[2] m5 / m8, configs[3] m1 / m2 /
+    # m9 / m10, configs[4] m7 / m11 / m12, a2m / m2a / half-sync / pairwise in the first five
+    first9 = [(k.split(" ")[0], m) for k, *_x, m in bench.CPU_CELLS[:9]]
+    assert {"%s m%d" % km for km in first9} == \
+        {"configs[2] m5", "configs[2] m8", "configs[3] m1", "configs[3] m2", "configs[3] m9", "configs[3] m10",
+         "configs[4] m7", "configs[4] m11", "configs[4] m12"}
+    assert [m for _k, m in first9[1:6]] == [1, 2, 7, 11, 9]
+    assert r["cell_cap_s"] == bench.cell_cap(a) and "pinning" in r
     assert all(v.startswith("skipped: budget") for v in r["cells"].values())
     if not os.path.exists(os.path.join(REPO, "oracle", "_ref", "test")):
         pytest.skip("no reference build here")
@@ -411,7 +439,13 @@ def test_bench_baseline_configs_time_the_relay_form_where_it_applies(tmp_path):
     for m in (9, 10):
         c = cells["configs[3] m%d" % m]
         assert {"direct", "relay"} <= set(c["forms"]) and c["chosen"] in c["forms"] and c["verified"], c
-        assert c["forms"][c["chosen"]] == min(c["forms"].values()) and c["margin"] >= 0, c
+        for f in ("direct", "relay"):
+            st = c["forms"][f]
+            assert st["min_ms"] <= st["median_ms"] <= st["max_ms"], c
+        assert c["ms_per_run"] == c["forms"][c["chosen"]]["median_ms"] and c["margin"] is not None, c
+        # the relay form's calls put (G - 2) / G of every relayed byte on two links
+        if c["chosen"] == "relay":
+            assert c["link_bytes"] > c["cross_gpu_bytes"], c
     for m in (1, 2):
         assert "relay" not in cells["configs[3] m%d" % m].get("forms", {})
     # configs[4]'s 64 MiB segments are never packed: direct, and relay where it reroutes (m11 / m12)
@@ -444,3 +478,48 @@ def test_busiest_link_bytes_of_the_pairwise_plans(xg):
     assert bench.busiest_link_bytes(xg, s1, 8, 0, -1) == 512 << 20
     assert bench.link_rate({"xgmi": {"links": {"GBps": [[None, 40.0, 50.0], [45.0, None, 60.0], [55.0, 52.0, None]]}}}) == 52.0
     assert bench.link_rate({"xgmi": None}) is None
+
+
+def _line(outs):
+    return json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
+
+
+@pytest.mark.parametrize("delays,chosen", [
+    ("2:30", "direct"),                 # relay runs take 30 ms, the other forms ~0: direct kept
+    ("-1:60,1:60,0:60,2:10", "relay"),  # relay 10 ms against 60 ms for every other form: relay chosen
+])
+def test_headline_form_choice_weighs_the_relay_form(tmp_path, delays, chosen):
+    """a workload whose pairwise rounds the relay form reroutes (P16 A8 -d 1 MiB, m9, 3 GPUs): the N > 1
+    line's per-method choice times the relay form beside direct and both packed forms, FORM_REPS times
+    each (fake run times: XG_FAKE_FORM_DELAY), and keeps direct unless a form's median beats it by
+    more than the spread"""
+    argv = ["--gpus", "3", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-ktime", "--procs", "16",
+            "--aggs", "8", "--comm-size", "3", "--methods", "9"]
+    rcs, outs = _run_job(3, argv, tmp_path, {"XG_FAKE_FORM_DELAY": delays})
+    assert rcs == [0, 0, 0], [o[1][-1500:] for o in outs]
+    tune = _line(outs)["pack_autotune_ms_per_run"]["9"]
+    assert "relay_ms" in tune and set(tune["stats"]) == {"direct", "packed_one_sided", "packed_two_sided", "relay"}
+    assert tune["chosen"] == chosen, tune
+
+
+def test_choose_form_rule():
+    """choose_form: direct is kept unless another form's median beats it by more than the spread of
+    either; among those that do, the lowest median; without direct, the lowest median"""
+    import bench
+    ms = lambda *v: [x / 1e3 for x in v]
+    # relay's median 2 ms faster, both spreads 1 ms: relay
+    c, st, margin = bench.choose_form({"direct": ms(10, 10.5, 11), "relay": ms(8, 8.5, 9)})
+    assert c == "relay" and st["relay"]["median_ms"] == 8.5 and margin == pytest.approx(2 / 8.5, abs=1e-4)
+    # 0.5 ms faster with a 1 ms spread: direct kept, a negative margin records the faster median
+    c, st, margin = bench.choose_form({"direct": ms(10, 10.5, 11), "relay": ms(9.5, 10, 10.2)})
+    assert c == "direct" and margin < 0
+    # a noisy candidate (spread 5 ms) 3 ms ahead: direct kept
+    c, _st, _m = bench.choose_form({"direct": ms(10, 10, 10), "packed_two_sided": ms(4, 7, 9)})
+    assert c == "direct"
+    # two qualifying forms: the lower median
+    c, _st, _m = bench.choose_form({"direct": ms(10, 10, 10), "relay": ms(6, 6, 6), "packed_one_sided": ms(5, 5, 5)})
+    assert c == "packed_one_sided"
+    # direct failed verification: the lowest median of the rest
+    c, _st, margin = bench.choose_form({"relay": ms(6, 6, 7), "packed_two_sided": ms(5, 9, 9)})
+    assert c == "relay" and margin == pytest.approx(0.5)
+    assert bench.choose_form({}) == (None, {}, None)

@@ -177,12 +177,24 @@ def test_cross_gpu_step_forms(xg, form, rccl, G):
 @pytest.mark.parametrize("G", (2, 8))
 def test_wave_copy_on_every_cross_gpu_launch(xg, rccl, G, graph):
     """XG_COPY_WAVE_MIN=0: every plain, 16-B aligned copy launch of a cross-GPU step (packs,
-    unpacks, fused unpack + pack, the local part) runs copy_kernel_w over 8 KiB pieces --
-    every method, direct and both packed forms, a power-of-two -d and a ragged one (pieces of
-    every length below 8 KiB), every slot against the oracle."""
+    unpacks, fused unpack + pack, the local part) runs copy_kernel_w (these launches are small:
+    2 KiB pieces, wave_kib_for) -- every method, direct and both packed forms, a power-of-two -d
+    and a ragged one (pieces of every length below the piece size), every slot against the
+    oracle."""
+    _wave_copy_jobs(xg, rccl, G, graph, {})
+
+
+@pytest.mark.parametrize("kib", ["4", "8"])
+def test_wave_copy_piece_sizes(xg, kib):
+    """the same jobs with copy_kernel_w's piece size forced (XG_WAVE_KIB) to the 4 and 8 KiB
+    forms larger launches pick (wave_kib_for): 8 GPUs, copies"""
+    _wave_copy_jobs(xg, False, 8, False, {"XG_WAVE_KIB": kib})
+
+
+def _wave_copy_jobs(xg, rccl, G, graph, extra):
     import os
     import xg_oracle as O
-    env = {"XG_COPY_WAVE_MIN": "0"}
+    env = dict(extra, XG_COPY_WAVE_MIN="0")
     if graph:
         env["XG_GRAPH"] = "1"           # the whole job captured once and replayed (twice below)
     old = {k: os.environ.get(k) for k in env}
