@@ -76,10 +76,10 @@ def parse():
     ap.add_argument("--baseline-budget", type=float, default=130.0,
                     help="seconds the BASELINE-configs phase may take; cells past it are skipped (all ranks "
                          "alike), and a phase still running GUARD_GRACE s later prints the line without the rest")
-    ap.add_argument("--xgmi-budget", type=float, default=40.0,
+    ap.add_argument("--xgmi-budget", type=float, default=25.0,
                     help="N > 1: seconds the xGMI ceiling + sweep phase may take before the line is printed "
                          "without the rest of it")
-    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 150)),
+    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 130)),
                     help="rank process: seconds from the communicator init to the measured value before a rank "
                          "that is still running reports the phase it is stuck in and exits 124 (0: off) -- a lost "
                          "peer leaves RCCL waiting forever; the phases after the value have guards of their own")
@@ -89,7 +89,7 @@ def parse():
                     help="run the reference under mpiexec at BASELINE.json's 8-GPU configurations (configs[2] at "
                          "full size, configs[3] and [4] at -d 4 KiB) before the GPUs start (auto: when the job "
                          "has 8 GPUs)")
-    ap.add_argument("--cpu-configs-budget", type=float, default=170.0,
+    ap.add_argument("--cpu-configs-budget", type=float, default=205.0,
                     help="seconds those reference cells may take in all; a cell past it is recorded as skipped")
     return ap.parse_args()
 
@@ -630,7 +630,15 @@ BASELINE_CELLS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
 # the cross-GPU plan forms a BASELINE cell is timed in (pack_max_seg, pack_form), direct first: the
 # others only where they change the plan
 CELL_FORMS = (("direct", (0, -1)), ("packed_one_sided", (4 << 20, 1)), ("packed_two_sided", (4 << 20, 0)),
-              ("relay", (0, 2)))
+              ("relay", (0, 2)), ("relay_coalesced", (0, 3)))
+
+
+def cell_estimate_s(links, link_gbps):
+    """seconds a BASELINE cell's runs take at least: every form's verified run + FORM_REPS timed runs,
+    each its busiest-link bytes at the per-link rate (0 when no rate was measured)"""
+    if not link_gbps:
+        return 0.0
+    return sum((1 + FORM_REPS) * busiest / (link_gbps * 1e9) for busiest, _total in links.values())
 
 
 def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_CELLS, link_gbps=None):
@@ -641,8 +649,9 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
     Beside each: the plan's link bound -- its busiest-link bytes (busiest_link_bytes) at the per-link
     sweep's median rate (`link_gbps`) -- and the fraction of it the run reached.
     Every cross-GPU form that changes the cell's plan -- packed one-sided / two-sided (lists of
-    segments <= 4 MiB) and the relay form (XG_RELAY: configs[3]'s pairwise m9 / m10, whose XOR rounds
-    put each GPU on one link; configs[4]'s m11 / m12) -- is verified and timed beside the direct
+    segments <= 4 MiB) and the two relay forms (XG_RELAY, XG_RELAY_COALESCED: configs[3]'s pairwise
+    m9 / m10, whose XOR rounds put each GPU on one link; configs[4]'s m11 / m12) -- is verified and
+    timed beside the direct
     form; choose_form keeps direct unless another form's median beats it by more than the spread
     ("forms": each form's median / min / max, "chosen", "margin").  Collective throughout: every rank takes the same cells
     in the same order, and every decision (budget spent, a plan or allocation that failed on some
@@ -654,9 +663,9 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
     no_room = set()                   # (P, A, d) whose regions could not be allocated on some GPU
     needs = {}                        # (P, A, d, c) -> region bytes of every method and form on this GPU
 
-    def measure(s, P, A, d, c, form, reg):
+    def measure(s, P, A, d, c, form, reg, links):
         """one verified run of a plan form, then FORM_REPS timed runs (device time, MAX over GPUs) ->
-        (figures, per-run seconds, None) or (None, None, why)"""
+        (figures, per-run seconds, None) or (None, None, why).  links: link_bytes of the form (rank 0)"""
         run, err = None, ""
         try:
             run = xg.MethodRun(ctx, s, it=0, mode=0, regions=reg, pack_max_seg=form[0], pack_form=form[1])
@@ -687,7 +696,7 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
         t_run = statistics.median(runs_s) if runs_s else 0.0
         cross = sum(s.devplan(world, g).remote_send_bytes for g in range(world))
         # (rank 0 prints the line; the other ranks skip the host-side plan walk)
-        busiest, on_links = link_bytes(xg, s, world, form[0], form[1]) if rank == 0 else (0, 0)
+        busiest, on_links = links if rank == 0 else (0, 0)
         fig = {"P": P, "A": A, "d": d, "c": c, "ms_per_run": round(t_run * 1e3, 4),
                "runs_ms": [round(x * 1e3, 4) for x in runs_s],
                "GBps_delivered": round(P * A * d / t_run / 1e9, 2) if t_run > 0 else None,
@@ -754,9 +763,19 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                     continue
                 forms = dict(CELL_FORMS[:1])
                 forms.update((fname, f) for (fname, f), dif in zip(CELL_FORMS[1:], differs) if dif)
+                # the cell's runs at the measured link rate: a cell that would still be running when the
+                # phase's guard fires is skipped on every GPU alike (the cells after it may be shorter)
+                links = {f: link_bytes(xg, s, world, form[0], form[1]) if rank == 0 else (0, 0)
+                         for f, form in forms.items()}
+                est = cell_estimate_s(links, link_gbps) if rank == 0 else 0.0
+                est, spent = ctx.allreduce_max([est, time.time() - t0])
+                if spent + est > budget + GUARD_GRACE / 2:
+                    cells_out[key] = ("skipped: %.0f s of runs at the measured link rate would pass the phase "
+                                      "budget of %.0f s (%.0f s spent)" % (est, budget, spent))
+                    continue
                 figs, samples = {}, {}
                 for fname, form in forms.items():
-                    figs[fname], runs_s, why = measure(s, P, A, d, c, form, regions[(P, A, d)])
+                    figs[fname], runs_s, why = measure(s, P, A, d, c, form, regions[(P, A, d)], links[fname])
                     if why:
                         figs[fname] = why
                     elif figs[fname]["verified"]:
@@ -1120,23 +1139,27 @@ def main():
     # one op per segment (direct), in runs contiguous at one end with the rest staged on
     # the other (packed one-sided), packed into one staging buffer per peer (pack +
     # unpack launches, two-sided), or -- where it reroutes some step of the method (three or
-    # more GPUs, messages >= 1 MiB) -- cut over every link in two groups (relay).  Every form
+    # more GPUs, messages >= 1 MiB) -- cut over every link in two groups (relay; relay_coalesced:
+    # the same hops, one call per hop and kind).  Every form
     # is timed FORM_REPS times and choose_form keeps direct unless another form's median beats
     # it by more than the spread.  Every GPU sees the same MAX times -> the same choice.
     tune_on = a.tune_pack == 1 or (a.tune_pack < 0 and world > 1 and a.pack_max_seg == 4 << 20)
     names = {(0, -1): "direct", (4 << 20, xg.PACK_ONE_SIDED): "packed_one_sided",
-             (4 << 20, xg.PACK_TWO_SIDED): "packed_two_sided", (0, xg.RELAY): "relay"}
-    base = [k for k in names if k != (0, xg.RELAY)] if tune_on else [(a.pack_max_seg, -1)]
+             (4 << 20, xg.PACK_TWO_SIDED): "packed_two_sided", (0, xg.RELAY): "relay",
+             (0, xg.RELAY_COALESCED): "relay_coalesced"}
+    relays = ((0, xg.RELAY), (0, xg.RELAY_COALESCED))
+    base = [k for k in names if k not in relays] if tune_on else [(a.pack_max_seg, -1)]
     failed = {}         # method -> why each of its plan forms was refused (every form failed)
     for m in methods:
         phase("method %d: verify + plan choice" % m)
         s = xg.Schedule(m, a.procs, a.aggs, a.size, a.comm_size, rl, ntimes=1)
         cands = list(base)
         if tune_on and world >= 3:
-            # the relay form only where it changes some GPU's plan (MAX over the GPUs: all agree)
+            # the relay forms only where they change some GPU's plan (MAX over the GPUs: all agree;
+            # both reroute the same steps)
             v0, vr = s.devplan(world, rank, 0, 0, -1), s.devplan(world, rank, 0, 0, xg.RELAY)
             if ctx.allreduce_max([1.0 if (vr.copies, vr.p2p) != (v0.copies, v0.p2p) else 0.0])[0]:
-                cands.append((0, xg.RELAY))
+                cands.extend(relays)
         passed, samples, why = {}, {}, {}
         for pk, form in cands:
             fname = names.get((pk, form), "plan")

@@ -227,8 +227,16 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
  *                      bytes and every cross-GPU message is >= XG_RELAY_MIN_BYTES: pairwise m9 / m10
  *                      (one XOR partner per round, 16 -> 4 MiB of link time per round at configs[3]),
  *                      configs[4]'s half-sync m11.  Other steps: direct.  No copy kernel touches a
- *                      relayed byte (link-load table). */
-enum { XG_PACK_TWO_SIDED = 0, XG_PACK_ONE_SIDED = 1, XG_RELAY = 2 };
+ *                      relayed byte (link-load table).
+ *   XG_RELAY_COALESCED the relay form's steps, pieces and hops (the same link load), with each
+ *                      hop's pieces gathered into one call: group 0, per peer h, one call for the
+ *                      pieces that end at h and one for those h relays (by destination); group 1,
+ *                      per peer b, one call for this GPU's own second pieces and one per source
+ *                      whose pieces it forwards to b.  A call of one piece moves in place; a longer
+ *                      one is packed into STAGE_SEND / unpacked out of STAGE_RECV.  Pairwise rounds:
+ *                      G - 1 sends + G - 1 receives per group, where XG_RELAY posts a call per
+ *                      piece (RCCL's per-call cost: profiles/r06/relay_cost.log). */
+enum { XG_PACK_TWO_SIDED = 0, XG_PACK_ONE_SIDED = 1, XG_RELAY = 2, XG_RELAY_COALESCED = 3 };
 #define XG_PACK_FORM_DEFAULT XG_PACK_TWO_SIDED
 #define XG_RUN_CALL_BYTES (1 << 20)
 #define XG_RELAY_MIN_BYTES (1 << 20)

@@ -337,6 +337,187 @@ static void relay_calls(const xg_sched *s, const plan_bases *pb, const int *orde
     *rbase = roff;
 }
 
+/* ---- coalesced relay form (XG_RELAY_COALESCED, xg_sched.h): relay_step's steps, relay_cut's
+ * pieces, relay_gpu's hops -- so every link carries what it carries in the relay form -- but one
+ * RCCL call per (hop, kind) instead of one per piece.  RCCL serialises the calls of a group to
+ * one peer at 2.7-4 us each (profiles/r06/relay_cost.log), and the relay form posts G calls per
+ * message and direction: a pairwise round of 4 messages per GPU pair, 112 calls per GPU where
+ * the direct form posts 8.  Here GPU g posts:
+ *   group 0, per peer p: [pieces of g's messages to p that go straight (piece 0)],
+ *                        [pieces of g's messages p relays, by destination];
+ *            and receives the same two from p;
+ *   group 1, per peer p: [g's own second pieces to p], then per source a (ascending): [the block
+ *            of a's group-0 call that g relays to p] -- contiguous in g's STAGE_RECV, so it is
+ *            forwarded as it lies; and receives the same from p.
+ * A call of one piece moves in place (send from the segment, receive into the slot); a longer one
+ * is packed into STAGE_SEND in the step's pre launch and unpacked out of STAGE_RECV after the
+ * exchange (HBM copies, two orders of magnitude above a link's rate).  STAGE_RECV holds the
+ * unpacked receives from 0 on (the layout the device displacement scan rebuilds) and the relayed
+ * blocks behind them.  A pairwise round: G - 1 sends + G - 1 receives per group. */
+typedef struct {
+    const xg_sched *s;
+    const plan_bases *pb;
+    int G, g, dry;          /* dry: only sum the unpacked bytes (the relay area starts behind them) */
+    const int *bk, *bk_off; /* the step's cross messages by (source GPU, destination GPU), message order */
+    const xg_msg **pm;      /* pieces of the call being built: message, offset in it, length */
+    int64_t *po, *pl;
+    int64_t *blk;           /* [a * G + b]: where the block of a's pieces for b that g relays lies */
+    cvec *pre, *post;
+    pvec *pp;
+    int64_t sbase, ubase, rlbase, rl;   /* STAGE_SEND fill; STAGE_RECV unpack fill, relay area start / fill */
+} rcx;
+
+/* the piece of a message gs -> gd that travels via GPU h (relay_calls' assignment) */
+static int rc_piece(int gs, int gd, int h) { return h == gd ? 0 : h == gs ? 1 : 2 + h - (h > gs) - (h > gd); }
+
+/* the pieces of the messages a -> b that travel via h (b < 0: every b other than a and h,
+ * ascending), each message's in message order -> how many */
+static int rc_collect(rcx *x, int a, int b, int h)
+{
+    const int G = x->G, b0 = b < 0 ? 0 : b, b1 = b < 0 ? G : b + 1;
+    int n = 0, bb, k;
+    for (bb = b0; bb < b1; ++bb) {
+        if (bb == a || (b < 0 && bb == h)) continue;
+        for (k = x->bk_off[a * G + bb]; k < x->bk_off[a * G + bb + 1]; ++k) {
+            const xg_msg *m = &x->s->msgs[x->bk[k]];
+            const int pi = rc_piece(a, bb, h);
+            const int64_t lo = relay_cut(m->len, pi, G), hi = relay_cut(m->len, pi + 1, G);
+            if (hi <= lo) continue;
+            x->pm[n] = m; x->po[n] = lo; x->pl[n] = hi - lo; ++n;
+        }
+    }
+    return n;
+}
+
+static int64_t rc_total(const rcx *x, int n)
+{
+    int64_t t = 0;
+    int i;
+    for (i = 0; i < n; ++i) t += x->pl[i];
+    return t;
+}
+
+/* send the n collected pieces to peer in group grp: in place, or packed into STAGE_SEND */
+static void rc_send(rcx *x, int n, int peer, int grp)
+{
+    int64_t t = 0;
+    int i;
+    if (!n || x->dry) return;
+    if (n == 1) {
+        relay_push(x->pp, peer, 1, x->pm[0]->sbuf, src_off(x->pb, x->pm[0]) + x->po[0], x->pl[0], grp);
+        return;
+    }
+    for (i = 0; i < n; ++i) {
+        xg_copy *c = cpush(x->pre);
+        c->src_buf = x->pm[i]->sbuf; c->src_off = src_off(x->pb, x->pm[i]) + x->po[i];
+        c->dst_buf = XG_BUF_STAGE_SEND; c->dst_off = x->sbase + t;
+        c->len = x->pl[i];
+        t += x->pl[i];
+    }
+    relay_push(x->pp, peer, 1, XG_BUF_STAGE_SEND, x->sbase, t, grp);
+    x->sbase += t;
+}
+
+/* receive the n collected pieces (all ending at this GPU) from peer: in place, or into the unpack
+ * area of STAGE_RECV with one unpack copy per piece */
+static void rc_recv(rcx *x, int n, int peer, int grp)
+{
+    int64_t t = 0;
+    int i;
+    if (!n) return;
+    if (n == 1) {
+        if (!x->dry) relay_push(x->pp, peer, 0, x->pm[0]->dbuf, dst_off(x->pb, x->pm[0]) + x->po[0], x->pl[0], grp);
+        return;
+    }
+    for (i = 0; i < n && !x->dry; ++i) {
+        xg_copy *c = cpush(x->post);
+        c->src_buf = XG_BUF_STAGE_RECV; c->src_off = x->ubase + t;
+        c->dst_buf = x->pm[i]->dbuf; c->dst_off = dst_off(x->pb, x->pm[i]) + x->po[i];
+        c->len = x->pl[i];
+        t += x->pl[i];
+    }
+    if (x->dry) t = rc_total(x, n);
+    else relay_push(x->pp, peer, 0, XG_BUF_STAGE_RECV, x->ubase, t, grp);
+    x->ubase += t;
+}
+
+/* GPU g's calls of one relayed step (dry: only the unpack area's size, x->ubase) */
+static void rc_step(rcx *x)
+{
+    const int G = x->G, g = x->g;
+    int p, a, b, n;
+    for (p = 0; p < G; ++p) {           /* group 0 */
+        if (p == g) continue;
+        rc_send(x, rc_collect(x, g, p, p), p, 0);
+        rc_send(x, rc_collect(x, g, -1, p), p, 0);
+        rc_recv(x, rc_collect(x, p, g, g), p, 0);
+        n = rc_collect(x, p, -1, g);    /* what g relays for p: one receive into the relay area */
+        if (n && !x->dry) {
+            const int64_t at = x->rlbase + x->rl;
+            int64_t t = 0;
+            for (b = 0; b < G; ++b) {
+                if (b == p || b == g) continue;
+                x->blk[p * G + b] = at + t;
+                t += rc_total(x, rc_collect(x, p, b, g));
+            }
+            relay_push(x->pp, p, 0, XG_BUF_STAGE_RECV, at, t, 0);
+            x->rl += t;
+        }
+    }
+    for (p = 0; p < G; ++p) {           /* group 1 */
+        if (p == g) continue;
+        rc_send(x, rc_collect(x, g, p, g), p, 1);
+        for (a = 0; a < G && !x->dry; ++a)
+            if (a != g && a != p && (n = rc_collect(x, a, p, g)))
+                relay_push(x->pp, p, 1, XG_BUF_STAGE_RECV, x->blk[a * G + p], rc_total(x, n), 1);
+        rc_recv(x, rc_collect(x, p, g, p), p, 1);
+        for (a = 0; a < G; ++a)
+            if (a != g && a != p) rc_recv(x, rc_collect(x, a, g, p), p, 1);
+    }
+}
+
+/* the coalesced relay calls of step [b, e) for GPU g: packs into pre, calls into pp, unpacks into
+ * post; *sbase / *rbase: the step's STAGE_SEND / STAGE_RECV bytes.  -> 0, or -1 out of host memory */
+static int relay_coalesced_calls(const xg_sched *s, const plan_bases *pb, const int *order, int b, int e, int G,
+                                 int g, cvec *pre, pvec *pp, cvec *post, int64_t *sbase, int64_t *rbase)
+{
+    int k, rc = -1;
+    int *bk_off = (int *)calloc((size_t)G * G + 1, sizeof(int)), *fill = (int *)calloc((size_t)G * G, sizeof(int));
+    int *bk = (int *)malloc(sizeof(int) * ((size_t)(e - b) + 1));
+    const xg_msg **pm = (const xg_msg **)malloc(sizeof(xg_msg *) * ((size_t)(e - b) + 1));
+    int64_t *po = (int64_t *)malloc(sizeof(int64_t) * ((size_t)(e - b) + 1));
+    int64_t *pl = (int64_t *)malloc(sizeof(int64_t) * ((size_t)(e - b) + 1));
+    int64_t *blk = (int64_t *)calloc((size_t)G * G, sizeof(int64_t));
+    rcx x;
+    if (!bk_off || !fill || !bk || !pm || !po || !pl || !blk) goto done;
+    for (k = b; k < e; ++k) {
+        const xg_msg *m = &s->msgs[order[k]];
+        const int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
+        if (moves(m) && !is_stage(m) && gs != gd) bk_off[gs * G + gd + 1]++;
+    }
+    for (k = 0; k < G * G; ++k) bk_off[k + 1] += bk_off[k];
+    for (k = b; k < e; ++k) {
+        const xg_msg *m = &s->msgs[order[k]];
+        const int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
+        if (moves(m) && !is_stage(m) && gs != gd) bk[bk_off[gs * G + gd] + fill[gs * G + gd]++] = order[k];
+    }
+    memset(&x, 0, sizeof x);
+    x.s = s; x.pb = pb; x.G = G; x.g = g; x.bk = bk; x.bk_off = bk_off; x.pm = pm; x.po = po; x.pl = pl;
+    x.blk = blk; x.pre = pre; x.post = post; x.pp = pp;
+    x.dry = 1;
+    rc_step(&x);                        /* the unpack area's size: the relay area goes behind it */
+    x.rlbase = x.ubase;
+    x.ubase = 0;
+    x.dry = 0;
+    rc_step(&x);
+    *sbase = x.sbase;
+    *rbase = x.rlbase + x.rl;
+    rc = 0;
+done:
+    free(bk_off); free(fill); free(bk); free(pm); free(po); free(pl); free(blk);
+    return rc;
+}
+
 xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t pack_max_seg, int64_t pack_min,
                                   int form)
 {
@@ -355,8 +536,9 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
     plan_bases pb;
     memset(&pre, 0, sizeof pre); memset(&post, 0, sizeof post); memset(&pp, 0, sizeof pp);
     memset(&pb, 0, sizeof pb);
-    if (form != XG_PACK_TWO_SIDED && form != XG_PACK_ONE_SIDED && form != XG_RELAY) form = XG_PACK_FORM_DEFAULT;
-    if (form == XG_RELAY) pack_max_seg = 0;         /* relay form: every other step is direct */
+    if (form != XG_PACK_TWO_SIDED && form != XG_PACK_ONE_SIDED && form != XG_RELAY && form != XG_RELAY_COALESCED)
+        form = XG_PACK_FORM_DEFAULT;
+    if (form == XG_RELAY || form == XG_RELAY_COALESCED) pack_max_seg = 0;   /* every other step is direct */
     if (!dp || !cnt || !order || !pos || !bucket_n || !bucket_b || !os_out || !os_in || !rl_e || !rl_i || !rl_p ||
         plan_bases_init(&pb, s, G, g) ||
         !(dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan)))) {
@@ -384,7 +566,7 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
     dp->region_bytes[XG_BUF_RECV] = xg_region_bytes(s, G, g, XG_BUF_RECV);
     dp->region_bytes[XG_BUF_SCRATCH] = xg_region_bytes(s, G, g, XG_BUF_SCRATCH);
     for (st = 0; st < nst; ++st) {
-        int b = cnt[st], e = cnt[st + 1], k, p;
+        int b = cnt[st], e = cnt[st + 1], k, p, relayed;
         int64_t sbase = 0, rbase = 0;
         xg_stepplan *sp = &dp->steps[st];
         /* per-peer volume (out: [p], in: [G+p]) for the pack decision */
@@ -413,6 +595,12 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
                 bucket_n[G + gs]++; bucket_b[G + gs] += m->len;
             }
         }
+        sp->p2p_begin = pp.n;
+        sp->post_begin = post.n;
+        relayed = (form == XG_RELAY || form == XG_RELAY_COALESCED) && relay_step(s, order, b, e, G, rl_e, rl_i, rl_p);
+        /* coalesced relay: its packs follow the local copies in the pre launch */
+        if (relayed && form == XG_RELAY_COALESCED)
+            oom |= relay_coalesced_calls(s, &pb, order, b, e, G, g, &pre, &pp, &post, &sbase, &rbase) != 0;
         /* the one-sided layout of every packed list of this GPU's, both directions */
         if (form == XG_PACK_ONE_SIDED)
             for (p = 0; p < G; ++p) {
@@ -459,11 +647,9 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
         }
         sp->pre_count = pre.n - sp->pre_begin;
         /* the grouped exchange: per peer, sends then receives, message order */
-        sp->p2p_begin = pp.n;
-        sp->post_begin = post.n;
-        if (form == XG_RELAY && relay_step(s, order, b, e, G, rl_e, rl_i, rl_p)) {
+        if (relayed) {
             /* every message over all G - 1 links of its source, then of its destination (two groups) */
-            relay_calls(s, &pb, order, b, e, G, g, &pp, &rbase);
+            if (form == XG_RELAY) relay_calls(s, &pb, order, b, e, G, g, &pp, &rbase);
             for (p = 0; p < G; ++p)
                 if (p != g) {
                     dp->remote_send_bytes += bucket_b[p];

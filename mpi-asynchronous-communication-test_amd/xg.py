@@ -94,7 +94,7 @@ class Slot(C.Structure):
 
 A2M, M2A = 0, 1
 BUF_SEND, BUF_RECV, BUF_STAGE_SEND, BUF_STAGE_RECV, BUF_SCRATCH = 0, 1, 2, 3, 4
-PACK_TWO_SIDED, PACK_ONE_SIDED, RELAY = 0, 1, 2   # xg_devplan_build_form (RELAY: xg_sched.h XG_RELAY)
+PACK_TWO_SIDED, PACK_ONE_SIDED, RELAY, RELAY_COALESCED = 0, 1, 2, 3   # xg_devplan_build_form (xg_sched.h XG_RELAY, XG_RELAY_COALESCED)
 CALL_SEND, CALL_RECV, CALL_BARRIER, CALL_FENCE = 1, 2, 3, 4   # xg_call kinds
 MSG_COPY, MSG_COLL, MSG_CTRL = 1, 2, 4
 TAM_METHODS = (15, 16)

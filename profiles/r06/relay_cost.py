@@ -4,7 +4,8 @@
 1. RCCL's cost per call inside a group: xg_p2p_split_bench on a one-rank communicator
    (XG_SELF_COMM=1: rank 0 sends to itself) -- the same bytes posted as 1, 2, 4, 8, 16, 32 calls;
    the slope of time against calls is the per-call cost, the intercept the one-call time.
-2. The relay form against direct on configs[3] m9 / m10 (P256 A32, the pairwise XOR rounds the relay
+2. The relay form and the coalesced relay form (XG_RELAY_COALESCED: one call per hop and kind)
+   against direct on configs[3] m9 / m10 (P256 A32, the pairwise XOR rounds the relay
    form reroutes) as a virtual 8-GPU job whose pairs go through RCCL (xg_vplans_run_rccl: every
    GPU's calls of a step in one group on one device): device time per run, calls per step of
    GPU 0 in each form.  On one device no link is crossed, so the relay form's 4x link-time gain
@@ -71,7 +72,7 @@ def relay_vs_direct(reps=3):
         for d in (1 << 20, 4 << 20):
             for m in (9, 10):
                 s = xg.Schedule(m, P, A, d, 200000000, rl, ntimes=1, iteration=it)
-                forms = {"direct": (0, -1), "relay": (0, 2)}
+                forms = {"direct": (0, -1), "relay": (0, 2), "coalesced": (0, 3)}
                 need = [[0] * xg.NBUF for _ in range(8)]
                 for f in forms.values():
                     for g in range(8):
@@ -99,7 +100,8 @@ def relay_vs_direct(reps=3):
                                      "device_ms_max": round(max(t for t, _ in ts) * 1e3, 3),
                                      "host_ms_median": round(statistics.median(w for _, w in ts) * 1e3, 3),
                                      "gpu0_cross_calls_per_busy_step": round(cps, 2), "steps": nst, "bad_slots": bad}
-                    row["relay_over_direct"] = round(row["relay"]["device_ms_median"] / row["direct"]["device_ms_median"], 3)
+                    for f in ("relay", "coalesced"):
+                        row[f + "_over_direct"] = round(row[f]["device_ms_median"] / row["direct"]["device_ms_median"], 3)
                     out.append(row)
                     print(json.dumps(row), flush=True)
                 finally:
@@ -112,6 +114,7 @@ def relay_vs_direct(reps=3):
 
 
 if __name__ == "__main__":
-    split_costs()
+    if os.environ.get("SPLIT", "1") == "1":
+        split_costs()
     relay_vs_direct()
     print("relay_cost ok", flush=True)

@@ -4,7 +4,8 @@ this device (xg_plan_set_local_only: the product's copy launches -- pack, the lo
 side stream, unpack -- with its RCCL calls left out), so its regions are one real GPU's (32 MiB
 of segments, staging, slots: resident in the Infinity Cache as on the 8-GPU node).  REPS
 back-to-back runs; run under rocprofv3 --kernel-trace and reduce with kernel_classes.py.
-FORM: 0 two-sided (default) / 1 one-sided."""
+FORM: 0 two-sided (default) / 1 one-sided.  D_KIB: -d in KiB (default 256: GPU 0 has 16 local segments
+of -d and packs / unpacks 112 of them)."""
 import os
 import sys
 
@@ -13,7 +14,8 @@ sys.path.insert(0, REPO)
 import __graft_entry__ as G  # noqa: E402
 
 xg = G.load_package().xg
-P, A, d, GPUS, REPS = 64, 16, 256 << 10, 8, int(os.environ.get("REPS", "50"))
+P, A, GPUS, REPS = 64, 16, 8, int(os.environ.get("REPS", "50"))
+d = int(os.environ.get("D_KIB", "256")) << 10      # -d (configs[2]: 256 KiB)
 FORM = int(os.environ.get("FORM", "0"))
 rl = xg.aggregator_list(P, A)
 ctx = xg.Context.virtual(0, GPUS, device=0)

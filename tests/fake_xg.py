@@ -23,7 +23,7 @@ def make(real_xg):
     fake = types.ModuleType("xg")
     for name in ("aggregator_list", "Schedule", "XGError", "NBUF", "BUF_SEND", "BUF_RECV",
                  "BUF_STAGE_SEND", "BUF_STAGE_RECV", "BUF_SCRATCH", "PACK_TWO_SIDED", "PACK_ONE_SIDED",
-                 "RELAY", "CALL_SEND", "CALL_RECV", "CALL_BARRIER", "CALL_FENCE", "method_label", "host"):
+                 "RELAY", "RELAY_COALESCED", "CALL_SEND", "CALL_RECV", "CALL_BARRIER", "CALL_FENCE", "method_label", "host"):
         setattr(fake, name, getattr(real_xg, name))
     calls = {"p2p_bench": 0, "ktime": [], "runs": 0}
     fake.calls = calls

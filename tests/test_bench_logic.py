@@ -374,7 +374,7 @@ def test_wall_bound_of_the_driver_runs():
     import bench
     sys.argv = ["bench.py"]
     a = bench.parse()
-    assert bench.wall_bound(a, 1) == a.watchdog == 150
+    assert bench.wall_bound(a, 1) == a.watchdog == 130
     b8 = bench.wall_bound(a, 8)
     assert b8 == a.cpu_budget + a.cpu_configs_budget + bench.CPU_GRACE + a.watchdog + a.xgmi_budget + \
         a.baseline_budget + bench.GUARD_GRACE
@@ -429,7 +429,7 @@ def test_link_sweep_failure_is_recorded_with_the_rccl_tail(tmp_path):
 
 def test_bench_baseline_configs_time_the_relay_form_where_it_applies(tmp_path):
     """a 4-GPU job with the BASELINE phase on: configs[3]'s pairwise m9 / m10 (permutation rounds of
-    >= 1 MiB per GPU pair) are verified and timed in the direct and the relay form and the faster is
+    >= 1 MiB per GPU pair) are verified and timed in the direct and both relay forms and the faster is
     kept; m1 / m2 (every GPU to every GPU) have one form only"""
     argv = ["--gpus", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--methods", "1",
             "--baseline-configs", "on", "--no-ktime"]
@@ -438,20 +438,21 @@ def test_bench_baseline_configs_time_the_relay_form_where_it_applies(tmp_path):
     cells = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])["baseline_configs_8gpu"]["cells"]
     for m in (9, 10):
         c = cells["configs[3] m%d" % m]
-        assert {"direct", "relay"} <= set(c["forms"]) and c["chosen"] in c["forms"] and c["verified"], c
-        for f in ("direct", "relay"):
+        assert {"direct", "relay", "relay_coalesced"} <= set(c["forms"]) and c["chosen"] in c["forms"], c
+        assert c["verified"], c
+        for f in ("direct", "relay", "relay_coalesced"):
             st = c["forms"][f]
             assert st["min_ms"] <= st["median_ms"] <= st["max_ms"], c
         assert c["ms_per_run"] == c["forms"][c["chosen"]]["median_ms"] and c["margin"] is not None, c
         # the relay form's calls put (G - 2) / G of every relayed byte on two links
-        if c["chosen"] == "relay":
+        if c["chosen"] in ("relay", "relay_coalesced"):
             assert c["link_bytes"] > c["cross_gpu_bytes"], c
     for m in (1, 2):
-        assert "relay" not in cells["configs[3] m%d" % m].get("forms", {})
-    # configs[4]'s 64 MiB segments are never packed: direct, and relay where it reroutes (m11 / m12)
+        assert not {"relay", "relay_coalesced"} & set(cells["configs[3] m%d" % m].get("forms", {}))
+    # configs[4]'s 64 MiB segments are never packed: direct, and the relay forms where they reroute
     for k, c in cells.items():
         if k.startswith("configs[4] -c") and "at -d" not in k and isinstance(c, dict):
-            assert set(c.get("forms", {"direct": 0})) <= {"direct", "relay"}, (k, c)
+            assert set(c.get("forms", {"direct": 0})) <= {"direct", "relay", "relay_coalesced"}, (k, c)
 
 
 def test_bench_cell_forms_are_the_librarys():
@@ -460,7 +461,8 @@ def test_bench_cell_forms_are_the_librarys():
     import __graft_entry__ as G
     xg = G.load_package().xg
     assert dict(bench.CELL_FORMS) == {"direct": (0, -1), "packed_one_sided": (4 << 20, xg.PACK_ONE_SIDED),
-                                      "packed_two_sided": (4 << 20, xg.PACK_TWO_SIDED), "relay": (0, xg.RELAY)}
+                                      "packed_two_sided": (4 << 20, xg.PACK_TWO_SIDED), "relay": (0, xg.RELAY),
+                                      "relay_coalesced": (0, xg.RELAY_COALESCED)}
 
 
 def test_busiest_link_bytes_of_the_pairwise_plans(xg):
@@ -486,11 +488,12 @@ def _line(outs):
 
 @pytest.mark.parametrize("delays,chosen", [
     ("2:30", "direct"),                 # relay runs take 30 ms, the other forms ~0: direct kept
-    ("-1:60,1:60,0:60,2:10", "relay"),  # relay 10 ms against 60 ms for every other form: relay chosen
+    ("-1:60,1:60,0:60,2:10,3:40", "relay"),  # relay 10 ms against 40-60 ms for every other form
+    ("-1:60,1:60,0:60,2:30,3:10", "relay_coalesced"),
 ])
 def test_headline_form_choice_weighs_the_relay_form(tmp_path, delays, chosen):
     """a workload whose pairwise rounds the relay form reroutes (P16 A8 -d 1 MiB, m9, 3 GPUs): the N > 1
-    line's per-method choice times the relay form beside direct and both packed forms, FORM_REPS times
+    line's per-method choice times both relay forms beside direct and both packed forms, FORM_REPS times
     each (fake run times: XG_FAKE_FORM_DELAY), and keeps direct unless a form's median beats it by
     more than the spread"""
     argv = ["--gpus", "3", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-ktime", "--procs", "16",
@@ -498,7 +501,8 @@ def test_headline_form_choice_weighs_the_relay_form(tmp_path, delays, chosen):
     rcs, outs = _run_job(3, argv, tmp_path, {"XG_FAKE_FORM_DELAY": delays})
     assert rcs == [0, 0, 0], [o[1][-1500:] for o in outs]
     tune = _line(outs)["pack_autotune_ms_per_run"]["9"]
-    assert "relay_ms" in tune and set(tune["stats"]) == {"direct", "packed_one_sided", "packed_two_sided", "relay"}
+    assert "relay_ms" in tune and set(tune["stats"]) == {"direct", "packed_one_sided", "packed_two_sided", "relay",
+                                                         "relay_coalesced"}
     assert tune["chosen"] == chosen, tune
 
 
@@ -523,3 +527,12 @@ def test_choose_form_rule():
     c, _st, margin = bench.choose_form({"relay": ms(6, 6, 7), "packed_two_sided": ms(5, 9, 9)})
     assert c == "relay" and margin == pytest.approx(0.5)
     assert bench.choose_form({}) == (None, {}, None)
+
+
+def test_cell_estimate_from_the_link_rate():
+    """a BASELINE cell's least run time: every form's verified run + FORM_REPS timed runs, each its
+    busiest-link bytes at the measured per-link rate; no rate, no estimate (the cell runs)"""
+    import bench
+    links = {"direct": (50 * 10 ** 9, 0), "relay": (25 * 10 ** 9, 0)}
+    assert bench.cell_estimate_s(links, 50.0) == pytest.approx((1 + bench.FORM_REPS) * 1.5)
+    assert bench.cell_estimate_s(links, None) == 0.0

@@ -145,15 +145,17 @@ def _check_strong(s, res, d, it, tag, sample=7):
 @pytest.mark.parametrize("method", [1, 2, 9, 10])
 def test_config3_full_size_virtual8(xg, world8, method):
     """configs[3] at full size (P256 A32 -d 4 MiB: 32 GiB per direction) as an 8-GPU job: the
-    cross-GPU pairs as device copies in RCCL's pairing for direct / one-sided / two-sided / relay,
-    and through RCCL itself for the direct and relay forms"""
+    cross-GPU pairs as device copies in RCCL's pairing for direct / one-sided / two-sided / relay /
+    coalesced relay, and through RCCL itself for the direct and both relay forms"""
     P, A, d, it = 256, 32, 4 << 20, 1
     rl = xg.aggregator_list(P, A)
     s = xg.Schedule(method, P, A, d, 200000000, rl, ntimes=1, iteration=it)
     relay = (0, 2)           # XG_RELAY: m9 / m10's cross-GPU rounds over every link, two RCCL groups
-    regions = _shared_regions(xg, world8, [s], PACKINGS + (relay,))
+    coal = (0, 3)            # XG_RELAY_COALESCED: the same hops, one call per hop and kind
+    regions = _shared_regions(xg, world8, [s], PACKINGS + (relay, coal))
     try:
-        for (pack, form), rccl in [(p, False) for p in PACKINGS + (relay,)] + [(PACKINGS[0], True), (relay, True)]:
+        for (pack, form), rccl in [(p, False) for p in PACKINGS + (relay, coal)] + \
+                [(PACKINGS[0], True), (relay, True), (coal, True)]:
             res = _run_job(xg, world8, s, it, 1, pack, form, rccl, regions)
             _check_strong(s, res, d, it, ("m%d" % method, pack, form, rccl))
     finally:
@@ -171,23 +173,24 @@ def test_config4_d8m_virtual8(xg, world8):
     """configs[4] (P256 A64, m7 / m11 / m12) at -d 8 MiB -- 16 GiB of SEND + 16 GiB of RECV per
     GPU, 256 GiB for the job -- as an 8-GPU job at every -c in 1..8 (device copies in RCCL's
     pairing), and through RCCL itself at -c 1 and -c 8; regions allocated once per GPU.  m11 / m12
-    also in the relay form (XG_RELAY), the form the N = 8 BASELINE phase times beside direct on
-    exactly these plans (profiles/r05/link_load.txt): every -c through copies, -c 1 and 8 through
-    RCCL.  m7's plan is the same in both forms (no step gains), so it runs direct only."""
+    also in the relay form (XG_RELAY) and the coalesced relay form (XG_RELAY_COALESCED), the forms
+    the N = 8 BASELINE phase times beside direct on exactly these plans (profiles/r05/link_load.txt):
+    every -c through copies, -c 1 and 8 through RCCL.  m7's plan is the same in both forms (no step gains), so it runs direct only."""
     P, A, d, it = 256, 64, 8 << 20, 1
     rl = xg.aggregator_list(P, A)
     scheds = {(m, c): xg.Schedule(m, P, A, d, c, rl, ntimes=1, iteration=it) for m in (7, 11, 12)
               for c in range(1, 9)}
     pack = (4 << 20, -1)              # the default: 8 MiB segments are never packed
-    relay = (0, 2)
-    regions = _shared_regions(xg, world8, list(scheds.values()), (pack, relay))
+    relay, coal = (0, 2), (0, 3)
+    regions = _shared_regions(xg, world8, list(scheds.values()), (pack, relay, coal))
     try:
         for (m, c), s in scheds.items():
-            forms = [pack] + ([relay] if m != 7 else [])
-            if m != 7:       # the relay form must reroute these plans, or this test checks nothing new
-                assert _relayed_steps(xg, s, 8, relay) > 0 and _relayed_steps(xg, s, 8, pack) == 0, (m, c)
+            forms = [pack] + ([relay, coal] if m != 7 else [])
+            if m != 7:       # the relay forms must reroute these plans, or this test checks nothing new
+                assert _relayed_steps(xg, s, 8, pack) == 0, (m, c)
+                assert _relayed_steps(xg, s, 8, relay) == _relayed_steps(xg, s, 8, coal) > 0, (m, c)
             else:
-                assert _relayed_steps(xg, s, 8, relay) == 0
+                assert _relayed_steps(xg, s, 8, relay) == _relayed_steps(xg, s, 8, coal) == 0
             for form in forms:
                 for rccl in ((False, True) if c in (1, 8) else (False,)):
                     res = _run_job(xg, world8, s, it, 1, form[0], form[1], rccl, regions)

@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 
 WORKER = os.path.join(REPO, "tests", "multirank_worker.py")
 BIN = os.path.join(REPO, "mpi-asynchronous-communication-test_amd", "bin")
-DIRECT, ONE_SIDED, TWO_SIDED, RELAY = [0, -1], [1 << 30, 1], [1 << 30, 0], [0, 2]
+DIRECT, ONE_SIDED, TWO_SIDED, RELAY, COALESCED = [0, -1], [1 << 30, 1], [1 << 30, 0], [0, 2], [0, 3]
 
 
 def _env(tmp_path, **kw):
@@ -147,17 +147,20 @@ def test_bench_workloads_as_two_and_four_rank_jobs(tmp_path, cfg):
 
 @pytest.mark.parametrize("G", [4, 8])
 def test_relay_form_as_multi_rank_job(tmp_path, G):
-    """the relay form (XG_RELAY) between real ranks: pairwise m9 / m10 (each XOR round relayed over
-    every other GPU in two RCCL groups) and m12 / m1 (their permutation steps relayed, the rest
-    direct) at P16 A8 -d 1 MiB, and at 8 ranks configs[3]'s P256 A32 at -d 1 MiB (lists of 4 MiB per
-    round) -- every slot byte-checked on the device, sampled slots against the oracle's closed form;
-    an -d of (1 << 20) + 3 puts every piece of a relayed message at an odd address"""
-    cases = [{"shape": [16, 8, 1 << 20, 3], "methods": [9, 10, 12, 1], "forms": [DIRECT, RELAY]},
-             {"shape": [16, 8, (1 << 20) + 3, 3], "methods": [9, 10, 12], "forms": [DIRECT, RELAY]}]
+    """the relay forms (XG_RELAY, XG_RELAY_COALESCED) between real ranks: pairwise m9 / m10 (each XOR
+    round relayed over every other GPU in two RCCL groups) and m12 / m1 (their permutation steps
+    relayed, the rest direct) at P16 A8 -d 1 MiB, and at 8 ranks configs[3]'s P256 A32 at -d 1 MiB
+    (lists of 4 MiB per round: the coalesced form packs 4 pieces per call) -- every slot byte-checked
+    on the device, sampled slots against the oracle's closed form; an -d of (1 << 20) + 3 puts every
+    piece of a relayed message at an odd address"""
+    forms = [DIRECT, RELAY, COALESCED]
+    cases = [{"shape": [16, 8, 1 << 20, 3], "methods": [9, 10, 12, 1], "forms": forms},
+             {"shape": [16, 8, (1 << 20) + 3, 3], "methods": [9, 10, 12], "forms": forms},
+             {"shape": [32, 16, (1 << 20) + 3, 3], "methods": [9, 11, 12], "forms": [COALESCED]}]
     if G == 8:
-        cases.append({"shape": [256, 32, 1 << 20, 200000000], "methods": [9, 10], "forms": [DIRECT, RELAY]})
+        cases.append({"shape": [256, 32, 1 << 20, 200000000], "methods": [9, 10], "forms": forms})
     rows = _job(tmp_path, G, cases, timeout=140)
-    _assert_exact(rows, sum(len(c["methods"]) * 2 for c in cases))
+    _assert_exact(rows, sum(len(c["methods"]) * len(c["forms"]) for c in cases))
 
 
 @pytest.mark.parametrize("c", [1, 8])
@@ -167,12 +170,14 @@ def test_relay_form_config4_as_eight_rank_job(tmp_path, c):
     the relay form rewrites (252 of 256 and 256 of 256 at the stated size, profiles/r05/link_load.txt),
     and m7, which it leaves direct.  The N = 8 BASELINE phase times exactly these plans; every slot
     is byte-checked on the device and sampled slots equal the oracle's closed form.
+    The coalesced relay form (XG_RELAY_COALESCED) runs the same relayed steps.
     Reference: many_to_all_half_sync / all_to_many_half_sync2 (mpi_test.c:942-997, :999-1053)."""
-    cases = [{"shape": [256, 64, 1 << 20, c], "methods": [11, 12, 7], "forms": [DIRECT, RELAY]}]
+    cases = [{"shape": [256, 64, 1 << 20, c], "methods": [11, 12, 7], "forms": [DIRECT, RELAY, COALESCED]}]
     rows = _job(tmp_path, 8, cases, timeout=140)
-    _assert_exact(rows, 6)
-    relayed = {r["method"]: r["relayed_steps"] for r in rows if r["form"] == RELAY}
-    assert relayed[11] > 0 and relayed[12] > 0 and relayed[7] == 0, relayed
+    _assert_exact(rows, 9)
+    for form in (RELAY, COALESCED):
+        relayed = {r["method"]: r["relayed_steps"] for r in rows if r["form"] == form}
+        assert relayed[11] > 0 and relayed[12] > 0 and relayed[7] == 0, (form, relayed)
     assert all(r["relayed_steps"] == 0 for r in rows if r["form"] == DIRECT)
 
 

@@ -2,8 +2,9 @@
 
 configs[4] (P256 A64 -d 64 MiB, -c 1..8, m7/m11/m12) is the largest: on 8 GPUs each
 GPU holds 32 ranks' send segments (128 GiB) and 8 aggregators' receive slots
-(128 GiB); the per-peer staging buffers -- and the relay form's forwarding staging (<= 1.5 GiB
-at m11 -c 8) -- must not push that past one MI355X's 288 GB.
+(128 GiB); the per-peer staging buffers -- the relay form's forwarding staging (<= 1.5 GiB
+at m11 -c 8), the coalesced relay form's packed pieces and forwarded blocks (<= 5.5 GiB, m11 -c 8) --
+must not push that past one MI355X's 288 GB.
 """
 import pytest
 
@@ -21,7 +22,7 @@ def test_per_gpu_regions_fit_288gb(xg, case):
     for m in methods:
         for c in cs:
             s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
-            for pack, form in ((0, -1), (4 << 20, -1), (0, 2)):      # direct, packed, relay
+            for pack, form in ((0, -1), (4 << 20, -1), (0, 2), (0, 3)):   # direct, packed, relay, coalesced
                 tot = 0
                 for g in range(8):
                     v = s.devplan(8, g, pack, 0, form)
@@ -29,5 +30,7 @@ def test_per_gpu_regions_fit_288gb(xg, case):
                     # plan tables: <= 24 B per 32 KiB piece, 32 B per RCCL op
                     need += 24 * (sum(x[4] for x in v.copies) // 32768 + len(v.copies)) + 32 * len(v.p2p)
                     assert need < HBM, (m, c, pack, form, g, need)
+                    if form == 3:
+                        assert v.region_bytes[2] + v.region_bytes[3] <= 5632 << 20, (m, c, g, v.region_bytes)
                     tot += v.region_bytes[0] + v.region_bytes[1]
                 assert tot == 2 * P * A * d          # every segment and slot lives on exactly one GPU

@@ -19,8 +19,8 @@ CONFIGS = golden_configs()
 # direct (one call per segment), packed one-sided (runs; the default packed form), packed
 # two-sided (one staging buffer per peer and direction)
 PACKS = ((0, -1), (4 << 20, 1), (4 << 20, 0))
-# ... and the relay form (two RCCL groups in a permutation step; tests/test_relay.py)
-PACKS_RELAY = PACKS + ((0, 2),)
+# ... and the relay forms (two RCCL groups in a permutation step; tests/test_relay.py)
+PACKS_RELAY = PACKS + ((0, 2), (0, 3))
 
 
 def _ref_pairs(views):

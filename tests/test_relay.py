@@ -10,12 +10,13 @@ import pytest
 import xg_oracle as O
 from plan_exec import check_recv, simulate
 
-DIRECT, RELAY = (0, -1), (0, 2)
+DIRECT, RELAY, COALESCED = (0, -1), (0, 2), (0, 3)
 SEND, RECV, BARRIER, FENCE = 1, 2, 3, 4
 
 
+@pytest.mark.parametrize("form", [RELAY, COALESCED])
 @pytest.mark.parametrize("G, d", [(3, 1 << 20), (4, (1 << 20) + 48), (8, (1 << 20) + 3), (8, 1 << 20)])
-def test_relay_plans_deliver_every_byte(xg, G, d):
+def test_relay_plans_deliver_every_byte(xg, G, d, form):
     """P16 A8 (lists of >= 1 MiB per XOR round at every G), every method the relay form changes,
     collision-free fingerprint; 16-B aligned cuts of an unaligned -d ((1 << 20) + 3) included.
     (A plan the relay form leaves alone is the direct form's, call for call:
@@ -25,10 +26,11 @@ def test_relay_plans_deliver_every_byte(xg, G, d):
     relayed = set()
     for m in O.METHODS:
         s = xg.Schedule(m, P, A, d, 3, rl, ntimes=1, iteration=1)
-        if not any(o[5] == 1 for g in range(G) for o in s.devplan(G, g, RELAY[0], 0, RELAY[1]).p2p):
+        if not any(o[5] == 1 for g in range(G) for o in s.devplan(G, g, form[0], 0, form[1]).p2p):
             continue
         relayed.add(m)
-        _views, regs = simulate(s, G, it=1, mode=1, pack=RELAY[0], form=RELAY[1])
+        assert s.check_pairing(G, form[0], 0, form[1]) > 0
+        _views, regs = simulate(s, G, it=1, mode=1, pack=form[0], form=form[1])
         check_recv(s, G, regs, it=1, mode=1)
     assert {3, 4, 6, 9, 10, 11, 12} <= relayed, relayed
 
@@ -174,3 +176,82 @@ def test_relay_decision_follows_the_link_model(xg, m, P, A, d):
                 assert relay[g].calls(st) == direct[g].calls(st), (m, st, g)
     if d < 1 << 20:
         assert not any(o[5] for v in relay for o in v.p2p)
+
+
+def _link_bytes_by_step(views):
+    """{(step, group, src GPU, dst GPU): bytes} of every cross-GPU send"""
+    out = {}
+    for st in range(views[0].nsteps):
+        for g, v in enumerate(views):
+            q = 0
+            for kind, peer, _b, _o, ln in v.calls(st):
+                if kind == FENCE:
+                    q += 1
+                elif kind == SEND and peer != g:
+                    out[(st, q, g, peer)] = out.get((st, q, g, peer), 0) + ln
+    return out
+
+
+@pytest.mark.parametrize("m, P, A, d, c", [(9, 256, 32, 4 << 20, 200000000), (10, 256, 32, 4 << 20, 200000000),
+                                           (11, 256, 64, 8 << 20, 1), (12, 256, 64, 8 << 20, 8)])
+def test_coalesced_relay_same_links_fewer_calls(xg, m, P, A, d, c):
+    """the coalesced relay form (XG_RELAY_COALESCED) at configs[3] / configs[4]'s shapes on 8 GPUs:
+    the same steps relayed, every directed link carrying the same bytes in every step and group as the
+    relay form, every other step the direct form's call for call -- and a pairwise round (m9 / m10)
+    posts G - 1 sends + G - 1 receives per group on every GPU, where the relay form posts 112 calls
+    (4 messages per GPU pair, G calls per message and direction)"""
+    G = 8
+    s = xg.Schedule(m, P, A, d, c, xg.aggregator_list(P, A), ntimes=1)
+    assert s.check_pairing(G, COALESCED[0], 0, COALESCED[1]) > 0
+    direct = [s.devplan(G, g, DIRECT[0], 0, DIRECT[1]) for g in range(G)]
+    relay = [s.devplan(G, g, RELAY[0], 0, RELAY[1]) for g in range(G)]
+    coal = [s.devplan(G, g, COALESCED[0], 0, COALESCED[1]) for g in range(G)]
+    assert _link_bytes_by_step(coal) == _link_bytes_by_step(relay)
+    ncalls = {"relay": 0, "coalesced": 0}
+    for g in range(G):
+        for st in range(coal[g].nsteps):
+            cc, rc = coal[g].calls(st), relay[g].calls(st)
+            assert (FENCE in [x[0] for x in cc]) == (FENCE in [x[0] for x in rc]), (g, st)
+            if FENCE not in [x[0] for x in cc]:
+                assert cc == direct[g].calls(st), (g, st)
+                continue
+            ncalls["coalesced"] += sum(1 for x in cc if x[0] in (SEND, RECV))
+            ncalls["relay"] += sum(1 for x in rc if x[0] in (SEND, RECV))
+            if m in (9, 10):
+                f = [x[0] for x in cc].index(FENCE)
+                for grp in (cc[:f], cc[f + 1:]):
+                    assert sum(1 for x in grp if x[0] == SEND) == G - 1, (g, st)
+                    assert sum(1 for x in grp if x[0] == RECV) == G - 1, (g, st)
+                    assert len({x[1] for x in grp if x[0] == SEND}) == G - 1
+    assert ncalls["coalesced"] * 4 <= ncalls["relay"], ncalls
+    assert [v.remote_send_bytes for v in coal] == [v.remote_send_bytes for v in direct]
+
+
+@pytest.mark.parametrize("m", [9, 11, 12])
+def test_coalesced_relay_packs_and_unpacks(xg, m):
+    """P32 A16 on 8 GPUs (4 ranks per GPU: several messages per GPU pair, so calls carry several
+    pieces -- packed by the sender, unpacked by the receiver -- next to one-piece calls that move in
+    place), -d (1 << 20) + 3 (every piece at an odd address): every byte where the reference puts it,
+    no launch races (CPU executor), staging laid out as the device displacement scan rebuilds it"""
+    P, A, d, G = 32, 16, (1 << 20) + 3, 8
+    s = xg.Schedule(m, P, A, d, 3, xg.aggregator_list(P, A), ntimes=1, iteration=1)
+    views, regs = simulate(s, G, it=1, mode=1, pack=COALESCED[0], form=COALESCED[1])
+    check_recv(s, G, regs, it=1, mode=1)
+    packed = unpacked = 0
+    for v in views:
+        for st in range(v.nsteps):
+            pb, pc, _qb, _qc, ob, oc = v.steps[st]
+            packs = [c for c in v.copies[pb:pb + pc] if c[2] == 2]
+            unpacks = v.copies[ob:ob + oc]
+            # the displacement scan's layout: every step's packs / unpacks tile staging from 0, in order
+            off = 0
+            for c in packs:
+                assert c[3] == off
+                off += c[4]
+            off = 0
+            for c in unpacks:
+                assert c[0] == 3 and c[1] == off
+                off += c[4]
+            packed += len(packs)
+            unpacked += len(unpacks)
+    assert packed > 0 and unpacked > 0
