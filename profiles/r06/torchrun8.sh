@@ -3,7 +3,7 @@
 # box's one GPU): python -m torch.distributed.run ... bench.py --gpus 8 --steps K --warmup W with
 # the default phases (CPU baselines, xGMI phases, BASELINE configs), under a time limit.
 set -o pipefail
-out=${OUT:-gpurun_out/r06_torchrun8}
+out=${OUT:-gpurun_out/r06_torchrun8b}
 mkdir -p $out
 export XG_SHARE_GPU=1 GPU_MAX_HW_QUEUES=1
 t0=$(date +%s)
