@@ -266,3 +266,62 @@ def test_one_gpu_share_alone(xg, method):
                 run.close()
     finally:
         ctx.close()
+
+
+RELAYS = ((0, 2), (0, 3))           # XG_RELAY, XG_RELAY_COALESCED
+
+
+@pytest.mark.parametrize("rccl", [False, True])
+@pytest.mark.parametrize("G", (3, 8))
+def test_relay_forms_every_method(xg, worlds, G, rccl):
+    """both relay forms on every method 1-20 (TAM included) at P32 A16 -d (1 << 20) + 3 -- every
+    relayed piece at an odd address, the coalesced form's packs and unpacks through the LDS realign
+    path -- as a G-GPU job through copies and through RCCL: every slot byte-exact on the device,
+    sampled checksums equal the oracle's closed form; the methods the relay forms reroute include
+    the pairwise and half-sync ones"""
+    import xg_oracle as O
+    P, A, d, it = 32, 16, (1 << 20) + 3, 1
+    rl = xg.aggregator_list(P, A)
+    relayed = set()
+    for method in range(1, 21):
+        s = xg.Schedule(method, P, A, d, 3, rl, ntimes=1, iteration=it)
+        for pack, form in RELAYS:
+            v = s.devplan(G, 0, pack, 0, form)
+            if any(k == xg.CALL_FENCE for st in range(v.nsteps) for k, *_ in v.calls(st)):
+                relayed.add(method)
+            res = _run_job(xg, worlds[G], s, it, 1, pack, rccl=rccl, form=form)
+            assert res and all(nb == 0 for _slot, _ck, nb, _fb in res), (method, G, form, rccl)
+            for (src, seed, _dst, _off), ck, _nb, _fb in res[:: max(1, len(res) // 5)]:
+                assert ck == O.chk64(O.fingerprint(1, src, seed, it, d)), (method, G, form, src, seed)
+    assert {9, 10, 11, 12} <= relayed, relayed
+
+
+@pytest.mark.parametrize("step_form", ["split", "self_in_group", "local_in_fused", "graph"])
+def test_relay_forms_under_every_step_form(xg, worlds, step_form):
+    """the relay forms' steps (two RCCL groups; the coalesced form's packs, unpacks and in-place
+    pieces) beside each way a cross-GPU step's local part can travel -- side stream, self send/recv
+    in the first group, inside the fused pack launch -- and under graph replay: 8 GPUs through
+    RCCL, pairwise / half-sync / TAM methods, every slot byte-exact"""
+    import os
+    P, A, d, it = 32, 16, 1 << 20, 1
+    env = STEP_FORMS[step_form]
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        ctxs = [xg.Context.virtual(g, 8, device=0) for g in range(8)]     # the knobs are read at init
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        rl = xg.aggregator_list(P, A)
+        for method in (9, 11, 12, 15):
+            s = xg.Schedule(method, P, A, d, 3, rl, ntimes=1, iteration=it)
+            for pack, form in RELAYS:
+                res = _run_job(xg, ctxs, s, it, 1, pack, rccl=True, reps=2, form=form)
+                assert res and all(nb == 0 for _slot, _ck, nb, _fb in res), (method, form, step_form)
+    finally:
+        for c in ctxs:
+            c.close()
