@@ -104,6 +104,27 @@ def phase(name):
     PHASE_LOG.append((name, time.monotonic()))
 
 
+HEARTBEAT_S = 45.0      # rank 0 names its phase on stderr this often: a long quiet phase (the reference
+                        # at the BASELINE cells runs minutes without output) is not taken for a hang
+
+
+def start_heartbeat(seconds=HEARTBEAT_S):
+    """a daemon thread printing `bench: <phase> (<s> s in it, <s> s in all)` to stderr every `seconds`
+    -> an Event that stops it"""
+    t_start = time.monotonic()
+    stop = threading.Event()
+
+    def beat():
+        while not stop.wait(seconds):
+            now = time.monotonic()
+            t_phase = PHASE_LOG[-1][1] if PHASE_LOG else t_start
+            sys.stderr.write("bench: %s (%.0f s in it, %.0f s in all)\n" % (PHASE[0], now - t_phase, now - t_start))
+            sys.stderr.flush()
+
+    threading.Thread(target=beat, name="bench-heartbeat", daemon=True).start()
+    return stop
+
+
 def phase_walls():
     """seconds spent in each phase so far (a phase entered several times: summed)"""
     out = {}
@@ -903,9 +924,13 @@ def spawn_ranks(a):
     methods = [int(x) for x in a.methods.split(",")]
     cpu = cpu_cfg = None
     if not a.no_cpu_baseline and not stub:
+        start_heartbeat()             # the children's rank 0 has its own once they start
+        phase("cpu baseline")
         cpu = cpu_baseline(a, methods)
         if cpu_configs_on(a, a.gpus):
+            phase("cpu baseline at the BASELINE 8-GPU configurations")
             cpu_cfg = cpu_baseline_configs(a)
+        phase("children")
     key = "bench%d_%d" % (os.getpid(), int(time.time() * 1e3))
     argv = [x for x in sys.argv[1:]]
     if "--no-cpu-baseline" not in argv:
@@ -1089,6 +1114,8 @@ def main():
     # up to the communicator: the reference's CPU phases on rank 0 (under a launcher) come first
     wd = start_watchdog(a.watchdog + pre_value_allowance(a, rank, world, parent) if a.watchdog > 0 else 0, rank)
     phase("start")
+    if rank == 0:
+        start_heartbeat()
 
     # host-MPI baselines first, before this process touches the GPU (rank 0; a parent
     # process of an N-GPU job runs them itself and passes --no-cpu-baseline)

@@ -566,3 +566,15 @@ def test_bench_baseline_configs_drop_the_coalesced_staging_when_it_does_not_fit(
         assert set(cell["forms_not_run"]) == {"relay_coalesced"}, cell
     # the reduced -d configuration's regions fit whole (nothing relayed there: no relay form at all)
     assert "forms_not_run" not in cells["configs[3] at -d 4 KiB m9"]
+
+
+def test_heartbeat_names_the_phase(capfd):
+    """rank 0's heartbeat: the current phase on stderr every HEARTBEAT_S seconds, so a quiet phase
+    (minutes of the reference at the BASELINE cells) shows progress"""
+    import bench
+    bench.phase("cpu baseline at the BASELINE 8-GPU configurations")
+    stop = bench.start_heartbeat(0.2)
+    time.sleep(0.7)
+    stop.set()
+    err = capfd.readouterr().err
+    assert err.count("bench: cpu baseline at the BASELINE 8-GPU configurations (") >= 2, err
