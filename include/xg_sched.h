@@ -235,7 +235,10 @@ xg_devplan *xg_devplan_build_ex(const xg_sched *s, int ngpus, int g, int64_t pac
  *                      whose pieces it forwards to b.  A call of one piece moves in place; a longer
  *                      one is packed into STAGE_SEND / unpacked out of STAGE_RECV.  Pairwise rounds:
  *                      G - 1 sends + G - 1 receives per group, where XG_RELAY posts a call per
- *                      piece (RCCL's per-call cost: profiles/r06/relay_cost.log). */
+ *                      piece (RCCL's per-call cost: profiles/r06/relay_cost.log).  A step the
+ *                      uniform cut does not help may take a weighted two-hop split instead
+ *                      (Frank-Wolfe per step, shares in 1/1024ths of each GPU pair) when that
+ *                      carries <= 0.85 of its busiest pair's bytes: configs[4]'s m7. */
 enum { XG_PACK_TWO_SIDED = 0, XG_PACK_ONE_SIDED = 1, XG_RELAY = 2, XG_RELAY_COALESCED = 3 };
 #define XG_PACK_FORM_DEFAULT XG_PACK_TWO_SIDED
 #define XG_RUN_CALL_BYTES (1 << 20)

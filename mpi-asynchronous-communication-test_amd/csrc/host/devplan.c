@@ -7,6 +7,7 @@
 #include "sched_int.h"
 
 #include <limits.h>
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -354,11 +355,15 @@ static void relay_calls(const xg_sched *s, const plan_bases *pb, const int *orde
  * exchange (HBM copies, two orders of magnitude above a link's rate).  STAGE_RECV holds the
  * unpacked receives from 0 on (the layout the device displacement scan rebuilds) and the relayed
  * blocks behind them.  A pairwise round: G - 1 sends + G - 1 receives per group. */
+#define XG_WEIGHT_ONE 1024      /* a weighted step's shares: 1/1024ths of each GPU pair's bytes */
+
 typedef struct {
     const xg_sched *s;
     const plan_bases *pb;
     int G, g, dry;          /* dry: only sum the unpacked bytes (the relay area starts behind them) */
     const int *bk, *bk_off; /* the step's cross messages by (source GPU, destination GPU), message order */
+    const int *w;           /* weighted step: [(a * G + b) * G + h] = pair (a, b)'s share via h in
+                               1/XG_WEIGHT_ONE (weighted_step); NULL: relay_cut's uniform pieces */
     const xg_msg **pm;      /* pieces of the call being built: message, offset in it, length */
     int64_t *po, *pl;
     int64_t *blk;           /* [a * G + b]: where the block of a's pieces for b that g relays lies */
@@ -370,6 +375,26 @@ typedef struct {
 /* the piece of a message gs -> gd that travels via GPU h (relay_calls' assignment) */
 static int rc_piece(int gs, int gd, int h) { return h == gd ? 0 : h == gs ? 1 : 2 + h - (h > gs) - (h > gd); }
 
+/* cut at c / XG_WEIGHT_ONE of a message of len bytes, 16-B aligned (the last cut: len) */
+static int64_t wcut(int64_t len, int c) { return c >= XG_WEIGHT_ONE ? len : ((len * c / XG_WEIGHT_ONE) & ~(int64_t)15); }
+
+/* [lo, hi) of message m (a -> b) that travels via h: relay_cut's piece, or a weighted step's share,
+ * the shares laid out in hop order (h = 0 .. G-1) */
+static void rc_range(const rcx *x, const xg_msg *m, int a, int b, int h, int64_t *lo, int64_t *hi)
+{
+    if (x->w) {
+        const int *w = &x->w[((size_t)a * x->G + b) * x->G];
+        int c = 0, k;
+        for (k = 0; k < h; ++k) c += w[k];
+        *lo = wcut(m->len, c);
+        *hi = w[h] ? wcut(m->len, c + w[h]) : *lo;
+    } else {
+        const int pi = rc_piece(a, b, h);
+        *lo = relay_cut(m->len, pi, x->G);
+        *hi = relay_cut(m->len, pi + 1, x->G);
+    }
+}
+
 /* the pieces of the messages a -> b that travel via h (b < 0: every b other than a and h,
  * ascending), each message's in message order -> how many */
 static int rc_collect(rcx *x, int a, int b, int h)
@@ -380,8 +405,8 @@ static int rc_collect(rcx *x, int a, int b, int h)
         if (bb == a || (b < 0 && bb == h)) continue;
         for (k = x->bk_off[a * G + bb]; k < x->bk_off[a * G + bb + 1]; ++k) {
             const xg_msg *m = &x->s->msgs[x->bk[k]];
-            const int pi = rc_piece(a, bb, h);
-            const int64_t lo = relay_cut(m->len, pi, G), hi = relay_cut(m->len, pi + 1, G);
+            int64_t lo, hi;
+            rc_range(x, m, a, bb, h, &lo, &hi);
             if (hi <= lo) continue;
             x->pm[n] = m; x->po[n] = lo; x->pl[n] = hi - lo; ++n;
         }
@@ -476,10 +501,131 @@ static void rc_step(rcx *x)
     }
 }
 
+/* ---- weighted two-hop split (XG_RELAY_COALESCED on a step relay_step leaves direct).  A traffic
+ * matrix that is not a permutation -- configs[4]'s m7 (mpi_test.c:942-997): every GPU sends 512 MiB
+ * to each of 3-4 others per step, some GPUs receive from 4 -- gains nothing from the uniform cut
+ * ((max egress + max ingress) / G is not below its busiest pair), yet a non-uniform one exists: the
+ * best two-hop routing in two groups carries 0.78 of the direct form's busiest-link bytes
+ * (profiles/r05/relay_lp.txt, an LP).  Per step, Frank-Wolfe on a soft-max of the busiest group-0
+ * and group-1 links (profiles/relay_lp.py's fw_two_hop, here in C): every pair's bytes split over
+ * its G paths -- straight in group 0 (h = b), straight in group 1 (h = a), via relay h -- starting
+ * half straight in each group; each iteration moves 2 / (t + 3) of every pair onto its cheapest
+ * path under the current gradient.  The best split seen is rounded to 1/1024ths (shares under
+ * 16/1024 go to the pair's largest: each more hop is one more call), and the step is weighted
+ * when its quantised link time is at
+ * most XG_WEIGHTED_GAIN of the busiest pair's and every cross message is >= XG_RELAY_MIN_BYTES.
+ * Deterministic: every GPU computes it from the same message list with the same code. */
+#define XG_FW_ITERS 300
+#define XG_FW_SHARP 40.0
+#define XG_WEIGHTED_GAIN 0.85
+
+/* group-0 / group-1 link loads of split y (pairs pr[np][2], y[np][G] bytes) -> max l0 + max l1 */
+static double fw_cost(int G, int np, const int *pr, const double *y, double *l0, double *l1)
+{
+    int i, h, k;
+    double m0 = 0, m1 = 0;
+    memset(l0, 0, sizeof(double) * (size_t)G * G);
+    memset(l1, 0, sizeof(double) * (size_t)G * G);
+    for (i = 0; i < np; ++i) {
+        const int a = pr[2 * i], b = pr[2 * i + 1];
+        for (h = 0; h < G; ++h) {
+            if (h != a) l0[a * G + h] += y[i * G + h];
+            if (h != b) l1[h * G + b] += y[i * G + h];
+        }
+    }
+    for (k = 0; k < G * G; ++k) {
+        m0 = l0[k] > m0 ? l0[k] : m0;
+        m1 = l1[k] > m1 ? l1[k] : m1;
+    }
+    return m0 + m1;
+}
+
+/* The weighted split of step [b, e) into w[(a * G + b) * G + h] (1/XG_WEIGHT_ONE) -> 1 when the
+ * step is to be weighted, 0 when it stays direct, -1 out of host memory */
+static int weighted_step(const xg_sched *s, const int *order, int b, int e, int G, int *w)
+{
+    int k, i, h, np = 0, t, rc = -1;
+    double direct = 0, best = -1, cost;
+    double *D = (double *)calloc((size_t)G * G, sizeof(double));
+    int *pr = (int *)malloc(sizeof(int) * 2 * (size_t)G * G);
+    double *y = (double *)calloc((size_t)G * G * G, sizeof(double)), *yb = (double *)calloc((size_t)G * G * G, sizeof(double));
+    double *l0 = (double *)malloc(sizeof(double) * (size_t)G * G), *l1 = (double *)malloc(sizeof(double) * (size_t)G * G);
+    double *g0 = (double *)malloc(sizeof(double) * (size_t)G * G), *g1 = (double *)malloc(sizeof(double) * (size_t)G * G);
+    if (!D || !pr || !y || !yb || !l0 || !l1 || !g0 || !g1) goto done;
+    rc = 0;
+    if (G < 3) goto done;
+    for (k = b; k < e; ++k) {
+        const xg_msg *m = &s->msgs[order[k]];
+        const int gs = xg_gpu_of(s->P, G, m->src), gd = xg_gpu_of(s->P, G, m->dst);
+        if (!moves(m) || is_stage(m) || gs == gd) continue;
+        if (m->len < XG_RELAY_MIN_BYTES) goto done;
+        D[gs * G + gd] += (double)m->len;
+    }
+    for (i = 0; i < G * G; ++i) {
+        direct = D[i] > direct ? D[i] : direct;
+        if (D[i] > 0) {
+            pr[2 * np] = i / G;
+            pr[2 * np + 1] = i % G;
+            y[(size_t)np * G + i / G] = y[(size_t)np * G + i % G] = D[i] / 2;   /* half straight in each group */
+            ++np;
+        }
+    }
+    if (!np) goto done;
+    for (t = 0; t <= XG_FW_ITERS; ++t) {
+        double m0 = 0, m1 = 0, z0 = 0, z1 = 0, beta;
+        cost = fw_cost(G, np, pr, y, l0, l1);
+        if (best < 0 || cost < best) {
+            best = cost;
+            memcpy(yb, y, sizeof(double) * (size_t)np * G);
+        }
+        if (t == XG_FW_ITERS) break;
+        for (k = 0; k < G * G; ++k) {
+            m0 = l0[k] > m0 ? l0[k] : m0;
+            m1 = l1[k] > m1 ? l1[k] : m1;
+        }
+        beta = XG_FW_SHARP / cost;
+        for (k = 0; k < G * G; ++k) {
+            g0[k] = exp(beta * (l0[k] - m0));
+            g1[k] = exp(beta * (l1[k] - m1));
+            z0 += g0[k];
+            z1 += g1[k];
+        }
+        for (i = 0; i < np; ++i) {
+            const int a = pr[2 * i], bb = pr[2 * i + 1];
+            const double step = 2.0 / (t + 3), dem = D[a * G + bb];
+            int arg = 0;
+            double cmin = 0;
+            for (h = 0; h < G; ++h) {
+                const double c = (h != a ? g0[a * G + h] / z0 : 0.0) + (h != bb ? g1[h * G + bb] / z1 : 0.0);
+                if (h == 0 || c < cmin) { cmin = c; arg = h; }
+            }
+            for (h = 0; h < G; ++h) y[(size_t)i * G + h] += step * ((h == arg ? dem : 0.0) - y[(size_t)i * G + h]);
+        }
+    }
+    /* quantise the best split: 1/1024ths, small shares folded into the pair's largest */
+    memset(w, 0, sizeof(int) * (size_t)G * G * G);
+    for (i = 0; i < np; ++i) {
+        const int a = pr[2 * i], bb = pr[2 * i + 1];
+        int *wp = &w[((size_t)a * G + bb) * G], sum = 0, big = 0;
+        for (h = 0; h < G; ++h) {
+            const int q = (int)(yb[(size_t)i * G + h] / D[a * G + bb] * XG_WEIGHT_ONE + 0.5);
+            wp[h] = q >= 16 ? q : 0;
+            sum += wp[h];
+            if (wp[h] > wp[big]) big = h;
+        }
+        wp[big] += XG_WEIGHT_ONE - sum;
+        for (h = 0; h < G; ++h) yb[(size_t)i * G + h] = D[a * G + bb] * wp[h] / XG_WEIGHT_ONE;
+    }
+    rc = fw_cost(G, np, pr, yb, l0, l1) <= XG_WEIGHTED_GAIN * direct;
+done:
+    free(D); free(pr); free(y); free(yb); free(l0); free(l1); free(g0); free(g1);
+    return rc;
+}
+
 /* the coalesced relay calls of step [b, e) for GPU g: packs into pre, calls into pp, unpacks into
  * post; *sbase / *rbase: the step's STAGE_SEND / STAGE_RECV bytes.  -> 0, or -1 out of host memory */
 static int relay_coalesced_calls(const xg_sched *s, const plan_bases *pb, const int *order, int b, int e, int G,
-                                 int g, cvec *pre, pvec *pp, cvec *post, int64_t *sbase, int64_t *rbase)
+                                 int g, const int *w, cvec *pre, pvec *pp, cvec *post, int64_t *sbase, int64_t *rbase)
 {
     int k, rc = -1;
     int *bk_off = (int *)calloc((size_t)G * G + 1, sizeof(int)), *fill = (int *)calloc((size_t)G * G, sizeof(int));
@@ -503,7 +649,7 @@ static int relay_coalesced_calls(const xg_sched *s, const plan_bases *pb, const 
     }
     memset(&x, 0, sizeof x);
     x.s = s; x.pb = pb; x.G = G; x.g = g; x.bk = bk; x.bk_off = bk_off; x.pm = pm; x.po = po; x.pl = pl;
-    x.blk = blk; x.pre = pre; x.post = post; x.pp = pp;
+    x.blk = blk; x.pre = pre; x.post = post; x.pp = pp; x.w = w;
     x.dry = 1;
     rc_step(&x);                        /* the unpack area's size: the relay area goes behind it */
     x.rlbase = x.ubase;
@@ -533,13 +679,14 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
     oneside *os_out = (oneside *)calloc((size_t)G, sizeof(oneside)), *os_in = (oneside *)calloc((size_t)G, sizeof(oneside));
     int64_t *rl_e = (int64_t *)calloc((size_t)G, sizeof(int64_t)), *rl_i = (int64_t *)calloc((size_t)G, sizeof(int64_t));
     int64_t *rl_p = (int64_t *)calloc((size_t)G * G, sizeof(int64_t));
+    int *rl_w = (int *)calloc((size_t)G * G * G, sizeof(int));       /* a weighted step's shares */
     plan_bases pb;
     memset(&pre, 0, sizeof pre); memset(&post, 0, sizeof post); memset(&pp, 0, sizeof pp);
     memset(&pb, 0, sizeof pb);
     if (form != XG_PACK_TWO_SIDED && form != XG_PACK_ONE_SIDED && form != XG_RELAY && form != XG_RELAY_COALESCED)
         form = XG_PACK_FORM_DEFAULT;
     if (form == XG_RELAY || form == XG_RELAY_COALESCED) pack_max_seg = 0;   /* every other step is direct */
-    if (!dp || !cnt || !order || !pos || !bucket_n || !bucket_b || !os_out || !os_in || !rl_e || !rl_i || !rl_p ||
+    if (!dp || !cnt || !order || !pos || !bucket_n || !bucket_b || !os_out || !os_in || !rl_e || !rl_i || !rl_p || !rl_w ||
         plan_bases_init(&pb, s, G, g) ||
         !(dp->steps = (xg_stepplan *)calloc(nst + 1, sizeof(xg_stepplan)))) {
         oom = 1;
@@ -566,7 +713,7 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
     dp->region_bytes[XG_BUF_RECV] = xg_region_bytes(s, G, g, XG_BUF_RECV);
     dp->region_bytes[XG_BUF_SCRATCH] = xg_region_bytes(s, G, g, XG_BUF_SCRATCH);
     for (st = 0; st < nst; ++st) {
-        int b = cnt[st], e = cnt[st + 1], k, p, relayed;
+        int b = cnt[st], e = cnt[st + 1], k, p, relayed, weighted;
         int64_t sbase = 0, rbase = 0;
         xg_stepplan *sp = &dp->steps[st];
         /* per-peer volume (out: [p], in: [G+p]) for the pack decision */
@@ -598,9 +745,18 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
         sp->p2p_begin = pp.n;
         sp->post_begin = post.n;
         relayed = (form == XG_RELAY || form == XG_RELAY_COALESCED) && relay_step(s, order, b, e, G, rl_e, rl_i, rl_p);
+        weighted = 0;
+        if (!relayed && form == XG_RELAY_COALESCED) {
+            /* a step the uniform cut does not help may still take a weighted two-hop split */
+            const int ws = weighted_step(s, order, b, e, G, rl_w);
+            oom |= ws < 0;
+            weighted = ws > 0;
+        }
         /* coalesced relay: its packs follow the local copies in the pre launch */
-        if (relayed && form == XG_RELAY_COALESCED)
-            oom |= relay_coalesced_calls(s, &pb, order, b, e, G, g, &pre, &pp, &post, &sbase, &rbase) != 0;
+        if ((relayed || weighted) && form == XG_RELAY_COALESCED)
+            oom |= relay_coalesced_calls(s, &pb, order, b, e, G, g, weighted ? rl_w : NULL, &pre, &pp, &post, &sbase,
+                                         &rbase) != 0;
+        relayed |= weighted;
         /* the one-sided layout of every packed list of this GPU's, both directions */
         if (form == XG_PACK_ONE_SIDED)
             for (p = 0; p < G; ++p) {
@@ -780,7 +936,7 @@ xg_devplan *xg_devplan_build_form(const xg_sched *s, int ngpus, int g, int64_t p
     oom |= !dp->copies || !dp->p2p;
 done:
     free(pre.v); free(post.v); free(pp.v); free(cnt); free(order); free(pos); free(bucket_n); free(bucket_b);
-    free(os_out); free(os_in); free(rl_e); free(rl_i); free(rl_p);
+    free(os_out); free(os_in); free(rl_e); free(rl_i); free(rl_p); free(rl_w);
     plan_bases_free(&pb);
     if (oom) {
         xg_devplan_free(dp);

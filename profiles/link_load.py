@@ -3,7 +3,7 @@
 
 For every method of configs[2] (P64 A16 -d 256 KiB), configs[3] (P256 A32 -d 4 MiB) and configs[4]
 (P256 A64 -d 64 MiB, -c 1..8) at G = 8, and every cross-GPU form (direct, packed one-sided,
-packed two-sided, relay), the calls each GPU posts (xg_devplan_step_calls: what enqueue_step hands
+packed two-sided, relay, coalesced relay), the calls each GPU posts (xg_devplan_step_calls: what enqueue_step hands
 RCCL) are summed per directed GPU link, per step and per RCCL group of the step:
 
   busiest   = sum over steps and groups of the most loaded link's bytes (one direction)
@@ -27,7 +27,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 L_GBPS = 50.0
-FORMS = (("direct", 0, -1), ("one-sided", 4 << 20, 1), ("two-sided", 4 << 20, 0), ("relay", 0, 2))
+FORMS = (("direct", 0, -1), ("one-sided", 4 << 20, 1), ("two-sided", 4 << 20, 0), ("relay", 0, 2),
+         ("coalesced", 0, 3))
 CONFIGS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
             ("configs[3]", 256, 32, 4 << 20, 200000000, (1, 2, 9, 10))] +
            [("configs[4] -c %d" % c, 256, 64, 64 << 20, c, (7, 11, 12)) for c in range(1, 9)])

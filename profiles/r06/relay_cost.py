@@ -63,50 +63,55 @@ def calls_per_step(s, form):
     return sum(n) / max(1, sum(1 for x in n if x)), v.nsteps
 
 
-def relay_vs_direct(reps=3):
-    P, A, it = 256, 32, 1
-    rl = xg.aggregator_list(P, A)
+CASES = [(256, 32, d, 200000000, m) for d in (1 << 20, 4 << 20) for m in (9, 10)]
+# CASES=m7: configs[4]'s m7 (P256 A64) at -d 1 / 8 MiB, which only the coalesced form's weighted
+# two-hop split reroutes
+M7_CASES = [(256, 64, d, 1, 7) for d in (1 << 20, 8 << 20)]
+
+
+def relay_vs_direct(reps=3, cases=CASES):
+    it = 1
     ctxs = [xg.Context.virtual(g, 8, device=0) for g in range(8)]
     out = []
     try:
-        for d in (1 << 20, 4 << 20):
-            for m in (9, 10):
-                s = xg.Schedule(m, P, A, d, 200000000, rl, ntimes=1, iteration=it)
-                forms = {"direct": (0, -1), "relay": (0, 2), "coalesced": (0, 3)}
-                need = [[0] * xg.NBUF for _ in range(8)]
-                for f in forms.values():
-                    for g in range(8):
-                        need[g] = [max(a, b) for a, b in zip(need[g], s.devplan(8, g, f[0], 0, f[1]).region_bytes)]
-                regs = [xg.Regions(c, n) for c, n in zip(ctxs, need)]
-                try:
-                    row = {"what": "virtual8_rccl", "P": P, "A": A, "d": d, "method": m}
-                    for name, f in forms.items():
-                        runs = [xg.MethodRun(c, s, it=it, mode=1, pack_max_seg=f[0], pack_form=f[1], regions=regs[g])
-                                for g, c in enumerate(ctxs)]
-                        try:
-                            xg.run_virtual(runs, rccl=True)          # warm-up (connection set-up)
-                            ts = []
-                            for _ in range(reps):
-                                t0 = time.perf_counter()
-                                done = xg.run_virtual(runs, rccl=True)
-                                ts.append((done[-1], time.perf_counter() - t0))
-                            bad = sum(sum(1 for b in r.verify()[1] if b) for r in runs)
-                        finally:
-                            for r in runs:
-                                r.close()
-                        cps, nst = calls_per_step(s, f)
-                        row[name] = {"device_ms_median": round(statistics.median(t for t, _ in ts) * 1e3, 3),
-                                     "device_ms_min": round(min(t for t, _ in ts) * 1e3, 3),
-                                     "device_ms_max": round(max(t for t, _ in ts) * 1e3, 3),
-                                     "host_ms_median": round(statistics.median(w for _, w in ts) * 1e3, 3),
-                                     "gpu0_cross_calls_per_busy_step": round(cps, 2), "steps": nst, "bad_slots": bad}
-                    for f in ("relay", "coalesced"):
-                        row[f + "_over_direct"] = round(row[f]["device_ms_median"] / row["direct"]["device_ms_median"], 3)
-                    out.append(row)
-                    print(json.dumps(row), flush=True)
-                finally:
-                    for r in regs:
-                        r.close()
+        for P, A, d, comm, m in cases:
+            rl = xg.aggregator_list(P, A)
+            s = xg.Schedule(m, P, A, d, comm, rl, ntimes=1, iteration=it)
+            forms = {"direct": (0, -1), "relay": (0, 2), "coalesced": (0, 3)}
+            need = [[0] * xg.NBUF for _ in range(8)]
+            for f in forms.values():
+                for g in range(8):
+                    need[g] = [max(a, b) for a, b in zip(need[g], s.devplan(8, g, f[0], 0, f[1]).region_bytes)]
+            regs = [xg.Regions(c, n) for c, n in zip(ctxs, need)]
+            try:
+                row = {"what": "virtual8_rccl", "P": P, "A": A, "d": d, "c": comm, "method": m}
+                for name, f in forms.items():
+                    runs = [xg.MethodRun(c, s, it=it, mode=1, pack_max_seg=f[0], pack_form=f[1], regions=regs[g])
+                            for g, c in enumerate(ctxs)]
+                    try:
+                        xg.run_virtual(runs, rccl=True)          # warm-up (connection set-up)
+                        ts = []
+                        for _ in range(reps):
+                            t0 = time.perf_counter()
+                            done = xg.run_virtual(runs, rccl=True)
+                            ts.append((done[-1], time.perf_counter() - t0))
+                        bad = sum(sum(1 for b in r.verify()[1] if b) for r in runs)
+                    finally:
+                        for r in runs:
+                            r.close()
+                    cps, nst = calls_per_step(s, f)
+                    row[name] = {"device_ms_median": round(statistics.median(t for t, _ in ts) * 1e3, 3),
+                                 "device_ms_min": round(min(t for t, _ in ts) * 1e3, 3),
+                                 "device_ms_max": round(max(t for t, _ in ts) * 1e3, 3),
+                                 "host_ms_median": round(statistics.median(w for _, w in ts) * 1e3, 3),
+                                 "gpu0_cross_calls_per_busy_step": round(cps, 2), "steps": nst, "bad_slots": bad}
+                for f in ("relay", "coalesced"):
+                    row[f + "_over_direct"] = round(row[f]["device_ms_median"] / row["direct"]["device_ms_median"], 3)
+                out.append(row)
+                print(json.dumps(row), flush=True)
+            finally:
+                for r in regs:
+                    r.close()
     finally:
         for c in ctxs:
             c.close()
@@ -116,5 +121,5 @@ def relay_vs_direct(reps=3):
 if __name__ == "__main__":
     if os.environ.get("SPLIT", "1") == "1":
         split_costs()
-    relay_vs_direct()
+    relay_vs_direct(cases=M7_CASES if os.environ.get("CASES") == "m7" else CASES)
     print("relay_cost ok", flush=True)

@@ -170,14 +170,17 @@ def test_relay_form_config4_as_eight_rank_job(tmp_path, c):
     the relay form rewrites (252 of 256 and 256 of 256 at the stated size, profiles/r05/link_load.txt),
     and m7, which it leaves direct.  The N = 8 BASELINE phase times exactly these plans; every slot
     is byte-checked on the device and sampled slots equal the oracle's closed form.
-    The coalesced relay form (XG_RELAY_COALESCED) runs the same relayed steps.
+    The coalesced relay form (XG_RELAY_COALESCED) runs the same relayed steps, and m7's steps in its
+    weighted two-hop split.
     Reference: many_to_all_half_sync / all_to_many_half_sync2 (mpi_test.c:942-997, :999-1053)."""
     cases = [{"shape": [256, 64, 1 << 20, c], "methods": [11, 12, 7], "forms": [DIRECT, RELAY, COALESCED]}]
     rows = _job(tmp_path, 8, cases, timeout=140)
     _assert_exact(rows, 9)
     for form in (RELAY, COALESCED):
         relayed = {r["method"]: r["relayed_steps"] for r in rows if r["form"] == form}
-        assert relayed[11] > 0 and relayed[12] > 0 and relayed[7] == 0, (form, relayed)
+        assert relayed[11] > 0 and relayed[12] > 0, (form, relayed)
+        # m7: no uniform cut helps; the coalesced form's weighted two-hop split reroutes its steps
+        assert (relayed[7] > 0) == (form == COALESCED), (form, relayed)
     assert all(r["relayed_steps"] == 0 for r in rows if r["form"] == DIRECT)
 
 
