@@ -1201,11 +1201,12 @@ def main():
         s = xg.Schedule(m, a.procs, a.aggs, a.size, a.comm_size, rl, ntimes=1)
         cands = list(base)
         if tune_on and world >= 3:
-            # the relay forms only where they change some GPU's plan (MAX over the GPUs: all agree;
-            # both reroute the same steps)
-            v0, vr = s.devplan(world, rank, 0, 0, -1), s.devplan(world, rank, 0, 0, xg.RELAY)
-            if ctx.allreduce_max([1.0 if (vr.copies, vr.p2p) != (v0.copies, v0.p2p) else 0.0])[0]:
-                cands.extend(relays)
+            # a relay form only where it changes some GPU's plan (MAX over the GPUs: all agree; the
+            # coalesced form also reroutes steps the uniform cut does not help, by a weighted split)
+            v0 = s.devplan(world, rank, 0, 0, -1)
+            vs = [s.devplan(world, rank, pk, 0, form) for pk, form in relays]
+            dif = ctx.allreduce_max([1.0 if (v.copies, v.p2p) != (v0.copies, v0.p2p) else 0.0 for v in vs])
+            cands.extend(f for f, d in zip(relays, dif) if d)
         passed, samples, why = {}, {}, {}
         for pk, form in cands:
             fname = names.get((pk, form), "plan")
