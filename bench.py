@@ -652,8 +652,10 @@ BASELINE_CELLS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
 # others only where they change the plan
 CELL_FORMS = (("direct", (0, -1)), ("packed_one_sided", (4 << 20, 1)), ("packed_two_sided", (4 << 20, 0)),
               ("relay", (0, 2)), ("relay_coalesced", (0, 3)))
-# forms left out of a configuration whose regions cannot hold their staging as well (the others run)
-CELL_HEAVY = ("relay_coalesced",)
+# region tiers of a configuration, largest first: when its regions cannot hold every form's staging
+# the forms of the next tier run (on every GPU alike), down to direct alone (no staging at all)
+CELL_TIERS = (tuple(f for f, _ in CELL_FORMS), tuple(f for f, _ in CELL_FORMS if f != "relay_coalesced"),
+              ("direct",))
 
 
 def cell_estimate_s(links, link_gbps):
@@ -683,7 +685,7 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
     t0 = time.time()
     result["cells"] = cells_out = {}
     regions = {}                      # (P, A, d) -> Regions shared by that configuration's cells
-    lean_rk = set()                   # (P, A, d) whose regions hold every form but CELL_HEAVY's
+    tier_of = {}                      # (P, A, d) -> the CELL_TIERS index its regions hold
     no_room = set()                   # (P, A, d) whose regions could not be allocated on some GPU
     needs = {}                        # (P, A, d, c) -> region bytes of every method and form on this GPU
 
@@ -757,50 +759,51 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                         v = s.devplan(world, rank, f[0], 0, f[1])
                         differs[i] = 1.0 if (v.copies, v.p2p) != (v0.copies, v0.p2p) else 0.0
                     if (P, A, d, c) not in needs:   # one allocation per configuration: all its methods, all forms
-                        need, lean = [0] * xg.NBUF, [0] * xg.NBUF
+                        tiers = [[0] * xg.NBUF for _ in CELL_TIERS]
                         for mm in methods:
                             sm = xg.Schedule(mm, P, A, d, c, rl, ntimes=1)
                             for fname, f in CELL_FORMS:
                                 v = sm.devplan(world, rank, f[0], 0, f[1])
-                                need = [max(x, y) for x, y in zip(need, v.region_bytes)]
-                                if fname not in CELL_HEAVY:
-                                    lean = [max(x, y) for x, y in zip(lean, v.region_bytes)]
-                        needs[(P, A, d, c)] = (need, lean)
-                    need, lean = needs[(P, A, d, c)]
+                                for k, names in enumerate(CELL_TIERS):
+                                    if fname in names:
+                                        tiers[k] = [max(x, y) for x, y in zip(tiers[k], v.region_bytes)]
+                        needs[(P, A, d, c)] = tiers
+                    tiers = needs[(P, A, d, c)]
                     rk = (P, A, d)
-                    if rk not in regions or not regions[rk].fits(lean if rk in lean_rk else need):
+                    if rk not in regions or not regions[rk].fits(tiers[tier_of[rk]]):
                         # a new configuration, or one whose -c needs more staging than the cells
                         # before it (configs[4] at -d 4 KiB: -c 8 after -c 1): regions sized for both
                         if rk in regions:
-                            need = [max(x, y) for x, y in zip(need, regions[rk].bytes)]
-                            lean = [max(x, y) for x, y in zip(lean, regions[rk].bytes)]
+                            tiers = [[max(x, y) for x, y in zip(tb, regions[rk].bytes)] for tb in tiers]
                         for old in regions.values():
                             old.close()
                         regions.clear()
-                        lean_rk.discard(rk)
+                        tier_of.pop(rk, None)
                         no_alloc = True
-                        try:
-                            regions[rk] = xg.Regions(ctx, need)
-                        except xg.XGError:
+                        for k, tb in enumerate(tiers):
                             # the coalesced relay form's staging (up to 5.5 GiB beside configs[4]'s
-                            # 256 GiB, tests/test_hbm_fit.py) did not fit: the other forms' regions
-                            regions[rk] = xg.Regions(ctx, lean)
-                            lean_rk.add(rk)
+                            # 256 GiB, tests/test_hbm_fit.py), then the other forms', may not fit
+                            try:
+                                regions[rk] = xg.Regions(ctx, tb)
+                                tier_of[rk] = k
+                                break
+                            except xg.XGError:
+                                if k == len(tiers) - 1:
+                                    raise
                         no_alloc = False
                 except xg.XGError as e:
                     err = str(e)
-                failed, unplaced, is_lean, *differs = ctx.allreduce_max(
-                    [1.0 if err else 0.0, 1.0 if no_alloc else 0.0, 1.0 if (P, A, d) in lean_rk else 0.0] + differs)
+                failed, unplaced, tier, *differs = ctx.allreduce_max(
+                    [1.0 if err else 0.0, 1.0 if no_alloc else 0.0, float(tier_of.get((P, A, d), 0))] + differs)
                 if failed:
                     cells_out[key] = "failed: %s" % (err or "on another GPU")
                     if unplaced:      # some GPU never got this configuration's regions: the rest would fail alike
                         no_room.add((P, A, d))
                     continue
+                held = CELL_TIERS[int(tier)]
                 forms = dict(CELL_FORMS[:1])
-                forms.update((fname, f) for (fname, f), dif in zip(CELL_FORMS[1:], differs)
-                             if dif and not (is_lean and fname in CELL_HEAVY))
-                dropped = [fname for (fname, _f), dif in zip(CELL_FORMS[1:], differs)
-                           if dif and is_lean and fname in CELL_HEAVY]
+                forms.update((fname, f) for (fname, f), dif in zip(CELL_FORMS[1:], differs) if dif and fname in held)
+                dropped = [fname for (fname, _f), dif in zip(CELL_FORMS[1:], differs) if dif and fname not in held]
                 # the cell's runs at the measured link rate: a cell that would still be running when the
                 # phase's guard fires is skipped on every GPU alike (the cells after it may be shorter)
                 links = {f: link_bytes(xg, s, world, form[0], form[1]) if rank == 0 else (0, 0)

@@ -538,32 +538,36 @@ def test_cell_estimate_from_the_link_rate():
     assert bench.cell_estimate_s(links, None) == 0.0
 
 
-def test_bench_baseline_configs_drop_the_coalesced_staging_when_it_does_not_fit(tmp_path, xg):
-    """GPU 1 of a 4-GPU job can hold configs[3]'s full-size regions with the relay form's staging but
-    not with the coalesced relay form's as well (injected limit between the two): the pairwise cells
-    run every other form, on every GPU alike, and say which form was left out and why"""
+@pytest.mark.parametrize("tier", [1, 2])
+def test_bench_baseline_configs_drop_the_staging_that_does_not_fit(tmp_path, xg, tier):
+    """GPU 1 of a 4-GPU job can hold configs[3]'s full-size regions with the staging of tier `tier`'s
+    forms but not of the tier above (injected limit between the two; tier 1: every form but the
+    coalesced relay form, tier 2: direct alone): the pairwise cells run the forms that fit, on every
+    GPU alike, and say which forms were left out and why"""
     import bench
     P, A, d, c = 256, 32, 4 << 20, 200000000
     rl = xg.aggregator_list(P, A)
-    need, lean = [0] * xg.NBUF, [0] * xg.NBUF
+    sums = [[0] * xg.NBUF for _ in bench.CELL_TIERS]
     for m in (1, 2, 9, 10):
         s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
         for fname, f in bench.CELL_FORMS:
             rb = s.devplan(4, 1, f[0], 0, f[1]).region_bytes
-            need = [max(x, y) for x, y in zip(need, rb)]
-            if fname not in bench.CELL_HEAVY:
-                lean = [max(x, y) for x, y in zip(lean, rb)]
-    assert sum(lean) < sum(need)
+            for k, names in enumerate(bench.CELL_TIERS):
+                if fname in names:
+                    sums[k] = [max(x, y) for x, y in zip(sums[k], rb)]
+    lo, hi = sum(sums[tier]), sum(sums[tier - 1])
+    assert lo < hi
     argv = ["--gpus", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--methods", "1",
             "--baseline-configs", "on", "--no-ktime"]
-    rcs, outs = _run_job(4, argv, tmp_path, {"XG_FAKE_REGIONS_FAIL": "%d:1" % ((sum(lean) + sum(need)) // 2)})
+    rcs, outs = _run_job(4, argv, tmp_path, {"XG_FAKE_REGIONS_FAIL": "%d:1" % ((lo + hi) // 2)})
     assert rcs == [0] * 4, [o[1][-1500:] for o in outs]
     cells = _line(outs)["baseline_configs_8gpu"]["cells"]
     for m in (9, 10):
         cell = cells["configs[3] m%d" % m]
         assert isinstance(cell, dict) and cell["verified"], cell
-        assert "relay" in cell["forms"] and "relay_coalesced" not in cell["forms"], cell
-        assert set(cell["forms_not_run"]) == {"relay_coalesced"}, cell
+        ran = set(cell.get("forms", {"direct": 0}))
+        assert ran == {"direct", "relay", "relay_coalesced"} & set(bench.CELL_TIERS[tier]), cell
+        assert set(cell["forms_not_run"]) == {"relay", "relay_coalesced"} - ran, cell
     # the reduced -d configuration's regions fit whole (nothing relayed there: no relay form at all)
     assert "forms_not_run" not in cells["configs[3] at -d 4 KiB m9"]
 
