@@ -330,3 +330,22 @@ def test_weighted_split_matches_the_python_frank_wolfe(xg):
             got = _groups_busiest(coal, st) / 2 ** 20
             assert got <= 1.05 * lp.fw_two_hop(D), (m, st, got)
         assert seen
+
+
+@pytest.mark.parametrize("P, A, G, methods", [(32, 16, 3, (7, 9, 12)), (24, 6, 4, (1, 2, 12)), (32, 8, 8, (7,)),
+                                              (16, 8, 3, (5, 8, 15, 16))])
+def test_weighted_split_delivers_every_byte(xg, P, A, G, methods):
+    """steps the coalesced form splits by weight (the uneven block maps of 3 / 4 GPUs, m7's matrices,
+    m5 / m8's alltoallw, TAM m15 / m16's aggregation) at -d (1 << 20) + 3: every byte where the
+    reference puts it, no launch races, RCCL pairs every call; every such step has a second group"""
+    d = (1 << 20) + 3
+    rl = xg.aggregator_list(P, A)
+    for m in methods:
+        s = xg.Schedule(m, P, A, d, 3, rl, ntimes=1, iteration=1)
+        relay = s.devplan(G, 0, RELAY[0], 0, RELAY[1])
+        coal = s.devplan(G, 0, COALESCED[0], 0, COALESCED[1])
+        fences = lambda v: sum(1 for st in range(v.nsteps) if FENCE in [x[0] for x in v.calls(st)])
+        assert fences(coal) > fences(relay), (P, A, G, m)      # some step is weighted, not uniform
+        assert s.check_pairing(G, COALESCED[0], 0, COALESCED[1]) > 0
+        _views, regs = simulate(s, G, it=1, mode=1, pack=COALESCED[0], form=COALESCED[1])
+        check_recv(s, G, regs, it=1, mode=1)
