@@ -507,7 +507,7 @@ static void rc_step(rcx *x)
  * ((max egress + max ingress) / G is not below its busiest pair), yet a non-uniform one exists: the
  * best two-hop routing in two groups carries 0.78 of the direct form's busiest-link bytes
  * (profiles/r05/relay_lp.txt, an LP).  Per step, Frank-Wolfe on a soft-max of the busiest group-0
- * and group-1 links (profiles/relay_lp.py's fw_two_hop, here in C): every pair's bytes split over
+ * and group-1 links (profiles/relay_lp.py's fw_two_hop, here in C, 1000 iterations): every pair's bytes split over
  * its G paths -- straight in group 0 (h = b), straight in group 1 (h = a), via relay h -- starting
  * half straight in each group; each iteration moves 2 / (t + 3) of every pair onto its cheapest
  * path under the current gradient.  The best split seen is rounded to 1/1024ths (shares under
@@ -515,8 +515,8 @@ static void rc_step(rcx *x)
  * when its quantised link time is at
  * most XG_WEIGHTED_GAIN of the busiest pair's and every cross message is >= XG_RELAY_MIN_BYTES.
  * Deterministic: every GPU computes it from the same message list with the same code. */
-#define XG_FW_ITERS 300
-#define XG_FW_SHARP 40.0
+#define XG_FW_ITERS 1000
+#define XG_FW_SHARP 80.0
 #define XG_WEIGHTED_GAIN 0.85
 
 /* group-0 / group-1 link loads of split y (pairs pr[np][2], y[np][G] bytes) -> max l0 + max l1 */

@@ -275,8 +275,8 @@ def test_weighted_split_of_configs4_m7(xg, c):
     """configs[4]'s m7 (P256 A64, here -d 8 MiB) on 8 GPUs: no step is a permutation, so the uniform
     cut gains nothing (the relay form leaves it direct), but the coalesced form's weighted two-hop
     split (devplan.c weighted_step, Frank-Wolfe) reroutes all 64 of its cross-GPU steps: each weighted
-    step's busiest group-0 + group-1 links carry <= 0.85 of its busiest pair's bytes, the run 0.83 of
-    the direct form's (4096 -> 3362 MiB; the LP optimum of two-hop routing is 0.78,
+    step's busiest group-0 + group-1 links carry <= 0.85 of its busiest pair's bytes, the run 0.81 of
+    the direct form's (4096 -> 3302 MiB; the LP optimum of two-hop routing is 0.78,
     profiles/r05/relay_lp.txt); RCCL pairs every call, and no more calls than direct"""
     P, A, d, G = 256, 64, 8 << 20, 8
     s = xg.Schedule(7, P, A, d, c, xg.aggregator_list(P, A), ntimes=1)
@@ -295,7 +295,7 @@ def test_weighted_split_of_configs4_m7(xg, c):
             assert bc == bd
         tot_d += bd
         tot_c += bc
-    assert weighted == 64 and tot_d == 4096 << 20 and tot_c <= 0.83 * tot_d, (weighted, tot_d >> 20, tot_c >> 20)
+    assert weighted == 64 and tot_d == 4096 << 20 and tot_c <= 0.81 * tot_d, (weighted, tot_d >> 20, tot_c >> 20)
     for g in range(G):
         n = lambda v: sum(1 for st in range(v.nsteps) for x in v.calls(st) if x[0] in (SEND, RECV))
         assert n(coal[g]) <= n(direct[g])
