@@ -175,8 +175,8 @@ def test_config4_d8m_virtual8(xg, world8):
     pairing), and through RCCL itself at -c 1 and -c 8; regions allocated once per GPU.  m11 / m12
     also in the relay form (XG_RELAY) and the coalesced relay form (XG_RELAY_COALESCED), the forms
     the N = 8 BASELINE phase times beside direct on exactly these plans (profiles/r05/link_load.txt):
-    every -c through copies, -c 1 and 8 through RCCL.  m7, which no uniform cut helps, runs in the
-    coalesced form's weighted two-hop split (every step).  m7's plan is the same in both forms (no step gains), so it runs direct only."""
+    every -c through copies (the coalesced form at -c 1 and 8), -c 1 and 8 through RCCL.  m7, which
+    no uniform cut helps, runs in the coalesced form's weighted two-hop split (every step).  m7's plan is the same in both forms (no step gains), so it runs direct only."""
     P, A, d, it = 256, 64, 8 << 20, 1
     rl = xg.aggregator_list(P, A)
     scheds = {(m, c): xg.Schedule(m, P, A, d, c, rl, ntimes=1, iteration=it) for m in (7, 11, 12)
@@ -186,7 +186,8 @@ def test_config4_d8m_virtual8(xg, world8):
     regions = _shared_regions(xg, world8, list(scheds.values()), (pack, relay, coal))
     try:
         for (m, c), s in scheds.items():
-            forms = [pack] + ([relay, coal] if m != 7 else [coal])
+            # the coalesced form at the -c the N = 8 bench reaches first (the suite's time: 1 and 8)
+            forms = [pack] + ([relay] if m != 7 else []) + ([coal] if c in (1, 8) else [])
             # the relay forms must reroute these plans, or this test checks nothing new: m11 / m12
             # in both (the same steps), m7 only in the coalesced form's weighted two-hop split
             assert _relayed_steps(xg, s, 8, pack) == 0, (m, c)
