@@ -279,11 +279,15 @@ def host_cpus():
 
 
 def reference_cpus():
-    """CPUs to pin the reference's MPI processes to: with a cgroup CPU quota below the affinity mask
-    (a one-GPU box: 16 CPUs of quota spread over 256 in the mask) the first `quota` CPUs of the mask,
-    else None (no pinning).  Busy-polling MPICH ranks spread over the whole mask burn the quota in
-    parallel and are then throttled for the rest of every period together, so a message waits for
-    the next period; pinned, they time-slice on as many CPUs as they are paid for."""
+    """CPUs to pin the reference's MPI processes to: None (no pinning) unless XG_REF_PIN=1, which pins
+    them to the first `quota` CPUs of the mask when a cgroup CPU quota sits below the affinity mask (a
+    one-GPU box: 16 CPUs of quota over 256 in the mask).  Measured on those boxes, pinning makes the
+    reference 5-10x SLOWER at configs[1] (32 busy-polling ranks time-slicing 16 CPUs: 3.1-3.8 s per
+    method, 1.3-1.5 GB/s, profiles/r06/torchrun8*/ against 0.2-0.6 s, 9.2-12.6 GB/s unpinned,
+    BENCH_r05.json, profiles/r05/torchrun8_shared_gpu_c/) and no faster at the P256 cells: the
+    baseline is the reference at its best, so it runs unpinned, throttled by the quota alone."""
+    if os.environ.get("XG_REF_PIN") != "1":
+        return None
     n, _how = host_cpus()
     if not hasattr(os, "sched_getaffinity"):
         return None
