@@ -278,19 +278,25 @@ def host_cpus():
     return n, how
 
 
-def reference_cpus():
-    """CPUs to pin the reference's MPI processes to: None (no pinning) unless XG_REF_PIN=1, which pins
-    them to the first `quota` CPUs of the mask when a cgroup CPU quota sits below the affinity mask (a
-    one-GPU box: 16 CPUs of quota over 256 in the mask).  Measured on those boxes, pinning makes the
-    reference 5-10x SLOWER at configs[1] (32 busy-polling ranks time-slicing 16 CPUs: 3.1-3.8 s per
-    method, 1.3-1.5 GB/s, profiles/r06/torchrun8*/ against 0.2-0.6 s, 9.2-12.6 GB/s unpinned,
-    BENCH_r05.json, profiles/r05/torchrun8_shared_gpu_c/) and no faster at the P256 cells: the
-    baseline is the reference at its best, so it runs unpinned, throttled by the quota alone."""
-    if os.environ.get("XG_REF_PIN") != "1":
+def reference_cpus(pin):
+    """CPUs to pin the reference's MPI processes to, or None (not pinned).  pin: the first `quota` CPUs
+    of the mask when a cgroup CPU quota sits below the affinity mask (a one-GPU box: 16 CPUs of quota
+    over 256 in the mask).  Measured on those boxes, the two settings suit different runs:
+      * configs[1]'s 32 ranks (cpu_baseline) run 5-10x FASTER unpinned -- 0.2-0.6 s per method
+        (9.2-18 GB/s, BENCH_r05.json, profiles/r06/unpinned/) against 3.1-3.8 s pinned (1.3-1.5 GB/s,
+        profiles/r06/torchrun8*/): 32 busy-polling ranks time-slicing 16 CPUs wait out each other's
+        slices, while unpinned they run together until the quota throttles them;
+      * the 256-rank BASELINE cells (cpu_baseline_configs) take 48-61 s of wall each unpinned, almost
+        all of it MPI start-up under the quota, against 2-16 s pinned, for max total times within
+        +-30 % of each other (profiles/r06/torchrun8d/ against torchrun8c/): pinned, every 8-GPU
+        method gets its cell inside the budget.
+    XG_REF_PIN=1 / 0 forces either for both."""
+    env = os.environ.get("XG_REF_PIN")
+    if env in ("0", "1"):
+        pin = env == "1"
+    if not pin or not hasattr(os, "sched_getaffinity"):
         return None
     n, _how = host_cpus()
-    if not hasattr(os, "sched_getaffinity"):
-        return None
     mask = sorted(os.sched_getaffinity(0))
     return mask[:n] if n < len(mask) else None
 
@@ -339,7 +345,7 @@ def cpu_baseline(a, methods):
     if not os.path.exists(os.path.join(REPO, "oracle", "_ref", "test")):
         return cpu_baseline_port(a, methods)
     tot_bytes, tot_time, per = 0.0, 0.0, {}
-    cpus = reference_cpus()
+    cpus = reference_cpus(pin=False)      # configs[1]: faster unpinned
     t0 = time.time()
     for m in methods:
         args = ["-n", str(a.procs), "-a", str(a.aggs), "-p", "1", "-d", str(a.size), "-m", str(m), "-i", "1",
@@ -408,7 +414,7 @@ def cpu_baseline_configs(a, cells=CPU_CELLS):
     that would start past it, or runs past it, is recorded as skipped.  Run before any process
     touches a GPU (the parent of an N-GPU job, or rank 0 under a launcher)."""
     ncpu, how = host_cpus()
-    cpus = reference_cpus()
+    cpus = reference_cpus(pin=True)       # 256 ranks: start-up fits the budget pinned
     cap = cell_cap(a)
     t0 = time.time()
     res = {"budget_s": a.cpu_configs_budget, "cell_cap_s": cap, "cores": ncpu, "cores_how": how,

@@ -582,3 +582,18 @@ def test_heartbeat_names_the_phase(capfd):
     stop.set()
     err = capfd.readouterr().err
     assert err.count("bench: cpu baseline at the BASELINE 8-GPU configurations (") >= 2, err
+
+
+def test_reference_pinning_per_run(monkeypatch):
+    """the reference's configs[1] baseline runs unpinned, its 256-rank BASELINE cells pinned to the
+    quota's CPUs (when a quota sits below the mask); XG_REF_PIN=0 / 1 forces either"""
+    import bench
+    monkeypatch.setattr(bench, "host_cpus", lambda: (2, "test quota"))
+    monkeypatch.delenv("XG_REF_PIN", raising=False)
+    mask = sorted(os.sched_getaffinity(0))
+    assert bench.reference_cpus(pin=False) is None
+    assert bench.reference_cpus(pin=True) == (mask[:2] if len(mask) > 2 else None)
+    monkeypatch.setenv("XG_REF_PIN", "0")
+    assert bench.reference_cpus(pin=True) is None
+    monkeypatch.setenv("XG_REF_PIN", "1")
+    assert bench.reference_cpus(pin=False) == (mask[:2] if len(mask) > 2 else None)
