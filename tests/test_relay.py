@@ -349,3 +349,36 @@ def test_weighted_split_delivers_every_byte(xg, P, A, G, methods):
         assert s.check_pairing(G, COALESCED[0], 0, COALESCED[1]) > 0
         _views, regs = simulate(s, G, it=1, mode=1, pack=COALESCED[0], form=COALESCED[1])
         check_recv(s, G, regs, it=1, mode=1)
+
+
+def _random_shapes(seed, n):
+    import random
+    rnd = random.Random(seed)
+    out = []
+    while len(out) < n:
+        P = rnd.randint(6, 40)
+        A = rnd.randint(1, min(P, 16))
+        G = rnd.randint(3, min(8, P))
+        d = rnd.choice([1 << 20, (1 << 20) + 3, (1 << 20) + 48, (2 << 20) + 5])
+        c = rnd.choice([1, 2, 3, 8, 200000000])
+        m = rnd.randint(1, 20)
+        out.append((P, A, G, d, c, m))
+    return out
+
+
+@pytest.mark.parametrize("P, A, G, d, c, m", _random_shapes(2026, 40))
+def test_relay_forms_random_shapes(xg, P, A, G, d, c, m):
+    """random shapes (P 6-40, A 1-16, G 3-8, -d 1-2 MiB aligned and not, -c 1-8 / default, methods
+    1-20): both relay forms (uniform cuts, coalesced calls, weighted splits) deliver every byte
+    where the reference puts it, race-free, and RCCL pairs every call; a schedule MPI itself would
+    deadlock on (m6 at some -c) is refused alike in every form"""
+    rl = xg.aggregator_list(P, A)
+    try:
+        s = xg.Schedule(m, P, A, d, c, rl, ntimes=1, iteration=1)
+    except xg.XGError as e:
+        assert "deadlock" in str(e).lower() or "hang" in str(e).lower(), str(e)
+        return
+    for form in (RELAY, COALESCED):
+        assert s.check_pairing(G, form[0], 0, form[1]) >= 0
+        _views, regs = simulate(s, G, it=1, mode=1, pack=form[0], form=form[1])
+        check_recv(s, G, regs, it=1, mode=1)
