@@ -76,20 +76,20 @@ def parse():
     ap.add_argument("--baseline-budget", type=float, default=130.0,
                     help="seconds the BASELINE-configs phase may take; cells past it are skipped (all ranks "
                          "alike), and a phase still running GUARD_GRACE s later prints the line without the rest")
-    ap.add_argument("--xgmi-budget", type=float, default=25.0,
+    ap.add_argument("--xgmi-budget", type=float, default=20.0,
                     help="N > 1: seconds the xGMI ceiling + sweep phase may take before the line is printed "
                          "without the rest of it")
-    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 130)),
+    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("XG_BENCH_WATCHDOG", 110)),
                     help="rank process: seconds from the communicator init to the measured value before a rank "
                          "that is still running reports the phase it is stuck in and exits 124 (0: off) -- a lost "
                          "peer leaves RCCL waiting forever; the phases after the value have guards of their own")
-    ap.add_argument("--cpu-budget", type=float, default=40.0,
+    ap.add_argument("--cpu-budget", type=float, default=30.0,
                     help="seconds the reference's configs[1] run under mpiexec may take in all")
     ap.add_argument("--cpu-configs", choices=("auto", "on", "off"), default="auto",
                     help="run the reference under mpiexec at BASELINE.json's 8-GPU configurations (configs[2] at "
                          "full size, configs[3] and [4] at -d 4 KiB) before the GPUs start (auto: when the job "
                          "has 8 GPUs)")
-    ap.add_argument("--cpu-configs-budget", type=float, default=205.0,
+    ap.add_argument("--cpu-configs-budget", type=float, default=240.0,
                     help="seconds those reference cells may take in all; a cell past it is recorded as skipped")
     return ap.parse_args()
 

@@ -374,7 +374,7 @@ def test_wall_bound_of_the_driver_runs():
     import bench
     sys.argv = ["bench.py"]
     a = bench.parse()
-    assert bench.wall_bound(a, 1) == a.watchdog == 130
+    assert bench.wall_bound(a, 1) == a.watchdog == 110
     b8 = bench.wall_bound(a, 8)
     assert b8 == a.cpu_budget + a.cpu_configs_budget + bench.CPU_GRACE + a.watchdog + a.xgmi_budget + \
         a.baseline_budget + bench.GUARD_GRACE
