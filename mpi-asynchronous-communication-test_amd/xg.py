@@ -438,7 +438,8 @@ class DevicePlanView:
 
     def __init__(self, sched, ngpus, g, pack_max_seg, pack_min=0, pack_form=-1):
         self.sched = sched
-        # pack_form: PACK_TWO_SIDED, PACK_ONE_SIDED, or -1 = the library's default (xg_sched.h)
+        # pack_form: PACK_TWO_SIDED, PACK_ONE_SIDED, RELAY, RELAY_COALESCED, or -1 = the library's
+        # default (xg_sched.h)
         self._p = host().xg_devplan_build_form(sched.handle, ngpus, g, pack_max_seg, pack_min, pack_form)
         if not self._p:
             self._p = None
