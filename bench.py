@@ -668,6 +668,28 @@ CELL_TIERS = (tuple(f for f, _ in CELL_FORMS), tuple(f for f, _ in CELL_FORMS if
               ("direct",))
 
 
+def plan_signature(v):
+    """what a GPU's plan makes the device do, up to order inside a launch or an RCCL group and where
+    staged bytes sit in STAGE_SEND / STAGE_RECV: per step its stage / pre / post copies and the calls
+    of each group, as sorted lists (staging offsets left out).  Two forms with one signature on every
+    GPU are one plan to time."""
+    def cp(c):
+        return tuple(x if not (k in (1, 3) and c[k - 1] in (2, 3)) else -1 for k, x in enumerate(c))
+    out = []
+    for st in range(v.nsteps):
+        pb, pc, _qb, _qc, ob, oc = v.steps[st]
+        groups, cur = [], []
+        for kind, peer, buf, off, ln in v.calls(st):
+            if kind in (1, 2):
+                cur.append((kind, peer, buf, -1 if buf in (2, 3) else off, ln))
+            else:
+                groups.append(sorted(cur))
+                cur = [(kind, -1, -1, -1, 0)]
+        groups.append(sorted(cur))
+        out.append((sorted(map(cp, v.copies[pb:pb + pc])), sorted(map(cp, v.copies[ob:ob + oc])), groups))
+    return out
+
+
 def cell_estimate_s(links, link_gbps):
     """seconds a BASELINE cell's runs take at least: every form's verified run + FORM_REPS timed runs,
     each its busiest-link bytes at the per-link rate (0 when no rate was measured)"""
@@ -759,15 +781,21 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                 if (P, A, d) in no_room:
                     cells_out[key] = "skipped: this configuration's regions did not fit"
                     continue
-                err, no_alloc, differs = "", False, [0.0] * (len(CELL_FORMS) - 1)
+                nf = len(CELL_FORMS) - 1
+                err, no_alloc, differs, new_plan = "", False, [0.0] * nf, [0.0] * nf
                 try:
                     s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
                     # which forms change this GPU's plan (packing: lists of small segments; relay: a
-                    # permutation step with lists >= 1 MiB); MAX-reduced below, so all GPUs agree
+                    # permutation step with lists >= 1 MiB), and which of those are a plan no form
+                    # before them has (the coalesced form at configs[4]'s 64 MiB segments is the
+                    # relay form's plan); MAX-reduced below, so all GPUs agree
                     v0 = s.devplan(world, rank, 0, 0, -1)
+                    seen = [plan_signature(v0)]
                     for i, (_fname, f) in enumerate(CELL_FORMS[1:]):
-                        v = s.devplan(world, rank, f[0], 0, f[1])
-                        differs[i] = 1.0 if (v.copies, v.p2p) != (v0.copies, v0.p2p) else 0.0
+                        plan = plan_signature(s.devplan(world, rank, f[0], 0, f[1]))
+                        differs[i] = 1.0 if plan != seen[0] else 0.0
+                        new_plan[i] = 1.0 if plan not in seen else 0.0
+                        seen.append(plan)
                     if (P, A, d, c) not in needs:   # one allocation per configuration: all its methods, all forms
                         tiers = [[0] * xg.NBUF for _ in CELL_TIERS]
                         for mm in methods:
@@ -803,8 +831,10 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                         no_alloc = False
                 except xg.XGError as e:
                     err = str(e)
-                failed, unplaced, tier, *differs = ctx.allreduce_max(
-                    [1.0 if err else 0.0, 1.0 if no_alloc else 0.0, float(tier_of.get((P, A, d), 0))] + differs)
+                failed, unplaced, tier, *flags = ctx.allreduce_max(
+                    [1.0 if err else 0.0, 1.0 if no_alloc else 0.0, float(tier_of.get((P, A, d), 0))] + differs +
+                    new_plan)
+                differs, new_plan = flags[:nf], flags[nf:]
                 if failed:
                     cells_out[key] = "failed: %s" % (err or "on another GPU")
                     if unplaced:      # some GPU never got this configuration's regions: the rest would fail alike
@@ -812,7 +842,9 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                     continue
                 held = CELL_TIERS[int(tier)]
                 forms = dict(CELL_FORMS[:1])
-                forms.update((fname, f) for (fname, f), dif in zip(CELL_FORMS[1:], differs) if dif and fname in held)
+                forms.update((fname, f) for (fname, f), dif, nw in zip(CELL_FORMS[1:], differs, new_plan)
+                             if dif and nw and fname in held)
+                same = [fname for (fname, _f), dif, nw in zip(CELL_FORMS[1:], differs, new_plan) if dif and not nw]
                 dropped = [fname for (fname, _f), dif in zip(CELL_FORMS[1:], differs) if dif and fname not in held]
                 # the cell's runs at the measured link rate: a cell that would still be running when the
                 # phase's guard fires is skipped on every GPU alike (the cells after it may be shorter)
@@ -839,6 +871,9 @@ def baseline_configs_phase(xg, ctx, world, rank, budget, result, cells=BASELINE_
                 cell = dict(figs[best])
                 if dropped:
                     cell["forms_not_run"] = {f: "its staging did not fit beside the regions on some GPU" for f in dropped}
+                if same:
+                    cell.setdefault("forms_not_run", {}).update(
+                        (f, "the plan of a form before it, on every GPU") for f in same)
                 if len(figs) > 1:
                     cell["chosen"] = best
                     cell["forms"] = {k: (stats[k] if k in stats else str(v)) for k, v in figs.items()}

@@ -352,7 +352,8 @@ static void relay_calls(const xg_sched *s, const plan_bases *pb, const int *orde
  *            forwarded as it lies; and receives the same from p.
  * A call of one piece moves in place (send from the segment, receive into the slot); a longer one
  * is packed into STAGE_SEND in the step's pre launch and unpacked out of STAGE_RECV after the
- * exchange (HBM copies, two orders of magnitude above a link's rate).  STAGE_RECV holds the
+ * exchange (HBM copies, two orders of magnitude above a link's rate) -- unless its pieces average
+ * >= XG_COALESCE_SPLIT: then it goes one call per piece, in place (rc_split).  STAGE_RECV holds the
  * unpacked receives from 0 on (the layout the device displacement scan rebuilds) and the relayed
  * blocks behind them.  A pairwise round: G - 1 sends + G - 1 receives per group. */
 #define XG_WEIGHT_ONE 1024      /* a weighted step's shares: 1/1024ths of each GPU pair's bytes */
@@ -423,13 +424,21 @@ static int64_t rc_total(const rcx *x, int n)
 }
 
 /* send the n collected pieces to peer in group grp: in place, or packed into STAGE_SEND */
+/* a call of n pieces goes one call per piece, in place, when its pieces are large: at >= 4 MiB a
+ * piece an RCCL call (~3 us) costs less than packing and unpacking it (2 x its bytes of HBM traffic
+ * at ~5 TB/s each way: >= 3 us) -- configs[4]'s 64 MiB segments, whose pieces are 8 MiB.  Both ends
+ * of a call apply it to the same piece list, so the calls still pair one to one. */
+#define XG_COALESCE_SPLIT ((int64_t)4 << 20)
+static int rc_split(const rcx *x, int n) { return n > 1 && rc_total(x, n) >= XG_COALESCE_SPLIT * n; }
+
 static void rc_send(rcx *x, int n, int peer, int grp)
 {
     int64_t t = 0;
     int i;
     if (!n || x->dry) return;
-    if (n == 1) {
-        relay_push(x->pp, peer, 1, x->pm[0]->sbuf, src_off(x->pb, x->pm[0]) + x->po[0], x->pl[0], grp);
+    if (n == 1 || rc_split(x, n)) {
+        for (i = 0; i < n; ++i)
+            relay_push(x->pp, peer, 1, x->pm[i]->sbuf, src_off(x->pb, x->pm[i]) + x->po[i], x->pl[i], grp);
         return;
     }
     for (i = 0; i < n; ++i) {
@@ -450,8 +459,9 @@ static void rc_recv(rcx *x, int n, int peer, int grp)
     int64_t t = 0;
     int i;
     if (!n) return;
-    if (n == 1) {
-        if (!x->dry) relay_push(x->pp, peer, 0, x->pm[0]->dbuf, dst_off(x->pb, x->pm[0]) + x->po[0], x->pl[0], grp);
+    if (n == 1 || rc_split(x, n)) {
+        for (i = 0; i < n && !x->dry; ++i)
+            relay_push(x->pp, peer, 0, x->pm[i]->dbuf, dst_off(x->pb, x->pm[i]) + x->po[i], x->pl[i], grp);
         return;
     }
     for (i = 0; i < n && !x->dry; ++i) {
@@ -480,12 +490,18 @@ static void rc_step(rcx *x)
         if (n && !x->dry) {
             const int64_t at = x->rlbase + x->rl;
             int64_t t = 0;
-            for (b = 0; b < G; ++b) {
+            if (rc_split(x, n))         /* (or one per piece, as the sender splits them) */
+                for (b = 0; b < n; ++b) {
+                    relay_push(x->pp, p, 0, XG_BUF_STAGE_RECV, at + t, x->pl[b], 0);
+                    t += x->pl[b];
+                }
+            else
+                relay_push(x->pp, p, 0, XG_BUF_STAGE_RECV, at, rc_total(x, n), 0);
+            for (t = 0, b = 0; b < G; ++b) {
                 if (b == p || b == g) continue;
                 x->blk[p * G + b] = at + t;
                 t += rc_total(x, rc_collect(x, p, b, g));
             }
-            relay_push(x->pp, p, 0, XG_BUF_STAGE_RECV, at, t, 0);
             x->rl += t;
         }
     }
@@ -493,8 +509,14 @@ static void rc_step(rcx *x)
         if (p == g) continue;
         rc_send(x, rc_collect(x, g, p, g), p, 1);
         for (a = 0; a < G && !x->dry; ++a)
-            if (a != g && a != p && (n = rc_collect(x, a, p, g)))
-                relay_push(x->pp, p, 1, XG_BUF_STAGE_RECV, x->blk[a * G + p], rc_total(x, n), 1);
+            if (a != g && a != p && (n = rc_collect(x, a, p, g))) {
+                /* the block of a's pieces for p, as it lies (one call, or one per piece) */
+                int64_t at = x->blk[a * G + p];
+                if (rc_split(x, n))
+                    for (b = 0; b < n; at += x->pl[b], ++b) relay_push(x->pp, p, 1, XG_BUF_STAGE_RECV, at, x->pl[b], 1);
+                else
+                    relay_push(x->pp, p, 1, XG_BUF_STAGE_RECV, at, rc_total(x, n), 1);
+            }
         rc_recv(x, rc_collect(x, p, g, p), p, 1);
         for (a = 0; a < G; ++a)
             if (a != g && a != p) rc_recv(x, rc_collect(x, a, g, p), p, 1);

@@ -325,3 +325,21 @@ def test_relay_forms_under_every_step_form(xg, worlds, step_form):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("rccl", [False, True])
+def test_relay_forms_large_pieces(xg, worlds, rccl):
+    """P8 A4 -d (12 << 20) + 3 on 3 GPUs: pieces of 4 MiB and up, so the coalesced form's calls go one
+    per piece, in place, and its relayed pieces are received and forwarded piece by piece (rc_split,
+    as at configs[4]'s stated size) -- unordered, half-sync, pairwise, TAM; every slot byte-exact on
+    the device, sampled checksums against the oracle's closed form"""
+    import xg_oracle as O
+    P, A, d, it, G = 8, 4, (12 << 20) + 3, 1, 3
+    rl = xg.aggregator_list(P, A)
+    for method in (1, 7, 9, 12, 15):
+        s = xg.Schedule(method, P, A, d, 3, rl, ntimes=1, iteration=it)
+        for pack, form in RELAYS:
+            res = _run_job(xg, worlds[G], s, it, 1, pack, rccl=rccl, form=form)
+            assert res and all(nb == 0 for _slot, _ck, nb, _fb in res), (method, form, rccl)
+            for (src, seed, _dst, _off), ck, _nb, _fb in res[:: max(1, len(res) // 4)]:
+                assert ck == O.chk64(O.fingerprint(1, src, seed, it, d)), (method, form, src, seed)

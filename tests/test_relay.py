@@ -277,7 +277,8 @@ def test_weighted_split_of_configs4_m7(xg, c):
     split (devplan.c weighted_step, Frank-Wolfe) reroutes all 64 of its cross-GPU steps: each weighted
     step's busiest group-0 + group-1 links carry <= 0.85 of its busiest pair's bytes, the run 0.81 of
     the direct form's (4096 -> 3302 MiB; the LP optimum of two-hop routing is 0.78,
-    profiles/r05/relay_lp.txt); RCCL pairs every call, and no more calls than direct"""
+    profiles/r05/relay_lp.txt); RCCL pairs every call, within 10 % of direct's call count (a share of
+    >= 4 MiB a piece goes one call per piece, in place: rc_split)"""
     P, A, d, G = 256, 64, 8 << 20, 8
     s = xg.Schedule(7, P, A, d, c, xg.aggregator_list(P, A), ntimes=1)
     assert s.check_pairing(G, COALESCED[0], 0, COALESCED[1]) > 0
@@ -298,7 +299,7 @@ def test_weighted_split_of_configs4_m7(xg, c):
     assert weighted == 64 and tot_d == 4096 << 20 and tot_c <= 0.81 * tot_d, (weighted, tot_d >> 20, tot_c >> 20)
     for g in range(G):
         n = lambda v: sum(1 for st in range(v.nsteps) for x in v.calls(st) if x[0] in (SEND, RECV))
-        assert n(coal[g]) <= n(direct[g])
+        assert n(coal[g]) <= 1.1 * n(direct[g])
 
 
 def test_weighted_split_matches_the_python_frank_wolfe(xg):
@@ -382,3 +383,51 @@ def test_relay_forms_random_shapes(xg, P, A, G, d, c, m):
         assert s.check_pairing(G, form[0], 0, form[1]) >= 0
         _views, regs = simulate(s, G, it=1, mode=1, pack=form[0], form=form[1])
         check_recv(s, G, regs, it=1, mode=1)
+
+
+def test_coalesced_form_goes_in_place_for_large_pieces(xg):
+    """a coalesced call whose pieces average >= 4 MiB goes one call per piece, in place
+    (devplan.c rc_split): at configs[4]'s stated -d 64 MiB (8 MiB pieces) m11's coalesced plan posts
+    the relay form's calls in every step and group (bench.plan_signature: in another order, its
+    relayed pieces elsewhere in STAGE_RECV), with no pack or unpack; at -d 8 MiB (1 MiB pieces) it packs and
+    posts 4x fewer calls; RCCL pairs both"""
+    P, A, G = 256, 64, 8
+    rl = xg.aggregator_list(P, A)
+    for d, same in ((64 << 20, True), (8 << 20, False)):
+        s = xg.Schedule(11, P, A, d, 1, rl, ntimes=1)
+        assert s.check_pairing(G, COALESCED[0], 0, COALESCED[1]) > 0
+        for g in (0, 5):
+            r = s.devplan(G, g, RELAY[0], 0, RELAY[1])
+            c = s.devplan(G, g, COALESCED[0], 0, COALESCED[1])
+            calls = lambda v: [v.calls(st) for st in range(v.nsteps)]
+            if same:         # the same calls in every step and group, up to where a relay keeps its pieces
+                import bench
+                assert bench.plan_signature(c) == bench.plan_signature(r)
+                assert not [x for x in c.copies if x[2] == 2 or x[0] == 3]
+            else:
+                n = lambda v: sum(1 for cs in calls(v) for x in cs if x[0] in (SEND, RECV))
+                assert 4 * n(c) <= n(r) and [x for x in c.copies if x[2] == 2]
+
+
+def test_relay_forms_with_large_pieces_deliver_every_byte(xg):
+    """P8 A4 -d (12 << 20) + 3 on 3 GPUs (pieces of 4 MiB and up: the coalesced form's calls go one
+    per piece, in place, its relayed pieces received and forwarded piece by piece -- rc_split -- as at
+    configs[4]'s stated size): unordered, half-sync, pairwise, TAM; every byte where the reference
+    puts it"""
+    P, A, d, G = 8, 4, (12 << 20) + 3, 3
+    rl = xg.aggregator_list(P, A)
+    n = 0
+    for m in (1, 7, 9, 12, 15):
+        try:
+            s = xg.Schedule(m, P, A, d, 3, rl, ntimes=1, iteration=1)
+        except xg.XGError:
+            continue
+        for form in (RELAY, COALESCED):
+            v = s.devplan(G, 0, form[0], 0, form[1])
+            if not any(FENCE in [x[0] for x in v.calls(st)] for st in range(v.nsteps)):
+                continue
+            n += 1
+            assert s.check_pairing(G, form[0], 0, form[1]) > 0
+            _views, regs = simulate(s, G, it=1, mode=1, pack=form[0], form=form[1])
+            check_recv(s, G, regs, it=1, mode=1)
+    assert n >= 7, n
