@@ -423,7 +423,6 @@ static int64_t rc_total(const rcx *x, int n)
     return t;
 }
 
-/* send the n collected pieces to peer in group grp: in place, or packed into STAGE_SEND */
 /* a call of n pieces goes one call per piece, in place, when its pieces are large: at >= 4 MiB a
  * piece an RCCL call (~3 us) costs less than packing and unpacking it (2 x its bytes of HBM traffic
  * at ~5 TB/s each way: >= 3 us) -- configs[4]'s 64 MiB segments, whose pieces are 8 MiB.  Both ends
@@ -431,6 +430,7 @@ static int64_t rc_total(const rcx *x, int n)
 #define XG_COALESCE_SPLIT ((int64_t)4 << 20)
 static int rc_split(const rcx *x, int n) { return n > 1 && rc_total(x, n) >= XG_COALESCE_SPLIT * n; }
 
+/* send the n collected pieces to peer in group grp: in place, or packed into STAGE_SEND */
 static void rc_send(rcx *x, int n, int peer, int grp)
 {
     int64_t t = 0;
