@@ -562,10 +562,55 @@ static double fw_cost(int G, int np, const int *pr, const double *y, double *l0,
     return m0 + m1;
 }
 
+/* The split is a pure function of the step's GPU-pair matrix, and every GPU's plan (each rank
+ * builds all G of them for the pairing proof) asks for the same steps: a per-thread memo of the last
+ * XG_FW_MEMO matrices (G <= 8), matched on the exact matrix, answers the repeats. */
+#define XG_FW_MEMO 256
+typedef struct { int G, rc; uint64_t key; double D[64]; int w[512]; } fw_memo;
+static __thread fw_memo *fw_memo_tab;
+static __thread unsigned fw_memo_next;
+
+static uint64_t fw_key(const double *D, int n)
+{
+    uint64_t hsh = 1469598103934665603ull;
+    int i;
+    for (i = 0; i < n; ++i) {
+        uint64_t v;
+        memcpy(&v, &D[i], sizeof v);
+        hsh = (hsh ^ v) * 1099511628211ull;
+    }
+    return hsh;
+}
+
+/* the memo entry of matrix D (G x G), or NULL */
+static const fw_memo *fw_memo_find(const double *D, int G, uint64_t key)
+{
+    unsigned i;
+    if (!fw_memo_tab || G > 8) return NULL;
+    for (i = 0; i < XG_FW_MEMO; ++i)
+        if (fw_memo_tab[i].G == G && fw_memo_tab[i].key == key &&
+            !memcmp(fw_memo_tab[i].D, D, sizeof(double) * (size_t)G * G))
+            return &fw_memo_tab[i];
+    return NULL;
+}
+
+static void fw_memo_put(const double *D, int G, uint64_t key, const int *w, int rc)
+{
+    fw_memo *m;
+    if (G > 8) return;
+    if (!fw_memo_tab && !(fw_memo_tab = (fw_memo *)calloc(XG_FW_MEMO, sizeof(fw_memo)))) return;
+    m = &fw_memo_tab[fw_memo_next++ % XG_FW_MEMO];
+    m->G = G; m->rc = rc; m->key = key;
+    memcpy(m->D, D, sizeof(double) * (size_t)G * G);
+    memcpy(m->w, w, sizeof(int) * (size_t)G * G * G);
+}
+
 /* The weighted split of step [b, e) into w[(a * G + b) * G + h] (1/XG_WEIGHT_ONE) -> 1 when the
  * step is to be weighted, 0 when it stays direct, -1 out of host memory */
 static int weighted_step(const xg_sched *s, const int *order, int b, int e, int G, int *w)
 {
+    uint64_t key = 0;
+    const fw_memo *hit;
     int k, i, h, np = 0, t, rc = -1;
     double direct = 0, best = -1, cost;
     double *D = (double *)calloc((size_t)G * G, sizeof(double));
@@ -593,6 +638,12 @@ static int weighted_step(const xg_sched *s, const int *order, int b, int e, int 
         }
     }
     if (!np) goto done;
+    key = fw_key(D, G * G);
+    if ((hit = fw_memo_find(D, G, key))) {
+        memcpy(w, hit->w, sizeof(int) * (size_t)G * G * G);
+        rc = hit->rc;
+        goto done;
+    }
     for (t = 0; t <= XG_FW_ITERS; ++t) {
         double m0 = 0, m1 = 0, z0 = 0, z1 = 0, beta;
         cost = fw_cost(G, np, pr, y, l0, l1);
@@ -606,11 +657,16 @@ static int weighted_step(const xg_sched *s, const int *order, int b, int e, int 
             m1 = l1[k] > m1 ? l1[k] : m1;
         }
         beta = XG_FW_SHARP / cost;
-        for (k = 0; k < G * G; ++k) {
-            g0[k] = exp(beta * (l0[k] - m0));
-            g1[k] = exp(beta * (l1[k] - m1));
+        for (k = 0; k < G * G; ++k) {       /* links far below the busiest weigh nothing (< e^-30) */
+            const double e0 = beta * (l0[k] - m0), e1 = beta * (l1[k] - m1);
+            g0[k] = e0 > -30.0 ? exp(e0) : 0.0;
+            g1[k] = e1 > -30.0 ? exp(e1) : 0.0;
             z0 += g0[k];
             z1 += g1[k];
+        }
+        for (k = 0, z0 = 1.0 / z0, z1 = 1.0 / z1; k < G * G; ++k) {     /* soft-max weights */
+            g0[k] *= z0;
+            g1[k] *= z1;
         }
         for (i = 0; i < np; ++i) {
             const int a = pr[2 * i], bb = pr[2 * i + 1];
@@ -618,7 +674,7 @@ static int weighted_step(const xg_sched *s, const int *order, int b, int e, int 
             int arg = 0;
             double cmin = 0;
             for (h = 0; h < G; ++h) {
-                const double c = (h != a ? g0[a * G + h] / z0 : 0.0) + (h != bb ? g1[h * G + bb] / z1 : 0.0);
+                const double c = (h != a ? g0[a * G + h] : 0.0) + (h != bb ? g1[h * G + bb] : 0.0);
                 if (h == 0 || c < cmin) { cmin = c; arg = h; }
             }
             for (h = 0; h < G; ++h) y[(size_t)i * G + h] += step * ((h == arg ? dem : 0.0) - y[(size_t)i * G + h]);
@@ -639,6 +695,7 @@ static int weighted_step(const xg_sched *s, const int *order, int b, int e, int 
         for (h = 0; h < G; ++h) yb[(size_t)i * G + h] = D[a * G + bb] * wp[h] / XG_WEIGHT_ONE;
     }
     rc = fw_cost(G, np, pr, yb, l0, l1) <= XG_WEIGHTED_GAIN * direct;
+    fw_memo_put(D, G, key, w, rc);
 done:
     free(D); free(pr); free(y); free(yb); free(l0); free(l1); free(g0); free(g1);
     return rc;

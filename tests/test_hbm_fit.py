@@ -22,7 +22,8 @@ def test_per_gpu_regions_fit_288gb(xg, case):
     for m in methods:
         for c in cs:
             s = xg.Schedule(m, P, A, d, c, rl, ntimes=1)
-            for pack, form in ((0, -1), (4 << 20, -1), (0, 2), (0, 3)):   # direct, packed, relay, coalesced
+            # direct, packed, relay, coalesced (the coalesced form at the sweep's ends: suite time)
+            for pack, form in ((0, -1), (4 << 20, -1), (0, 2)) + (((0, 3),) if c in (1, 8, 200000000) else ()):
                 tot = 0
                 for g in range(8):
                     v = s.devplan(8, g, pack, 0, form)

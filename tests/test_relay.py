@@ -14,8 +14,8 @@ DIRECT, RELAY, COALESCED = (0, -1), (0, 2), (0, 3)
 SEND, RECV, BARRIER, FENCE = 1, 2, 3, 4
 
 
-@pytest.mark.parametrize("form", [RELAY, COALESCED])
-@pytest.mark.parametrize("G, d", [(3, 1 << 20), (4, (1 << 20) + 48), (8, (1 << 20) + 3), (8, 1 << 20)])
+@pytest.mark.parametrize("G, d, form", [(3, 1 << 20, RELAY), (4, (1 << 20) + 48, RELAY), (8, (1 << 20) + 3, RELAY),
+                                        (3, 1 << 20, COALESCED), (8, (1 << 20) + 3, COALESCED)])
 def test_relay_plans_deliver_every_byte(xg, G, d, form):
     """P16 A8 (lists of >= 1 MiB per XOR round at every G), every method the relay form changes,
     collision-free fingerprint; 16-B aligned cuts of an unaligned -d ((1 << 20) + 3) included.
@@ -367,7 +367,7 @@ def _random_shapes(seed, n):
     return out
 
 
-@pytest.mark.parametrize("P, A, G, d, c, m", _random_shapes(2026, 40))
+@pytest.mark.parametrize("P, A, G, d, c, m", _random_shapes(2026, 6))    # 450 more: profiles/r06/relay_random.py
 def test_relay_forms_random_shapes(xg, P, A, G, d, c, m):
     """random shapes (P 6-40, A 1-16, G 3-8, -d 1-2 MiB aligned and not, -c 1-8 / default, methods
     1-20): both relay forms (uniform cuts, coalesced calls, weighted splits) deliver every byte
@@ -412,12 +412,12 @@ def test_coalesced_form_goes_in_place_for_large_pieces(xg):
 def test_relay_forms_with_large_pieces_deliver_every_byte(xg):
     """P8 A4 -d (12 << 20) + 3 on 3 GPUs (pieces of 4 MiB and up: the coalesced form's calls go one
     per piece, in place, its relayed pieces received and forwarded piece by piece -- rc_split -- as at
-    configs[4]'s stated size): unordered, half-sync, pairwise, TAM; every byte where the reference
-    puts it"""
+    configs[4]'s stated size): half-sync and pairwise; every byte where the reference puts it (the
+    GPU test runs unordered and TAM too)"""
     P, A, d, G = 8, 4, (12 << 20) + 3, 3
     rl = xg.aggregator_list(P, A)
     n = 0
-    for m in (1, 7, 9, 12, 15):
+    for m in (7, 9, 12):
         try:
             s = xg.Schedule(m, P, A, d, 3, rl, ntimes=1, iteration=1)
         except xg.XGError:
@@ -430,4 +430,4 @@ def test_relay_forms_with_large_pieces_deliver_every_byte(xg):
             assert s.check_pairing(G, form[0], 0, form[1]) > 0
             _views, regs = simulate(s, G, it=1, mode=1, pack=form[0], form=form[1])
             check_recv(s, G, regs, it=1, mode=1)
-    assert n >= 7, n
+    assert n >= 4, n
