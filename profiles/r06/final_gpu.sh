@@ -2,7 +2,7 @@
 # Round 6 check: the driver's three commands (-m gpu suite, smoke, bench), then the bench
 # under rocprofv3 (kernel trace + stats, csv) and the two PMC passes (profiles/bench_rocprof.sh).
 set -o pipefail
-out=gpurun_out/r06_final
+out=${OUT:-gpurun_out/r06_final}
 mkdir -p $out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread --durations=25 > $out/gpu_tests.log 2>&1
 rc=$?; echo "gpu tests rc=$rc"; grep -E "passed|failed" $out/gpu_tests.log | tail -1; [ $rc -eq 0 ] || exit $rc
