@@ -1,11 +1,17 @@
 #!/usr/bin/env python3
 """Round 6: seeded random shapes (tests/test_relay.py _random_shapes) through both relay forms on the CPU executor:
 pairing proof, race check, every byte against the oracle.  usage: relay_random.py <seed> <shapes>"""
-import sys; sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/tests"); sys.path.insert(0, "/root/repo/oracle")
-import __graft_entry__ as G
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+for p in (REPO, os.path.join(REPO, "tests"), os.path.join(REPO, "oracle")):
+    sys.path.insert(0, p)
+import __graft_entry__ as G  # noqa: E402
+from plan_exec import check_recv, simulate  # noqa: E402  (CPU executor: test infrastructure)
+from test_relay import _random_shapes  # noqa: E402
+
 xg = G.load_package().xg
-from plan_exec import simulate, check_recv
-from test_relay import _random_shapes
 seed, n = int(sys.argv[1]), int(sys.argv[2])
 runs = fenced = refused = 0
 for P, A, Gn, d, c, m in _random_shapes(seed, n):
