@@ -71,14 +71,17 @@ ARGS = ["-m", 0, "-a", 3, "-d", 3000, "--procs", 7, "--verify"]
 
 @pytest.mark.parametrize("G", [2, 3, 4])
 @pytest.mark.parametrize("variant", ["default", "pack_all", "pack_one_sided", "strong_k3", "barrier_k2", "no_self",
-                                     "all_self"])
+                                     "all_self", "relay_1m", "coalesced_1m"])
 def test_every_method_verifies_on_n_processes(exes, tmp_path, G, variant):
     """-m 0 (all 20 methods) as G processes: every received byte right, the same report lines as
     the one-process run (numbers aside)."""
     extra, env = {"default": ([], {}), "pack_all": (["--pack-min", 0], {}),
                   "pack_one_sided": (["--pack-min", 0, "--pack-form", 1], {}),
                   "strong_k3": (["--fingerprint", "strong", "-k", 3], {}), "barrier_k2": (["-b", 1, "-k", 2], {}),
-                  "no_self": ([], {"XG_SELF_MAX": 0}), "all_self": ([], {"XG_SELF_MAX": 1 << 30})}[variant]
+                  "no_self": ([], {"XG_SELF_MAX": 0}), "all_self": ([], {"XG_SELF_MAX": 1 << 30}),
+                  # the relay forms (--pack-form 2 / 3) at an odd -d past 1 MiB, where they reroute steps
+                  "relay_1m": (["--pack-form", 2, "-d", (1 << 20) + 3], {}),
+                  "coalesced_1m": (["--pack-form", 3, "-d", (1 << 20) + 3], {})}[variant]
     p = _run(exes["test"], ARGS + extra + ["--gpus", G], tmp_path, **env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     ok = [ln for ln in p.stdout.splitlines() if "verify = OK" in ln]
