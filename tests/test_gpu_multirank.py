@@ -210,6 +210,20 @@ def test_cli_readme_config_as_multi_rank_job(tmp_path, G):
     assert _masked(out) == _masked(one)
 
 
+@pytest.mark.parametrize("form", [2, 3])
+def test_cli_relay_forms_as_four_rank_job(tmp_path, form):
+    """bin/test --gpus 4 --pack-form 2 / 3 (the relay and coalesced relay forms, through the drop-in
+    CLI) at an odd -d past 1 MiB, where they reroute steps: every method 1-20 byte-verified on the
+    device, the report identical in form to the one-process run's"""
+    args = ["--procs", 12, "-a", 5, "-d", (1 << 20) + 3, "-c", 3, "-m", 0, "-i", 1, "-k", 1, "--verify",
+            "--pack-form", form]
+    out = _cli(args, tmp_path, 4)
+    assert out.count("verify = OK") == 20 and "FAILED" not in out, out[-2000:]
+    (tmp_path / "one").mkdir()
+    one = _cli(args, tmp_path / "one", 1)
+    assert _masked(out) == _masked(one)
+
+
 def test_pt2pt_as_two_rank_job(tmp_path):
     """bin/pt2pt_test as two processes (the reference's pt2pt_test runs under mpiexec -n 2): rank
     1's Issend to rank 0 as an RCCL send between two communicator ranks; the output masked equals
