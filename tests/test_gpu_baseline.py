@@ -10,8 +10,8 @@
 2. test_config3_full_size_virtual8 / test_config4_d8m_virtual8: every byte of the 8-GPU plans
    of configs[3] (P256 A32 -d 4 MiB, m1 / m2 / m9 / m10) and configs[4] (P256 A64, m7 / m11 /
    m12, -c 1..8, at -d 8 MiB: 256 GiB for the 8 GPUs' regions) moved on the device as an 8-GPU
-   job, verified slot by slot (collision-free fingerprint) -- configs[4]'s m11 / m12 in the relay
-   form too (profiles/r06/relay_c4.log).
+   job, verified slot by slot (collision-free fingerprint) -- configs[4]'s m11 / m12 in both relay
+   forms too, m7 in the coalesced form's weighted split (profiles/r06/relay_c4.log, split_tests.log).
 3. test_config4_stated_size_gpu0_share: configs[4] at its stated -d 64 MiB, GPU 0's share of the
    8-GPU job (256 GiB of regions) run alone, every -c.
 Reference: mpi_test.c:1748-1950 (m1 / m2), :421-597 (m9 / m10), :942-1114 (m11 / m12 / m7).
@@ -92,11 +92,11 @@ def _run_job(xg, ctxs, s, it, mode, pack, form, rccl, regions=None):
 @pytest.mark.parametrize("cfg", baseline_configs())
 def test_baseline_virtual8_rccl(xg, world8, cfg):
     """every capture as an 8-GPU job over RCCL in every form; at configs[1]'s full size (1 MiB
-    segments) the relay form reroutes m9 / m10's cross-GPU XOR rounds (and the steps of other
-    methods its link model favours) over every link -- the reference's checksums still hold"""
+    segments) the relay forms reroute m9 / m10's cross-GPU XOR rounds (and the steps of other
+    methods their link model favours) over every link -- the reference's checksums still hold"""
     meta, _, data = load_baseline(cfg)
     it = meta["iters"] - 1
-    forms = PACKINGS + (((0, 2),) if meta["d"] >= 1 << 20 else ())
+    forms = PACKINGS + (((0, 2), (0, 3)) if meta["d"] >= 1 << 20 else ())
     for method in meta["method_list"]:
         s = _sched(xg, meta, method, it)
         for pack, form in forms:
@@ -169,18 +169,20 @@ def _relayed_steps(xg, s, G, form):
     return sum(1 for st in range(v.nsteps) if any(k == xg.CALL_FENCE for k, *_ in v.calls(st)))
 
 
-def test_config4_d8m_virtual8(xg, world8):
+@pytest.mark.parametrize("cs", [(1, 2, 3, 4), (5, 6, 7, 8)], ids=["c1-4", "c5-8"])
+def test_config4_d8m_virtual8(xg, world8, cs):
     """configs[4] (P256 A64, m7 / m11 / m12) at -d 8 MiB -- 16 GiB of SEND + 16 GiB of RECV per
     GPU, 256 GiB for the job -- as an 8-GPU job at every -c in 1..8 (device copies in RCCL's
-    pairing), and through RCCL itself at -c 1 and -c 8; regions allocated once per GPU.  m11 / m12
-    also in the relay form (XG_RELAY) and the coalesced relay form (XG_RELAY_COALESCED), the forms
-    the N = 8 BASELINE phase times beside direct on exactly these plans (profiles/r05/link_load.txt):
-    every -c through copies (the coalesced form at -c 1 and 8), -c 1 and 8 through RCCL.  m7, which
-    no uniform cut helps, runs in the coalesced form's weighted two-hop split (every step).  m7's plan is the same in both forms (no step gains), so it runs direct only."""
+    pairing), and through RCCL itself at -c 1 and -c 8; regions allocated once per GPU and half of
+    the sweep.  m11 / m12 also in the relay form (XG_RELAY) and the coalesced relay form
+    (XG_RELAY_COALESCED), the forms the N = 8 BASELINE phase times beside direct on exactly these
+    plans (profiles/r05/link_load.txt): every -c through copies (the coalesced form at -c 1 and 8),
+    -c 1 and 8 through RCCL.  m7, which no uniform cut helps, runs in the coalesced form's weighted
+    two-hop split (every step) at -c 1 and 8."""
     P, A, d, it = 256, 64, 8 << 20, 1
     rl = xg.aggregator_list(P, A)
     scheds = {(m, c): xg.Schedule(m, P, A, d, c, rl, ntimes=1, iteration=it) for m in (7, 11, 12)
-              for c in range(1, 9)}
+              for c in cs}
     pack = (4 << 20, -1)              # the default: 8 MiB segments are never packed
     relay, coal = (0, 2), (0, 3)
     regions = _shared_regions(xg, world8, list(scheds.values()), (pack, relay, coal))
