@@ -650,7 +650,11 @@ def link_rate(out):
 # (name, P, A, d, -c, methods): configs[2], configs[3], configs[4] at their stated sizes, and
 # configs[3] / [4] at the reduced -d (4 KiB) the reference runs at on the host (CPU_CELLS: the same keys),
 # ahead of configs[4]'s stated-size cells, which take most of the phase's budget
-BASELINE_CELLS = ([("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
+BASELINE_CELLS = ([  # first a link-level probe of two-hop routing: one rank per GPU, pairwise m9, so every XOR
+                   # round is a permutation of 16 MiB messages on one link each direct, on every link
+                   # relayed (busiest-link bytes 112 -> 28 MiB); not a BASELINE config, ~1 s
+                   ("two-hop probe P8 A8 -d 16 MiB", 8, 8, 16 << 20, 200000000, (9,)),
+                   ("configs[2]", 64, 16, 256 << 10, 200000000, (5, 8)),
                    ("configs[3]", 256, 32, 4 << 20, 200000000, (1, 2, 9, 10)),
                    ("configs[3] at -d 4 KiB", 256, 32, 4 << 10, 200000000, (1, 2, 9, 10))] +
                   [("configs[4] -c %d at -d 4 KiB" % c, 256, 64, 4 << 10, c, (7, 11, 12)) for c in (1, 8)] +

@@ -236,7 +236,8 @@ def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
     assert out["value"] > 0 and out["xgmi"]["peak"] > 0
     ex = out["baseline_configs_8gpu"]
     cells = ex["cells"]
-    want = ["configs[2] m5", "configs[2] m8"] + ["configs[3] m%d" % m for m in (1, 2, 9, 10)] + \
+    want = ["two-hop probe P8 A8 -d 16 MiB m9", "configs[2] m5", "configs[2] m8"] + \
+           ["configs[3] m%d" % m for m in (1, 2, 9, 10)] + \
            ["configs[3] at -d 4 KiB m%d" % m for m in (1, 2, 9, 10)] + \
            ["configs[4] -c %d at -d 4 KiB m%d" % (c, m) for c in (1, 8) for m in (7, 11, 12)] + \
            ["configs[4] -c %d m%d" % (c, m) for c in (1, 8, 2, 3, 4, 5, 6, 7) for m in (7, 11, 12)]
@@ -246,10 +247,11 @@ def test_bench_runs_the_8gpu_baseline_configs_after_the_line(tmp_path):
     def failed(v):       # one form: its failure; several: every form's failure under "forms"
         return str(v).startswith("failed") or (isinstance(v, dict) and "verified" not in v and
                                                 all(str(x).startswith("failed") for x in v["forms"].values()))
-    assert failed(cells["configs[3] m9"]) and failed(cells["configs[3] at -d 4 KiB m9"])
+    m9 = ("two-hop probe P8 A8 -d 16 MiB m9", "configs[3] m9", "configs[3] at -d 4 KiB m9")
+    assert all(failed(cells[k]) for k in m9)
     assert "injected" in str(out["rccl_log_tail"]) or out.get("rccl_log_tail") is None
     for k, v in cells.items():
-        if k not in ("configs[3] m9", "configs[3] at -d 4 KiB m9"):
+        if k not in m9:
             assert v["verified"] and v["ms_per_run"] > 0 and v["GBps_cross_gpu"] > 0, (k, v)
             # FORM_REPS timed runs of the chosen form, its median the figure; the bytes its calls put
             # on the links beside the logical payload (a relayed byte crosses two links)
@@ -275,7 +277,7 @@ def test_bench_baseline_configs_phase_keeps_to_its_budget(tmp_path):
     assert rcs == [0, 0], [o[1][-1500:] for o in outs]
     out = json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][0])
     cells = out["baseline_configs_8gpu"]["cells"]
-    assert len(cells) == 2 + 4 + 4 + 6 + 24 and all(str(v).startswith("skipped: phase budget") for v in cells.values())
+    assert len(cells) == 1 + 2 + 4 + 4 + 6 + 24 and all(str(v).startswith("skipped: phase budget") for v in cells.values())
 
 
 def test_bench_baseline_configs_phase_skips_a_configuration_that_does_not_fit(tmp_path):
